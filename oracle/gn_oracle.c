@@ -1,0 +1,494 @@
+/*
+ * gn_oracle.c — CPU restatement of the reference's backend Gauss-Newton path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / CPU
+ * baseline. The product path (mast3r-slam-ysh_amd/) never links or calls it.
+ *
+ * What it restates (all citations relative to /root/reference):
+ *   - per-edge residual + Jacobian + 14x14 Hessian accumulation
+ *       rays   mast3r_slam/backend/src/gn_kernels.cu:813-1138
+ *       calib  mast3r_slam/backend/src/gn_kernels.cu:1231-1543
+ *       points mast3r_slam/backend/src/gn_kernels.cu:455-723
+ *     including the reference's summation order: 256 "threads", pixel k goes
+ *     to thread k % 256 (GPU_1D_KERNEL_LOOP :31-32), then the shared-memory
+ *     tree 128,64,32,...,1 (blockReduce :36-55), with float accumulators and
+ *     the reference's double-promoted literals (1.0/x, 1.345, 2.0*...).
+ *   - Sim3 helpers: huber :172-175, quat :177-193, actSO3/actSim3 :195-219,
+ *     relSim3 :252-272, adjoint-transpose :274-297, Exp/retraction :299-453.
+ *   - host loop: unique+searchsorted remap :161-170, num_fix = 1 (:1157),
+ *     block assembly of Hs[4,E,7,7]/gs[2,E,7] into the (N-1)*7 system with
+ *     negative (fixed) indices dropped and duplicates summed (:57-113,
+ *     :1199-1206), fp64 LLT (Eigen SimplicialLLT :132-153; dense here, the
+ *     factor is unique so only roundoff differs), failure => dx = 0,
+ *     dx = -solve (:1209), retraction (:1212), ||dx|| < delta => stop
+ *     (:1219-1222).
+ *
+ * Parity pinning: no reference test holds golden vectors for this path
+ * (SURVEY.md §4, §8c). The restatement is pinned by (i) the reference's own
+ * tracker code run on identical inputs (tests/golden/, one-step
+ * tracker<->backend equivalence), and (ii) the kernel's
+ * bitwise self-symmetry Hs[0]==Hs[3], gs[0]==-gs[1].
+ *
+ * Build: see oracle/Makefile (gcc, OpenMP over edges).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NTHR 256 /* the reference's THREADS (gn_kernels.cu:28) */
+#define TRI 105  /* 14*15/2 */
+
+enum { MODE_POINTS = 0, MODE_RAYS = 1, MODE_CALIB = 2 };
+
+typedef struct {
+  int mode;
+  float sigma_a;  /* points: sigma_point; rays: sigma_ray;  calib: sigma_pixel */
+  float sigma_b;  /* rays: sigma_dist; calib: sigma_depth */
+  float C_thresh, Q_thresh;
+  /* calib only */
+  float fx, fy, cx, cy;
+  int height, width, pixel_border;
+  float z_eps;
+} params_t;
+
+/* ---------------------------------------------------------------- Sim3 -- */
+
+static float robust_w(float r) {
+  const float a = fabsf(r);
+  return a < 1.345 ? 1.0 : 1.345 / a;
+}
+
+static void qmul(const float *a, const float *b, float *o) {
+  float r[4];
+  r[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+  r[1] = a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0];
+  r[2] = a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3];
+  r[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+  memcpy(o, r, sizeof r);
+}
+
+static void qrot(const float *q, const float *X, float *Y) {
+  float u[3], out[3];
+  u[0] = 2.0 * (q[1] * X[2] - q[2] * X[1]);
+  u[1] = 2.0 * (q[2] * X[0] - q[0] * X[2]);
+  u[2] = 2.0 * (q[0] * X[1] - q[1] * X[0]);
+  out[0] = X[0] + q[3] * u[0] + (q[1] * u[2] - q[2] * u[1]);
+  out[1] = X[1] + q[3] * u[1] + (q[2] * u[0] - q[0] * u[2]);
+  out[2] = X[2] + q[3] * u[2] + (q[0] * u[1] - q[1] * u[0]);
+  memcpy(Y, out, sizeof out);
+}
+
+/* T = [t(3) q(4) s] ; Y = s R X + t */
+static void act(const float *T, const float *X, float *Y) {
+  qrot(T + 3, X, Y);
+  for (int c = 0; c < 3; c++) Y[c] = Y[c] * T[7] + T[c];
+}
+
+/* T_ij = T_i^-1 T_j */
+static void relative(const float *Ti, const float *Tj, float *Tij) {
+  const float inv_si = 1.0 / Ti[7];
+  const float qi_c[4] = {-Ti[3], -Ti[4], -Ti[5], Ti[6]};
+  float d[3];
+  Tij[7] = inv_si * Tj[7];
+  qmul(qi_c, Tj + 3, Tij + 3);
+  for (int c = 0; c < 3; c++) d[c] = Tj[c] - Ti[c];
+  qrot(qi_c, d, d);
+  for (int c = 0; c < 3; c++) Tij[c] = d[c] * inv_si;
+}
+
+/* out = Adj(T_i)^-T applied to a tangent row vector a = [tau, phi, sigma] */
+static void adjT_inv(const float *Ti, const float *a, float *out) {
+  const float *t = Ti, *q = Ti + 3;
+  const float inv_s = 1.0 / Ti[7];
+  float Ra[3], Rb[3];
+  qrot(q, a, Ra);
+  qrot(q, a + 3, Rb);
+  out[0] = inv_s * Ra[0];
+  out[1] = inv_s * Ra[1];
+  out[2] = inv_s * Ra[2];
+  out[3] = Rb[0] + inv_s * (t[1] * Ra[2] - t[2] * Ra[1]);
+  out[4] = Rb[1] + inv_s * (t[2] * Ra[0] - t[0] * Ra[2]);
+  out[5] = Rb[2] + inv_s * (t[0] * Ra[1] - t[1] * Ra[0]);
+  out[6] = a[6] + inv_s * (t[0] * Ra[0] + t[1] * Ra[1] + t[2] * Ra[2]);
+}
+
+static void cross_left(const float *a, float *b) { /* b <- a x b */
+  float x0 = a[1] * b[2] - a[2] * b[1];
+  float x1 = a[2] * b[0] - a[0] * b[2];
+  float x2 = a[0] * b[1] - a[1] * b[0];
+  b[0] = x0, b[1] = x1, b[2] = x2;
+}
+
+static void exp_sim3(const float *xi, float *t, float *q, float *s) {
+  const double EPSV = 1e-6;
+  float tau[3] = {xi[0], xi[1], xi[2]};
+  const float phi[3] = {xi[3], xi[4], xi[5]};
+  const float sigma = xi[6];
+  const float scale = expf(sigma);
+  float th2 = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  /* SO3 part: Taylor when theta^2 < EPS */
+  float im, re;
+  if (th2 < EPSV) {
+    float th4 = th2 * th2;
+    im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
+    re = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
+  } else {
+    float th = sqrtf(th2);
+    im = sinf(0.5 * th) / th;
+    re = cosf(0.5 * th);
+  }
+  q[0] = im * phi[0];
+  q[1] = im * phi[1];
+  q[2] = im * phi[2];
+  q[3] = re;
+  s[0] = scale;
+  /* translation: W tau with W = C I + A Phi + B Phi^2 */
+  float th = sqrtf(th2);
+  float A, B, C;
+  const float one = 1.0, half = 0.5;
+  if (fabs(sigma) < EPSV) {
+    C = one;
+    if (fabs(th) < EPSV) {
+      A = half;
+      B = 1.0 / 6.0;
+    } else {
+      A = (one - cosf(th)) / th2;
+      B = (th - sinf(th)) / (th2 * th);
+    }
+  } else {
+    C = (scale - one) / sigma;
+    if (fabs(th) < EPSV) {
+      float sg2 = sigma * sigma;
+      A = ((sigma - one) * scale + one) / sg2;
+      B = (scale * half * sg2 + scale - one - sigma * scale) / (sg2 * sigma);
+    } else {
+      float a = scale * sinf(th), b = scale * cosf(th), c = th2 + sigma * sigma;
+      A = (a * sigma + (one - b) * th) / (th * c);
+      B = (C - ((b - one) * sigma + a * th) / c) / th2;
+    }
+  }
+  t[0] = C * tau[0];
+  t[1] = C * tau[1];
+  t[2] = C * tau[2];
+  cross_left(phi, tau);
+  t[0] += A * tau[0];
+  t[1] += A * tau[1];
+  t[2] += A * tau[2];
+  cross_left(phi, tau);
+  t[0] += B * tau[0];
+  t[1] += B * tau[1];
+  t[2] += B * tau[2];
+}
+
+/* T <- Exp(xi) * T */
+static void retract(const float *xi, float *T) {
+  float dt[3], dq[4], ds, q1[4], t1[3];
+  exp_sim3(xi, dt, dq, &ds);
+  qmul(dq, T + 3, q1);
+  qrot(dq, T, t1);
+  for (int c = 0; c < 3; c++) t1[c] = t1[c] * ds + dt[c];
+  memcpy(T, t1, sizeof t1);
+  memcpy(T + 3, q1, sizeof q1);
+  T[7] = ds * T[7];
+}
+
+/* ------------------------------------------------------ residual rows -- */
+/* Fill up to 4 local Jacobian rows J[r][7], errors e[r] and weights w[r]
+ * for one (edge, pixel). Returns the row count. */
+static int rows_for_pixel(const params_t *P, const float *Tij, const float *Xi, const float *Xj,
+                          int64_t id_i, float q, float ci, float cj, int vmatch, float J[4][7],
+                          float e[4], float w[4]) {
+  float Y[3];
+  act(Tij, Xj, Y);
+  const int ok_conf = vmatch & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh);
+  if (P->mode == MODE_POINTS) {
+    const float inv_sig = 1.0 / P->sigma_a;
+    const float sw = ok_conf ? inv_sig * sqrtf(q) : 0;
+    const float w2 = sw * sw;
+    for (int c = 0; c < 3; c++) {
+      e[c] = Y[c] - Xi[c];
+      w[c] = robust_w(sw * e[c]) * w2;
+    }
+    const float rows[3][7] = {{1.0, 0.0, 0.0, 0.0, Y[2], -Y[1], Y[0]},
+                              {0.0, 1.0, 0.0, -Y[2], 0, Y[0], Y[1]},
+                              {0.0, 0.0, 1.0, Y[1], -Y[0], 0, Y[2]}};
+    memcpy(J, rows, sizeof rows);
+    return 3;
+  }
+  if (P->mode == MODE_RAYS) {
+    const float ni2 = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
+    const float ni = sqrtf(ni2);
+    const float ni_inv = 1.0 / ni;
+    float ri[3];
+    for (int c = 0; c < 3; c++) ri[c] = ni_inv * Xi[c];
+    const float nj2 = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
+    const float nj = sqrtf(nj2);
+    const float nj_inv = 1.0 / nj;
+    float rj[3];
+    for (int c = 0; c < 3; c++) rj[c] = nj_inv * Y[c];
+    for (int c = 0; c < 3; c++) e[c] = rj[c] - ri[c];
+    e[3] = nj - ni;
+    const float inv_ray = 1.0 / P->sigma_a, inv_dist = 1.0 / P->sigma_b;
+    const float sw_r = ok_conf ? inv_ray * sqrtf(q) : 0;
+    const float sw_d = ok_conf ? inv_dist * sqrtf(q) : 0;
+    for (int c = 0; c < 3; c++) w[c] = robust_w(sw_r * e[c]);
+    w[3] = robust_w(sw_d * e[3]);
+    const float k_r = sw_r * sw_r, k_d = sw_d * sw_d;
+    for (int c = 0; c < 3; c++) w[c] *= k_r;
+    w[3] *= k_d;
+    const float n3 = nj_inv / nj2;
+    const float dxx = nj_inv - Y[0] * Y[0] * n3, dyy = nj_inv - Y[1] * Y[1] * n3,
+                dzz = nj_inv - Y[2] * Y[2] * n3;
+    const float dxy = -Y[0] * Y[1] * n3, dxz = -Y[0] * Y[2] * n3, dyz = -Y[1] * Y[2] * n3;
+    const float rows[4][7] = {{dxx, dxy, dxz, 0.0, rj[2], -rj[1], 0.0},
+                              {dxy, dyy, dyz, -rj[2], 0.0, rj[0], 0.0},
+                              {dxz, dyz, dzz, rj[1], -rj[0], 0.0, 0.0},
+                              {rj[0], rj[1], rj[2], 0.0, 0.0, 0.0, nj}};
+    memcpy(J, rows, sizeof rows);
+    return 4;
+  }
+  /* MODE_CALIB */
+  const int u_t = (int)(id_i % P->width), v_t = (int)(id_i / P->width);
+  const int vz = (Y[2] > P->z_eps) && (Xi[2] > P->z_eps);
+  const float zinv = vz ? 1.0 / Y[2] : 0.0;
+  const float lzj = vz ? logf(Y[2]) : 0.0;
+  const float lzi = vz ? logf(Xi[2]) : 0.0;
+  const float x = Y[0] * zinv, y = Y[1] * zinv;
+  const float u = P->fx * x + P->cx, v = P->fy * y + P->cy;
+  const int vu = (u > P->pixel_border) && (u < P->width - 1 - P->pixel_border);
+  const int vv = (v > P->pixel_border) && (v < P->height - 1 - P->pixel_border);
+  e[0] = u - u_t;
+  e[1] = v - v_t;
+  e[2] = lzj - lzi;
+  const int ok = ok_conf & vu & vv & vz;
+  const float inv_pix = 1.0 / P->sigma_a, inv_dep = 1.0 / P->sigma_b;
+  const float sw_p = ok ? inv_pix * sqrtf(q) : 0;
+  const float sw_z = ok ? inv_dep * sqrtf(q) : 0;
+  w[0] = robust_w(sw_p * e[0]);
+  w[1] = robust_w(sw_p * e[1]);
+  w[2] = robust_w(sw_z * e[2]);
+  const float k_p = sw_p * sw_p, k_z = sw_z * sw_z;
+  w[0] *= k_p;
+  w[1] *= k_p;
+  w[2] *= k_z;
+  const float fx = P->fx, fy = P->fy;
+  const float rows[3][7] = {
+      {fx * zinv, 0.0, -fx * x * zinv, -fx * x * y, fx * (1 + x * x), -fx * y, 0.0},
+      {0.0, fy * zinv, -fy * y * zinv, -fy * (1 + y * y), fy * x * y, fy * x, 0.0},
+      {0.0, 0.0, zinv, y, -x, 0.0, 1.0}};
+  memcpy(J, rows, sizeof rows);
+  return 3;
+}
+
+/* ---------------------------------------------------------- edge pass -- */
+/* Hs: [4][E][7][7], gs: [2][E][7]; ranks ix/jx index Twc/Xs/Cs. */
+static void edge_blocks(const params_t *P, const float *Twc, const float *Xs, const float *Cs,
+                        int HW, int e, int ix, int jx, const int64_t *idx, const uint8_t *valid,
+                        const float *Q, int E, float *Hs, float *gs) {
+  float *acc = (float *)calloc((size_t)NTHR * (TRI + 14), sizeof(float));
+  float Tij[8];
+  relative(Twc + 8 * ix, Twc + 8 * jx, Tij);
+  const float *Ti = Twc + 8 * ix;
+  const float *Xs_i = Xs + (size_t)ix * HW * 3, *Xs_j = Xs + (size_t)jx * HW * 3;
+  const float *Cs_i = Cs + (size_t)ix * HW, *Cs_j = Cs + (size_t)jx * HW;
+  for (int k = 0; k < HW; k++) {
+    float *h = acc + (size_t)(k % NTHR) * (TRI + 14);
+    float *vi = h + TRI, *vj = h + TRI + 7;
+    const size_t ek = (size_t)e * HW + k;
+    const int vm = valid[ek] != 0;
+    const int64_t id = vm ? idx[ek] : 0;
+    float J[4][7], err[4], w[4];
+    const int nr = rows_for_pixel(P, Tij, Xs_i + 3 * id, Xs_j + 3 * (size_t)k, id, Q[ek],
+                                  Cs_i[id], Cs_j[k], vm, J, err, w);
+    for (int r = 0; r < nr; r++) {
+      float Jx[14];
+      adjT_inv(Ti, J[r], Jx + 7);
+      for (int n = 0; n < 7; n++) Jx[n] = -Jx[7 + n];
+      int l = 0;
+      for (int n = 0; n < 14; n++)
+        for (int m = 0; m <= n; m++, l++) h[l] += w[r] * Jx[n] * Jx[m];
+      for (int n = 0; n < 7; n++) {
+        vi[n] += w[r] * err[r] * Jx[n];
+        vj[n] += w[r] * err[r] * Jx[7 + n];
+      }
+    }
+  }
+  /* shared-memory tree, entry by entry (blockReduce) */
+  for (int stride = NTHR / 2; stride >= 1; stride >>= 1)
+    for (int t = 0; t < stride; t++) {
+      float *a = acc + (size_t)t * (TRI + 14), *b = acc + (size_t)(t + stride) * (TRI + 14);
+      for (int x = 0; x < TRI + 14; x++) a[x] += b[x];
+    }
+  const float *h = acc, *vi = acc + TRI, *vj = acc + TRI + 7;
+  for (int n = 0; n < 7; n++) {
+    gs[(size_t)(0 * E + e) * 7 + n] = vi[n];
+    gs[(size_t)(1 * E + e) * 7 + n] = vj[n];
+  }
+#define HS(b, r, c) Hs[(((size_t)(b)*E + e) * 7 + (r)) * 7 + (c)]
+  int l = 0;
+  for (int n = 0; n < 14; n++)
+    for (int m = 0; m <= n; m++, l++) {
+      const float val = h[l];
+      if (n < 7) {
+        HS(0, n, m) = val;
+        HS(0, m, n) = val;
+      } else if (m < 7) {
+        HS(1, m, n - 7) = val;
+        HS(2, n - 7, m) = val;
+      } else {
+        HS(3, n - 7, m - 7) = val;
+        HS(3, m - 7, n - 7) = val;
+      }
+    }
+#undef HS
+  free(acc);
+}
+
+/* ---------------------------------------------------------- remapping -- */
+static int cmp_i64(const void *a, const void *b) {
+  int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+  return (x > y) - (x < y);
+}
+
+/* rank of each ii/jj in sorted-unique(cat(ii,jj)); returns #unique */
+static int remap(const int64_t *ii, const int64_t *jj, int E, int *ri, int *rj) {
+  int64_t *u = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(E > 0 ? E : 1));
+  memcpy(u, ii, sizeof(int64_t) * E);
+  memcpy(u + E, jj, sizeof(int64_t) * E);
+  qsort(u, 2 * (size_t)E, sizeof(int64_t), cmp_i64);
+  int n = 0;
+  for (int k = 0; k < 2 * E; k++)
+    if (n == 0 || u[n - 1] != u[k]) u[n++] = u[k];
+  for (int e = 0; e < E; e++) {
+    int64_t *p = (int64_t *)bsearch(&ii[e], u, n, sizeof(int64_t), cmp_i64);
+    int64_t *q = (int64_t *)bsearch(&jj[e], u, n, sizeof(int64_t), cmp_i64);
+    ri[e] = (int)(p - u);
+    rj[e] = (int)(q - u);
+  }
+  free(u);
+  return n;
+}
+
+/* dense fp64 LLT of A (n x n, row-major, lower used), in place; 0 = ok */
+static int llt(double *A, int n) {
+  for (int k = 0; k < n; k++) {
+    double d = A[(size_t)k * n + k];
+    for (int p = 0; p < k; p++) d -= A[(size_t)k * n + p] * A[(size_t)k * n + p];
+    if (!(d > 0.0)) return 1;
+    d = sqrt(d);
+    A[(size_t)k * n + k] = d;
+    for (int i = k + 1; i < n; i++) {
+      double s = A[(size_t)i * n + k];
+      for (int p = 0; p < k; p++) s -= A[(size_t)i * n + p] * A[(size_t)k * n + p];
+      A[(size_t)i * n + k] = s / d;
+    }
+  }
+  return 0;
+}
+
+static void llt_solve(const double *L, int n, double *b) {
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int p = 0; p < i; p++) s -= L[(size_t)i * n + p] * b[p];
+    b[i] = s / L[(size_t)i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = b[i];
+    for (int p = i + 1; p < n; p++) s -= L[(size_t)p * n + i] * b[p];
+    b[i] = s / L[(size_t)i * n + i];
+  }
+}
+
+/* ------------------------------------------------------------ exports -- */
+
+/* One linearisation: Hs/gs for every directed edge at the current poses.
+ * Returns 0, or -1 if an edge references a rank >= N. */
+int oracle_edge_blocks(const params_t *P, const float *Twc, const float *Xs, const float *Cs,
+                       int N, int HW, const int64_t *ii, const int64_t *jj, int E,
+                       const int64_t *idx, const uint8_t *valid, const float *Q, float *Hs,
+                       float *gs) {
+  int *ri = (int *)malloc(sizeof(int) * (E > 0 ? E : 1));
+  int *rj = (int *)malloc(sizeof(int) * (E > 0 ? E : 1));
+  remap(ii, jj, E, ri, rj);
+  for (int e = 0; e < E; e++)
+    if (ri[e] >= N || rj[e] >= N) {
+      free(ri), free(rj);
+      return -1;
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int e = 0; e < E; e++)
+    edge_blocks(P, Twc, Xs, Cs, HW, e, ri[e], rj[e], idx, valid, Q, E, Hs, gs);
+  free(ri), free(rj);
+  return 0;
+}
+
+/* Full backend GN (gauss_newton_{points,rays,calib}_cuda). Twc is updated in
+ * place; dx_out [N-1][7] receives the last step. Returns the number of
+ * iterations run (>=0), or -1 on invalid input. *solve_failed counts
+ * iterations whose LLT failed (dx = 0 then, exactly as the reference). */
+int oracle_gn(const params_t *P, float *Twc, const float *Xs, const float *Cs, int N, int HW,
+              const int64_t *ii, const int64_t *jj, int E, const int64_t *idx,
+              const uint8_t *valid, const float *Q, int max_iter, float delta_thresh,
+              float *dx_out, int *solve_failed) {
+  if (N < 1) return -1;
+  const int M = 7, nv = N - 1, n = nv * M;
+  int *ri = (int *)malloc(sizeof(int) * (E > 0 ? E : 1));
+  int *rj = (int *)malloc(sizeof(int) * (E > 0 ? E : 1));
+  remap(ii, jj, E, ri, rj);
+  for (int e = 0; e < E; e++)
+    if (ri[e] >= N || rj[e] >= N) {
+      free(ri), free(rj);
+      return -1;
+    }
+  float *Hs = (float *)calloc((size_t)4 * E * 49 + 1, sizeof(float));
+  float *gs = (float *)calloc((size_t)2 * E * 7 + 1, sizeof(float));
+  double *A = (double *)malloc(sizeof(double) * ((size_t)n * n + 1));
+  double *b = (double *)malloc(sizeof(double) * ((size_t)n + 1));
+  int it = 0;
+  if (solve_failed) *solve_failed = 0;
+  for (it = 0; it < max_iter;) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int e = 0; e < E; e++)
+      edge_blocks(P, Twc, Xs, Cs, HW, e, ri[e], rj[e], idx, valid, Q, E, Hs, gs);
+    memset(A, 0, sizeof(double) * (size_t)n * n);
+    memset(b, 0, sizeof(double) * (size_t)n);
+    for (int blk = 0; blk < 4; blk++)
+      for (int e = 0; e < E; e++) {
+        const int r = ((blk < 2) ? ri[e] : rj[e]) - 1; /* cat(ii,ii,jj,jj) */
+        const int c = ((blk % 2 == 0) ? ri[e] : rj[e]) - 1; /* cat(ii,jj,ii,jj) */
+        if (r < 0 || c < 0) continue;
+        for (int a = 0; a < M; a++)
+          for (int d = 0; d < M; d++)
+            A[(size_t)(r * M + a) * n + c * M + d] +=
+                (double)Hs[(((size_t)blk * E + e) * 7 + a) * 7 + d];
+      }
+    for (int blk = 0; blk < 2; blk++)
+      for (int e = 0; e < E; e++) {
+        const int r = ((blk == 0) ? ri[e] : rj[e]) - 1;
+        if (r < 0) continue;
+        for (int a = 0; a < M; a++) b[r * M + a] += (double)gs[((size_t)blk * E + e) * 7 + a];
+      }
+    const int fail = (n == 0) ? 0 : llt(A, n);
+    if (fail) {
+      if (solve_failed) (*solve_failed)++;
+      for (int k = 0; k < n; k++) dx_out[k] = 0.0f;
+    } else {
+      llt_solve(A, n, b);
+      for (int k = 0; k < n; k++) dx_out[k] = -(float)b[k];
+    }
+    for (int k = 1; k < N; k++) retract(dx_out + (size_t)(k - 1) * M, Twc + 8 * (size_t)k);
+    it++;
+    float nrm2 = 0.0f;
+    for (int k = 0; k < n; k++) nrm2 += dx_out[k] * dx_out[k];
+    if (sqrtf(nrm2) < delta_thresh) break;
+  }
+  free(Hs), free(gs), free(A), free(b), free(ri), free(rj);
+  return it;
+}
+
+/* exposed Sim3 helpers (for cross-checks of the device Sim3 code) */
+void oracle_retract(const float *xi, float *T) { retract(xi, T); }
+void oracle_relative(const float *Ti, const float *Tj, float *Tij) { relative(Ti, Tj, Tij); }
+void oracle_adjT_inv(const float *Ti, const float *a, float *out) { adjT_inv(Ti, a, out); }

@@ -1,0 +1,151 @@
+/*
+ * m3s_gn.h — C ABI of the MI355X Gauss-Newton backend for MASt3R-SLAM.
+ *
+ * Drop-in for the reference's `mast3r_slam_backends` GN entry points
+ * (pybind module, /root/reference/mast3r_slam/backend/src/gn.cpp:116-122,
+ * declarations gn.h:11-80). Everything here is plain C: device pointers,
+ * sizes, a hipStream_t passed as `void *`, an int status. No torch types.
+ *
+ * Layouts are exactly the reference's tensors (all contiguous, device memory):
+ *   Twc        float  [N, 8]      t(3) q(xyzw) s      — updated IN PLACE
+ *   Xs         float  [N, HW, 3]  canonical pointmaps (rank order)
+ *   Cs         float  [N, HW]     (the reference's [N, HW, 1]) average conf
+ *   ii, jj     int64  [E]         global keyframe ids of each directed edge
+ *   idx_ii2jj  int64  [E, HW]     pixel of KF ii matched to pixel k of KF jj
+ *   valid_match uint8 [E, HW]     (torch.bool, [E, HW, 1] in the reference)
+ *   Q          float  [E, HW]     match quality
+ *   K          float  [3, 3]      calib only
+ * ii/jj are remapped on device to ranks in sorted-unique(cat(ii, jj)) as the
+ * reference does (gn_kernels.cu:161-170); pose rank 0 is held fixed
+ * (num_fix = 1, gn_kernels.cu:1157).
+ *
+ * All launches are asynchronous on `stream`; the calls never synchronise the
+ * host and never allocate (the caller passes a workspace of
+ * m3s_gn_workspace_size() bytes, 256-byte aligned). Device-side outcomes
+ * (iterations run, solve failures, invalid edge ids) land in `info`.
+ */
+#ifndef M3S_GN_H
+#define M3S_GN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes (host side) */
+#define M3S_OK 0
+#define M3S_EINVAL 1     /* bad sizes / null pointers / workspace too small */
+#define M3S_ELAUNCH 2    /* a HIP launch failed */
+#define M3S_ETOOLARGE 3  /* problem size beyond this build's limits */
+
+/* residual models (gn_kernels.cu kernels) */
+#define M3S_MODE_POINTS 0 /* point_align_kernel  :455-723  */
+#define M3S_MODE_RAYS 1   /* ray_align_kernel    :813-1138 */
+#define M3S_MODE_CALIB 2  /* calib_proj_kernel   :1231-1543 */
+
+/* device-side info block, int32[8], written by the GN launches */
+#define M3S_INFO_ITERS 0        /* GN iterations executed                     */
+#define M3S_INFO_SOLVE_FAIL 1   /* iterations whose LLT failed (dx = 0 then)   */
+#define M3S_INFO_BAD_EDGE 2     /* 1 if an edge id maps to a rank >= N         */
+#define M3S_INFO_CONVERGED 3    /* 1 if ||dx|| < delta_thresh stopped the loop */
+#define M3S_INFO_N_UNIQUE 4     /* number of unique keyframe ids in ii/jj      */
+
+typedef struct m3s_gn_args {
+  float *Twc;
+  const float *Xs;
+  const float *Cs;
+  const int64_t *ii;
+  const int64_t *jj;
+  const int64_t *idx_ii2jj;
+  const uint8_t *valid_match;
+  const float *Q;
+  const float *K; /* calib only, else NULL */
+  int64_t N, HW, E;
+  int mode;
+  /* residual parameters: points: sigma_a = sigma_point
+   *                      rays:   sigma_a = sigma_ray,   sigma_b = sigma_dist
+   *                      calib:  sigma_a = sigma_pixel, sigma_b = sigma_depth */
+  float sigma_a, sigma_b;
+  float C_thresh, Q_thresh;
+  int height, width, pixel_border; /* calib */
+  float z_eps;                     /* calib */
+  int max_iter;
+  float delta_thresh;
+  float *dx_out;  /* [N-1, 7] float: the last GN step (the reference's return) */
+  int32_t *info;  /* [8] int32 device */
+  void *workspace;
+  size_t workspace_bytes;
+} m3s_gn_args;
+
+/* Bytes of scratch the GN entry points need for this problem size. */
+size_t m3s_gn_workspace_size(int64_t N, int64_t HW, int64_t E);
+
+/* Replaces gauss_newton_points (gn.cpp:3-27 -> gn_kernels.cu:725-811). */
+int m3s_gauss_newton_points(const m3s_gn_args *a, void *stream);
+/* Replaces gauss_newton_rays   (gn.cpp:29-54 -> gn_kernels.cu:1140-1228). */
+int m3s_gauss_newton_rays(const m3s_gn_args *a, void *stream);
+/* Replaces gauss_newton_calib  (gn.cpp:56-85 -> gn_kernels.cu:1546-1638). */
+int m3s_gauss_newton_calib(const m3s_gn_args *a, void *stream);
+
+/* ---- stepwise API (edge-sharded multi-GPU path; same math as above) ----
+ * m3s_gn_prepare:   remap ii/jj -> ranks, zero info/flags.
+ * m3s_gn_linearize: per-edge local normal equations for edges
+ *                   [edge_begin, edge_end) into edge_sums (double[E_loc][36]:
+ *                   28 upper-triangular J^T W J, 7 J^T W r, 1 cost, in the
+ *                   frame of the residual).
+ * m3s_gn_solve:     given edge_sums for ALL E edges: assemble the
+ *                   (N-1)*7 system, fp64 LLT, dx = -H^-1 g, retract Twc, update
+ *                   info/convergence flag. Iterations after convergence are
+ *                   skipped on device. */
+int m3s_gn_prepare(const m3s_gn_args *a, void *stream);
+int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end,
+                     double *edge_sums, void *stream);
+int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream);
+#define M3S_EDGE_SUM_STRIDE 36
+
+/* ---- tracker (new entry points; the reference tracker is pure PyTorch,
+ *      tracker.py:173-266) ----
+ * Frame -> keyframe relative Sim(3) GN with the reference's convergence rule
+ * (nonlinear_optimizer.py:5-25). Inputs are the tensors opt_pose_* receive:
+ *   Xf [HW,3] (frame points gathered by idx_f2k), Xk [HW,3], Qk [HW],
+ *   valid [HW] uint8, T_WCf / T_WCk [8]; calib additionally K [3,3] and the
+ *   image size (meas_k is formed on device from the pixel grid and Xk).
+ * Outputs: T_WCf_out [8], T_CkCf_out [8], info [8] (ITERS, SOLVE_FAIL=1 if
+ * the Cholesky failed — the reference raises, tracker.py:91-93). */
+typedef struct m3s_track_args {
+  const float *Xf;
+  const float *Xk;
+  const float *Qk;
+  const uint8_t *valid;
+  const float *T_WCf;
+  const float *T_WCk;
+  const float *K; /* calib only */
+  int64_t HW;
+  int height, width, pixel_border;
+  float z_eps;
+  float sigma_a, sigma_b; /* (sigma_ray, sigma_dist) or (sigma_pixel, sigma_depth) */
+  float huber_k;          /* config tracking.huber (1.345) */
+  int max_iters;
+  float rel_error, delta_norm;
+  int sync_every; /* 0: launch all max_iters (device-side early exit);
+                     k>0: read the convergence flag every k iterations */
+  float *T_WCf_out;
+  float *T_CkCf_out;
+  int32_t *info;
+  void *workspace;
+  size_t workspace_bytes;
+} m3s_track_args;
+
+size_t m3s_track_workspace_size(int64_t HW);
+int m3s_track_rays_sim3(const m3s_track_args *a, void *stream);
+int m3s_track_calib_sim3(const m3s_track_args *a, void *stream);
+
+/* build identification (for the loaded-library check) */
+const char *m3s_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* M3S_GN_H */

@@ -1,0 +1,342 @@
+// m3s_device.h — device helpers for the MI355X GN path: Sim(3) algebra,
+// residual-row builders, packed normal-equation accumulation.
+//
+// Sim(3) algebra follows the reference's CUDA helpers (lietorch semantics):
+//   quaternion xyzw product / rotation  gn_kernels.cu:177-205
+//   relative pose T_i^-1 T_j            gn_kernels.cu:252-272
+//   Exp / left retraction               gn_kernels.cu:299-413
+// The Jacobian design differs from the reference on purpose: the reference
+// builds the 14-wide [J_i, J_j] row per pixel and accumulates the 105-entry
+// upper triangle of [J_i J_j]^T W [J_i J_j] (gn_kernels.cu:990-1089). Since
+// J_j = M(T_i) J_local and J_i = -J_j exactly (:999-1000), every block of the
+// 14x14 matrix is +-M L M^T with L = sum w J_local J_local^T. We accumulate
+// only L (28 entries, and only the structurally non-zero ones per row) and
+// the 7-vector l = sum w e J_local, and apply M once per edge in fp64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace m3s {
+
+constexpr int kNP = 36;  // per-edge partial: 28 (upper-tri L) + 7 (l) + 1 (cost)
+constexpr int kL = 0, kG = 28, kCost = 35;
+
+// packed upper-triangular index of (m, n), m <= n < 7
+__host__ __device__ constexpr int tri(int m, int n) { return m * 7 - (m * (m - 1)) / 2 + (n - m); }
+
+// ------------------------------------------------------------------ Sim3 --
+struct Sim3f {
+  float t[3];
+  float q[4];  // x y z w
+  float s;
+};
+
+__device__ __forceinline__ Sim3f load_sim3(const float *p) {
+  Sim3f T;
+  T.t[0] = p[0], T.t[1] = p[1], T.t[2] = p[2];
+  T.q[0] = p[3], T.q[1] = p[4], T.q[2] = p[5], T.q[3] = p[6];
+  T.s = p[7];
+  return T;
+}
+
+__device__ __forceinline__ void store_sim3(float *p, const Sim3f &T) {
+  p[0] = T.t[0], p[1] = T.t[1], p[2] = T.t[2];
+  p[3] = T.q[0], p[4] = T.q[1], p[5] = T.q[2], p[6] = T.q[3];
+  p[7] = T.s;
+}
+
+__device__ __forceinline__ void quat_mul(const float *a, const float *b, float *o) {
+  const float x = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+  const float y = a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0];
+  const float z = a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3];
+  const float w = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+  o[0] = x, o[1] = y, o[2] = z, o[3] = w;
+}
+
+// R(q) X = X + 2w (v x X) + v x (2 v x X)
+__device__ __forceinline__ void quat_rot(const float *q, const float *X, float *Y) {
+  const float ux = 2.0f * (q[1] * X[2] - q[2] * X[1]);
+  const float uy = 2.0f * (q[2] * X[0] - q[0] * X[2]);
+  const float uz = 2.0f * (q[0] * X[1] - q[1] * X[0]);
+  const float y0 = X[0] + q[3] * ux + (q[1] * uz - q[2] * uy);
+  const float y1 = X[1] + q[3] * uy + (q[2] * ux - q[0] * uz);
+  const float y2 = X[2] + q[3] * uz + (q[0] * uy - q[1] * ux);
+  Y[0] = y0, Y[1] = y1, Y[2] = y2;
+}
+
+__device__ __forceinline__ void act(const Sim3f &T, const float *X, float *Y) {
+  quat_rot(T.q, X, Y);
+  Y[0] = Y[0] * T.s + T.t[0];
+  Y[1] = Y[1] * T.s + T.t[1];
+  Y[2] = Y[2] * T.s + T.t[2];
+}
+
+__device__ __forceinline__ Sim3f inverse(const Sim3f &T) {
+  Sim3f R;
+  R.q[0] = -T.q[0], R.q[1] = -T.q[1], R.q[2] = -T.q[2], R.q[3] = T.q[3];
+  R.s = 1.0f / T.s;
+  float d[3];
+  quat_rot(R.q, T.t, d);
+  R.t[0] = -R.s * d[0], R.t[1] = -R.s * d[1], R.t[2] = -R.s * d[2];
+  return R;
+}
+
+// A * B
+__device__ __forceinline__ Sim3f compose(const Sim3f &A, const Sim3f &B) {
+  Sim3f C;
+  quat_mul(A.q, B.q, C.q);
+  float d[3];
+  quat_rot(A.q, B.t, d);
+  C.t[0] = A.t[0] + A.s * d[0];
+  C.t[1] = A.t[1] + A.s * d[1];
+  C.t[2] = A.t[2] + A.s * d[2];
+  C.s = A.s * B.s;
+  return C;
+}
+
+// T_i^-1 T_j  (relSim3, gn_kernels.cu:252-272)
+__device__ __forceinline__ Sim3f relative(const Sim3f &Ti, const Sim3f &Tj) {
+  Sim3f R;
+  const float inv_si = 1.0f / Ti.s;
+  const float qc[4] = {-Ti.q[0], -Ti.q[1], -Ti.q[2], Ti.q[3]};
+  R.s = inv_si * Tj.s;
+  quat_mul(qc, Tj.q, R.q);
+  float d[3] = {Tj.t[0] - Ti.t[0], Tj.t[1] - Ti.t[1], Tj.t[2] - Ti.t[2]};
+  quat_rot(qc, d, d);
+  R.t[0] = d[0] * inv_si, R.t[1] = d[1] * inv_si, R.t[2] = d[2] * inv_si;
+  return R;
+}
+
+// Exp: tangent [tau, phi, sigma] -> Sim3 (lietorch RxSO3 W, gn_kernels.cu:299-390)
+__device__ inline Sim3f exp_sim3(const float *xi) {
+  const float EPSV = 1e-6f;
+  Sim3f E;
+  const float tau[3] = {xi[0], xi[1], xi[2]};
+  const float phi[3] = {xi[3], xi[4], xi[5]};
+  const float sg = xi[6];
+  const float scale = expf(sg);
+  const float th2 = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  float im, re;
+  if (th2 < EPSV) {
+    const float th4 = th2 * th2;
+    im = 0.5f - (1.0f / 48.0f) * th2 + (1.0f / 3840.0f) * th4;
+    re = 1.0f - (1.0f / 8.0f) * th2 + (1.0f / 384.0f) * th4;
+  } else {
+    const float th = sqrtf(th2);
+    im = sinf(0.5f * th) / th;
+    re = cosf(0.5f * th);
+  }
+  E.q[0] = im * phi[0], E.q[1] = im * phi[1], E.q[2] = im * phi[2], E.q[3] = re;
+  E.s = scale;
+  const float th = sqrtf(th2);
+  float A, B, C;
+  if (fabsf(sg) < EPSV) {
+    C = 1.0f;
+    if (th < EPSV) {
+      A = 0.5f;
+      B = 1.0f / 6.0f;
+    } else {
+      A = (1.0f - cosf(th)) / th2;
+      B = (th - sinf(th)) / (th2 * th);
+    }
+  } else {
+    C = (scale - 1.0f) / sg;
+    if (th < EPSV) {
+      const float sg2 = sg * sg;
+      A = ((sg - 1.0f) * scale + 1.0f) / sg2;
+      B = (scale * 0.5f * sg2 + scale - 1.0f - sg * scale) / (sg2 * sg);
+    } else {
+      const float a = scale * sinf(th), b = scale * cosf(th), c = th2 + sg * sg;
+      A = (a * sg + (1.0f - b) * th) / (th * c);
+      B = (C - ((b - 1.0f) * sg + a * th) / c) / th2;
+    }
+  }
+  // W tau = C tau + A phi x tau + B phi x (phi x tau)
+  const float p1[3] = {phi[1] * tau[2] - phi[2] * tau[1], phi[2] * tau[0] - phi[0] * tau[2],
+                       phi[0] * tau[1] - phi[1] * tau[0]};
+  const float p2[3] = {phi[1] * p1[2] - phi[2] * p1[1], phi[2] * p1[0] - phi[0] * p1[2],
+                       phi[0] * p1[1] - phi[1] * p1[0]};
+  for (int c = 0; c < 3; c++) E.t[c] = C * tau[c] + A * p1[c] + B * p2[c];
+  return E;
+}
+
+// T <- Exp(xi) T  (retrSim3 / pose_retr_kernel, gn_kernels.cu:392-453)
+__device__ inline Sim3f retract(const float *xi, const Sim3f &T) { return compose(exp_sim3(xi), T); }
+
+// M = Adj(T_i)^-T as a dense 7x7 (double), so that J_j = M J_local
+// (apply_Sim3_adj_inv, gn_kernels.cu:274-297):
+//   [ s^-1 R          0   0 ]
+//   [ s^-1 [t]x R     R   0 ]
+//   [ s^-1 t^T R      0   1 ]
+__device__ inline void adjT_inv_matrix(const float *Tp, double M[7][7]) {
+  const double tx = Tp[0], ty = Tp[1], tz = Tp[2];
+  const double qx = Tp[3], qy = Tp[4], qz = Tp[5], qw = Tp[6];
+  const double is = 1.0 / (double)Tp[7];
+  // rotation matrix of the (not renormalised) quaternion, matching actSO3's
+  // formula X + 2w(v x X) + v x (2 v x X) applied to unit vectors
+  double R[3][3];
+  R[0][0] = 1.0 - 2.0 * (qy * qy + qz * qz);
+  R[0][1] = 2.0 * (qx * qy - qw * qz);
+  R[0][2] = 2.0 * (qx * qz + qw * qy);
+  R[1][0] = 2.0 * (qx * qy + qw * qz);
+  R[1][1] = 1.0 - 2.0 * (qx * qx + qz * qz);
+  R[1][2] = 2.0 * (qy * qz - qw * qx);
+  R[2][0] = 2.0 * (qx * qz - qw * qy);
+  R[2][1] = 2.0 * (qy * qz + qw * qx);
+  R[2][2] = 1.0 - 2.0 * (qx * qx + qy * qy);
+  for (int r = 0; r < 7; r++)
+    for (int c = 0; c < 7; c++) M[r][c] = 0.0;
+  const double t[3] = {tx, ty, tz};
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      M[r][c] = is * R[r][c];
+      M[3 + r][3 + c] = R[r][c];
+    }
+  // [t]x R
+  for (int c = 0; c < 3; c++) {
+    M[3][c] = is * (t[1] * R[2][c] - t[2] * R[1][c]);
+    M[4][c] = is * (t[2] * R[0][c] - t[0] * R[2][c]);
+    M[5][c] = is * (t[0] * R[1][c] - t[1] * R[0][c]);
+    M[6][c] = is * (t[0] * R[0][c] + t[1] * R[1][c] + t[2] * R[2][c]);
+  }
+  M[6][6] = 1.0;
+}
+
+// ----------------------------------------------------- fast scalar math --
+// One-ulp hardware ops for the per-pixel path (v_rcp_f32 / v_sqrt_f32 /
+// v_log_f32); the reference uses correctly rounded double-promoted forms —
+// the difference is below the fp32 summation noise (DESIGN.md tolerances).
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float flog(float x) { return __logf(x); }
+
+__device__ __forceinline__ float huber_w(float r, float k) {
+  const float a = fabsf(r);
+  return a < k ? 1.0f : k * frcp(a);
+}
+
+// ------------------------------------------------ normal-eq accumulation --
+// acc[tri(m,n)] += w a_m a_n over the structurally non-zero entries (MASK),
+// acc[kG+m] += (w e) a_m, acc[kCost] += w e^2.
+template <unsigned MASK>
+__device__ __forceinline__ void accum_row(float *acc, const float (&a)[7], float w, float e) {
+  float wa[7];
+#pragma unroll
+  for (int m = 0; m < 7; m++)
+    if (MASK & (1u << m)) wa[m] = w * a[m];
+#pragma unroll
+  for (int m = 0; m < 7; m++) {
+    if (!(MASK & (1u << m))) continue;
+#pragma unroll
+    for (int n = m; n < 7; n++)
+      if (MASK & (1u << n)) acc[kL + tri(m, n)] += wa[m] * a[n];
+  }
+  const float we = w * e;
+#pragma unroll
+  for (int m = 0; m < 7; m++)
+    if (MASK & (1u << m)) acc[kG + m] += we * a[m];
+  acc[kCost] += we * e;
+}
+
+// non-zero patterns of the local Jacobian rows (bits: tau0..2 phi0..2 sigma)
+constexpr unsigned kRayX = 0x37, kRayY = 0x2F, kRayZ = 0x1F, kRayD = 0x47;
+constexpr unsigned kCalU = 0x3D, kCalV = 0x3E, kCalZ = 0x5C;
+constexpr unsigned kPtX = 0x71, kPtY = 0x6A, kPtZ = 0x5C;
+
+struct ResidualParams {
+  float inv_sig_a, inv_sig_b;  // 1/sigma
+  float C_thresh, Q_thresh;
+  float fx, fy, cx, cy;
+  int width, height;
+  float border, z_eps;
+  float huber_k;
+};
+
+// One (edge, pixel) contribution. Xi: target point (KF i, gathered),
+// Y = T_ij Xj: source point in frame i. `ok` = match/threshold validity.
+// u_t/v_t: target pixel (calib).
+template <int MODE>
+__device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &P, const float *Xi,
+                                              const float *Y, bool ok, float q, int u_t, int v_t) {
+  if (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
+    const float ni = fsqrt(Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2]);
+    const float ini = frcp(ni);
+    const float nj2 = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
+    const float nj = fsqrt(nj2);
+    const float inj = frcp(nj);
+    const float rx = Y[0] * inj, ry = Y[1] * inj, rz = Y[2] * inj;
+    const float e0 = rx - Xi[0] * ini, e1 = ry - Xi[1] * ini, e2 = rz - Xi[2] * ini;
+    const float e3 = nj - ni;
+    const float sq = fsqrt(q);
+    const float swr = ok ? P.inv_sig_a * sq : 0.0f;
+    const float swd = ok ? P.inv_sig_b * sq : 0.0f;
+    const float kr = swr * swr, kd = swd * swd;
+    const float w0 = huber_w(swr * e0, P.huber_k) * kr;
+    const float w1 = huber_w(swr * e1, P.huber_k) * kr;
+    const float w2 = huber_w(swr * e2, P.huber_k) * kr;
+    const float w3 = huber_w(swd * e3, P.huber_k) * kd;
+    // d r / d P = (I - r r^T) / |P|
+    const float dxx = inj - rx * rx * inj, dyy = inj - ry * ry * inj, dzz = inj - rz * rz * inj;
+    const float dxy = -rx * ry * inj, dxz = -rx * rz * inj, dyz = -ry * rz * inj;
+    const float a0[7] = {dxx, dxy, dxz, 0.0f, rz, -ry, 0.0f};
+    const float a1[7] = {dxy, dyy, dyz, -rz, 0.0f, rx, 0.0f};
+    const float a2[7] = {dxz, dyz, dzz, ry, -rx, 0.0f, 0.0f};
+    const float a3[7] = {rx, ry, rz, 0.0f, 0.0f, 0.0f, nj};
+    accum_row<kRayX>(acc, a0, w0, e0);
+    accum_row<kRayY>(acc, a1, w1, e1);
+    accum_row<kRayZ>(acc, a2, w2, e2);
+    accum_row<kRayD>(acc, a3, w3, e3);
+  } else if (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
+    const bool vz = (Y[2] > P.z_eps) && (Xi[2] > P.z_eps);
+    const float zinv = vz ? frcp(Y[2]) : 0.0f;
+    const float lzj = vz ? flog(Y[2]) : 0.0f;
+    const float lzi = vz ? flog(Xi[2]) : 0.0f;
+    const float x = Y[0] * zinv, y = Y[1] * zinv;
+    const float u = P.fx * x + P.cx, v = P.fy * y + P.cy;
+    const bool vu = (u > P.border) && (u < (float)P.width - 1.0f - P.border);
+    const bool vv = (v > P.border) && (v < (float)P.height - 1.0f - P.border);
+    const float e0 = u - (float)u_t, e1 = v - (float)v_t, e2 = lzj - lzi;
+    const bool good = ok && vu && vv && vz;
+    const float sq = fsqrt(q);
+    const float swp = good ? P.inv_sig_a * sq : 0.0f;
+    const float swz = good ? P.inv_sig_b * sq : 0.0f;
+    const float kp = swp * swp, kz = swz * swz;
+    const float w0 = huber_w(swp * e0, P.huber_k) * kp;
+    const float w1 = huber_w(swp * e1, P.huber_k) * kp;
+    const float w2 = huber_w(swz * e2, P.huber_k) * kz;
+    const float fx = P.fx, fy = P.fy;
+    const float a0[7] = {fx * zinv, 0.0f, -fx * x * zinv, -fx * x * y, fx * (1.0f + x * x), -fx * y, 0.0f};
+    const float a1[7] = {0.0f, fy * zinv, -fy * y * zinv, -fy * (1.0f + y * y), fy * x * y, fy * x, 0.0f};
+    const float a2[7] = {0.0f, 0.0f, zinv, y, -x, 0.0f, 1.0f};
+    accum_row<kCalU>(acc, a0, w0, e0);
+    accum_row<kCalV>(acc, a1, w1, e1);
+    accum_row<kCalZ>(acc, a2, w2, e2);
+  } else {  // 3D point (point_align_kernel :564-674)
+    const float e0 = Y[0] - Xi[0], e1 = Y[1] - Xi[1], e2 = Y[2] - Xi[2];
+    const float sw = ok ? P.inv_sig_a * fsqrt(q) : 0.0f;
+    const float k2 = sw * sw;
+    const float w0 = huber_w(sw * e0, P.huber_k) * k2;
+    const float w1 = huber_w(sw * e1, P.huber_k) * k2;
+    const float w2 = huber_w(sw * e2, P.huber_k) * k2;
+    const float a0[7] = {1.0f, 0.0f, 0.0f, 0.0f, Y[2], -Y[1], Y[0]};
+    const float a1[7] = {0.0f, 1.0f, 0.0f, -Y[2], 0.0f, Y[0], Y[1]};
+    const float a2[7] = {0.0f, 0.0f, 1.0f, Y[1], -Y[0], 0.0f, Y[2]};
+    accum_row<kPtX>(acc, a0, w0, e0);
+    accum_row<kPtY>(acc, a1, w1, e1);
+    accum_row<kPtZ>(acc, a2, w2, e2);
+  }
+}
+
+// wave64 butterfly sum
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace m3s

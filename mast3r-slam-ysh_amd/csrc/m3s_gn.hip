@@ -1,0 +1,908 @@
+// m3s_gn.hip — MI355X (gfx950) Gauss-Newton backend for MASt3R-SLAM.
+//
+// One GN iteration of the backend (gauss_newton_{points,rays,calib}) is four
+// launches on the caller's stream, no host synchronisation:
+//
+//   linearize_kernel   grid = E_loc x chunks, 256 threads. Each block streams a
+//                      pixel chunk of one directed edge (idx/valid/Q/Xj/Cj
+//                      coalesced 16 B per lane, Xi/Ci gathered through
+//                      idx), builds the residual rows and accumulates the
+//                      28+7+1 local normal-equation sums in registers, then a
+//                      wave64 butterfly + LDS reduce -> one 36-float partial.
+//                      (replaces ray_align_kernel / calib_proj_kernel /
+//                      point_align_kernel, gn_kernels.cu:455-1543)
+//   edge_reduce_kernel fp64 sum of an edge's chunk partials in fixed order
+//                      (deterministic, no float atomics).
+//   assemble_kernel    one block per pose row: H_jj = M L M^T per touching
+//                      edge (M = Adj(T_i)^-T), +-H_jj into the dense fp64
+//                      system, g likewise. (replaces SparseBlock::update_lhs/
+//                      update_rhs, gn_kernels.cu:71-113, which ran on the CPU)
+//   chol_small_kernel  one 512-thread block: register-resident fp64 Cholesky
+//                      of the RHS-augmented system (forward solve for free),
+//                      blocked back-substitution, dx = -x, Sim3 retraction of
+//                      poses 1..N-1, ||dx|| < delta -> device stop flag.
+//                      (replaces Eigen SimplicialLLT on the host + the D2H/H2D
+//                      copies + pose_retr_kernel + .item() sync,
+//                      gn_kernels.cu:132-153, :1199-1222)
+//
+// The tracker entry points reuse linearize_kernel (no gather, frame-local
+// Jacobian) plus a one-block 7x7 solve/convergence kernel.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "m3s_device.h"
+#include "m3s_gn.h"
+
+using namespace m3s;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
+
+namespace {
+
+constexpr int kThreads = 256;        // linearize block
+constexpr int kPixPerThread = 4;     // one 16-B vector group
+constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
+constexpr int kTargetBlocks = 2048;  // ~8 blocks per CU on 256 CUs
+constexpr int kMaxSmallNp = 224;     // register Cholesky limit (n + 1 <= 7 * 32)
+constexpr int kCholThreads = 512;    // 16 x 32 thread grid
+
+// workspace-resident flags (int32)
+constexpr int kFlagStop = 0;  // set when converged / bad input: later launches no-op
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline int64_t chunks_for(int64_t HW, int64_t E_loc) {
+  const int64_t max_chunks = (HW + kBlockPix - 1) / kBlockPix;
+  int64_t c = (kTargetBlocks + E_loc - 1) / (E_loc > 0 ? E_loc : 1);
+  if (c < 1) c = 1;
+  if (c > max_chunks) c = max_chunks;
+  // make the chunk a multiple of kBlockPix, then recount
+  int64_t ch = (HW + c - 1) / c;
+  ch = (ch + kBlockPix - 1) / kBlockPix * kBlockPix;
+  return (HW + ch - 1) / ch;
+}
+inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
+  int64_t ch = (HW + chunks - 1) / chunks;
+  return (ch + kBlockPix - 1) / kBlockPix * kBlockPix;
+}
+
+struct Layout {
+  size_t flags, rank_i, rank_j, first, partials, edge_sums, H, g, total;
+};
+
+inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
+  Layout L;
+  const int64_t n = 7 * (N > 1 ? N - 1 : 0);
+  const int64_t max_partials = kTargetBlocks + E + 1;
+  size_t off = 0;
+  L.flags = off;
+  off = align_up(off + 64 * sizeof(int32_t), 256);
+  L.rank_i = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
+  L.rank_j = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
+  L.first = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)(2 * E + 1), 256);
+  L.partials = off;
+  off = align_up(off + sizeof(float) * kNP * (size_t)max_partials, 256);
+  L.edge_sums = off;
+  off = align_up(off + sizeof(double) * kNP * (size_t)(E + 1), 256);
+  L.H = off;
+  off = align_up(off + sizeof(double) * (size_t)(n * n + 1), 256);
+  L.g = off;
+  off = align_up(off + sizeof(double) * (size_t)(n + 1), 256);
+  L.total = off;
+  (void)HW;
+  return L;
+}
+
+template <typename T>
+inline T *at(void *base, size_t off) {
+  return reinterpret_cast<T *>(static_cast<char *>(base) + off);
+}
+
+// ------------------------------------------------------------- remapping --
+// rank of every ii/jj entry in sorted-unique(cat(ii, jj))  (gn_kernels.cu:161-170)
+__global__ void remap_first_kernel(const int64_t *__restrict__ ii, const int64_t *__restrict__ jj,
+                                   int64_t E, int32_t *__restrict__ first) {
+  __shared__ int64_t tile[1024];
+  const int64_t n = 2 * E;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t v = t < n ? (t < E ? ii[t] : jj[t - E]) : 0;
+  bool dup = false;
+  for (int64_t base = 0; base < n; base += 1024) {
+    __syncthreads();
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+      const int64_t s = base + k;
+      tile[k] = s < n ? (s < E ? ii[s] : jj[s - E]) : 0;
+    }
+    __syncthreads();
+    if (t < n) {
+      const int64_t lim = (t - base) < 1024 ? (t - base) : 1024;
+      for (int64_t k = 0; k < lim; k++) dup |= (tile[k] == v);
+    }
+  }
+  if (t < n) first[t] = dup ? 0 : 1;
+}
+
+__global__ void remap_rank_kernel(const int64_t *__restrict__ ii, const int64_t *__restrict__ jj,
+                                  int64_t E, int64_t N, const int32_t *__restrict__ first,
+                                  int32_t *__restrict__ rank_i, int32_t *__restrict__ rank_j,
+                                  int32_t *__restrict__ info, int32_t *__restrict__ flags) {
+  __shared__ int64_t tile[1024];
+  __shared__ int32_t tfirst[1024];
+  const int64_t n = 2 * E;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t v = t < n ? (t < E ? ii[t] : jj[t - E]) : 0;
+  int32_t r = 0;
+  for (int64_t base = 0; base < n; base += 1024) {
+    __syncthreads();
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+      const int64_t s = base + k;
+      tile[k] = s < n ? (s < E ? ii[s] : jj[s - E]) : 0;
+      tfirst[k] = s < n ? first[s] : 0;
+    }
+    __syncthreads();
+    if (t < n)
+      for (int k = 0; k < 1024; k++) r += (tfirst[k] && tile[k] < v) ? 1 : 0;
+  }
+  if (t < n) {
+    if (t < E)
+      rank_i[t] = r;
+    else
+      rank_j[t - E] = r;
+    atomicMax(&info[M3S_INFO_N_UNIQUE], r + 1);
+    if (r >= N) {
+      atomicExch(&info[M3S_INFO_BAD_EDGE], 1);
+      atomicExch(&flags[kFlagStop], 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------- linearize --
+struct LinArgs {
+  const float *Twc;        // backend: poses (rank order)
+  const float *T_rel;      // tracker: T_CkCf (single pose), else null
+  const float *Xs;
+  const float *Cs;
+  const float *Xsrc;       // tracker: Xf (source points); backend: unused
+  const int64_t *idx;
+  const uint8_t *valid;
+  const float *Q;
+  const int32_t *rank_i;
+  const int32_t *rank_j;
+  const int32_t *stop;
+  float *partials;
+  int64_t HW, edge_begin, chunks, chunk_pix;
+  ResidualParams P;
+};
+
+// one pixel's inputs -> contribution (shared by the vector and scalar paths)
+template <int MODE, bool TRACK>
+__device__ __forceinline__ void do_pixel(float *acc, const LinArgs &A, const Sim3f &Tij,
+                                         const float *Xs_i, const float *Cs_i, int64_t p, bool vm,
+                                         int64_t id_raw, float q, const float *Xj, float cj) {
+  const int64_t id = TRACK ? p : (vm ? id_raw : 0);
+  float Xi[3] = {Xs_i[3 * id + 0], Xs_i[3 * id + 1], Xs_i[3 * id + 2]};
+  bool ok;
+  if (TRACK) {
+    ok = vm;
+  } else {
+    const float ci = Cs_i[id];
+    ok = vm && (q > A.P.Q_thresh) && (ci > A.P.C_thresh) && (cj > A.P.C_thresh);
+  }
+  float Y[3];
+  act(Tij, Xj, Y);
+  int u_t = 0, v_t = 0;
+  if (MODE == M3S_MODE_CALIB) {
+    const int iid = (int)id;
+    int vv = (int)((float)iid * (1.0f / (float)A.P.width));
+    if (vv * A.P.width > iid) vv--;
+    if ((vv + 1) * A.P.width <= iid) vv++;
+    v_t = vv;
+    u_t = iid - vv * A.P.width;
+  }
+  pixel_contrib<MODE>(acc, A.P, Xi, Y, ok, q, u_t, v_t);
+}
+
+template <int MODE, bool TRACK, bool VEC>
+__global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
+  if (*A.stop) return;
+  const int64_t b = blockIdx.x;
+  const int64_t e_loc = b / A.chunks;
+  const int64_t c = b - e_loc * A.chunks;
+  const int64_t e = A.edge_begin + e_loc;
+  const int64_t HW = A.HW;
+
+  Sim3f Tij;
+  const float *Xs_i, *Xs_j, *Cs_i = nullptr, *Cs_j = nullptr;
+  if (TRACK) {
+    Tij = load_sim3(A.T_rel);
+    Xs_i = A.Xs;    // Xk (target, pixel-aligned)
+    Xs_j = A.Xsrc;  // Xf (source, already gathered by idx_f2k)
+  } else {
+    const int ri = A.rank_i[e], rj = A.rank_j[e];
+    Tij = relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj));
+    Xs_i = A.Xs + (size_t)ri * HW * 3;
+    Xs_j = A.Xs + (size_t)rj * HW * 3;
+    Cs_i = A.Cs + (size_t)ri * HW;
+    Cs_j = A.Cs + (size_t)rj * HW;
+  }
+  const size_t eoff = TRACK ? 0 : (size_t)e * HW;
+  const int64_t* __restrict__ idx = TRACK ? nullptr : A.idx + eoff;
+  const uint8_t* __restrict__ valid = A.valid + eoff;
+  const float* __restrict__ Qe = A.Q + eoff;
+
+  float acc[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) acc[k] = 0.0f;
+
+  const int64_t p_begin = c * A.chunk_pix;
+  const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
+
+  if (VEC) {
+    for (int64_t p0 = p_begin + kPixPerThread * threadIdx.x; p0 < p_end; p0 += kBlockPix) {
+      // edge data is read once per iteration: non-temporal, so the pointmaps
+      // (re-read by every edge that touches a keyframe) keep the caches
+      const uint32_t vb = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(valid + p0));
+      const f32x4 q4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(Qe + p0));
+      int64_t ids[4] = {0, 0, 0, 0};
+      if (!TRACK) {
+        const i64x2 i01 = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(idx + p0));
+        const i64x2 i23 = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(idx + p0 + 2));
+        ids[0] = i01.x, ids[1] = i01.y, ids[2] = i23.x, ids[3] = i23.y;
+      }
+      const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * p0);
+      const f32x4 xa = xj4[0], xb = xj4[1], xc = xj4[2];
+      f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
+      if (!TRACK) c4 = *reinterpret_cast<const f32x4 *>(Cs_j + p0);
+      const float Xj[4][3] = {{xa.x, xa.y, xa.z}, {xa.w, xb.x, xb.y}, {xb.z, xb.w, xc.x}, {xc.y, xc.z, xc.w}};
+      const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
+      const float cjs[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int s = 0; s < 4; s++)
+        do_pixel<MODE, TRACK>(acc, A, Tij, Xs_i, Cs_i, p0 + s, ((vb >> (8 * s)) & 0xffu) != 0,
+                              ids[s], qs[s], Xj[s], cjs[s]);
+    }
+  } else {
+    for (int64_t p = p_begin + threadIdx.x; p < p_end; p += kThreads) {
+      const bool vm = valid[p] != 0;
+      const int64_t id = TRACK ? p : idx[p];
+      const float Xj[3] = {Xs_j[3 * p], Xs_j[3 * p + 1], Xs_j[3 * p + 2]};
+      const float cj = TRACK ? 0.0f : Cs_j[p];
+      do_pixel<MODE, TRACK>(acc, A, Tij, Xs_i, Cs_i, p, vm, id, Qe[p], Xj, cj);
+    }
+  }
+
+  // block reduction: wave64 butterfly, then 4 waves through LDS
+  __shared__ float red[kThreads / 64][kNP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kNP; k++) {
+    const float v = wave_sum(acc[k]);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNP) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) s += red[w][threadIdx.x];
+    A.partials[(size_t)b * kNP + threadIdx.x] = s;
+  }
+}
+
+// fp64 sum of each edge's chunk partials (fixed order)
+__global__ void edge_reduce_kernel(const float *__restrict__ partials, int64_t chunks,
+                                   double *__restrict__ edge_sums, const int32_t *__restrict__ stop) {
+  if (*stop) return;
+  const int64_t e = blockIdx.x;
+  const int t = threadIdx.x;
+  if (t >= kNP) return;
+  double s = 0.0;
+  const float *p = partials + (size_t)e * chunks * kNP + t;
+  for (int64_t c = 0; c < chunks; c++) s += (double)p[(size_t)c * kNP];
+  edge_sums[(size_t)e * kNP + t] = s;
+}
+
+// ------------------------------------------------------------- assemble --
+// Block r owns rows [7r, 7r+7) of the (N-1)*7 system (pose rank r+1).
+__global__ void __launch_bounds__(256) assemble_kernel(const double *__restrict__ edge_sums,
+                                                       const int32_t *__restrict__ rank_i,
+                                                       const int32_t *__restrict__ rank_j, int64_t E,
+                                                       const float *__restrict__ Twc, int64_t n,
+                                                       double *__restrict__ H, double *__restrict__ g,
+                                                       const int32_t *__restrict__ stop) {
+  if (*stop) return;
+  const int r = blockIdx.x;
+  const int t = threadIdx.x;
+  __shared__ double M[7][7], Lm[7][7], T1[7][7], Hjj[7][7], l[7], gj[7];
+  for (int64_t k = t; k < 7 * n; k += blockDim.x) H[(size_t)7 * r * n + k] = 0.0;
+  if (t < 7) g[7 * r + t] = 0.0;
+  __syncthreads();
+  for (int64_t e = 0; e < E; e++) {
+    const int i = rank_i[e] - 1, j = rank_j[e] - 1;
+    if (i != r && j != r) continue;  // uniform across the block
+    const double *es = edge_sums + (size_t)e * kNP;
+    if (t == 0) adjT_inv_matrix(Twc + 8 * (size_t)(i + 1), M);
+    if (t < 49) {
+      const int a = t / 7, c = t % 7;
+      const int lo = a < c ? a : c, hi = a < c ? c : a;
+      Lm[a][c] = es[kL + tri(lo, hi)];
+    }
+    if (t < 7) l[t] = es[kG + t];
+    __syncthreads();
+    if (t < 49) {
+      const int a = t / 7, c = t % 7;
+      double s = 0.0;
+      for (int k = 0; k < 7; k++) s += M[a][k] * Lm[k][c];
+      T1[a][c] = s;
+    } else if (t < 56) {
+      const int a = t - 49;
+      double s = 0.0;
+      for (int k = 0; k < 7; k++) s += M[a][k] * l[k];
+      gj[a] = s;
+    }
+    __syncthreads();
+    if (t < 49) {
+      const int a = t / 7, c = t % 7;
+      double s = 0.0;
+      for (int k = 0; k < 7; k++) s += T1[a][k] * M[c][k];
+      Hjj[a][c] = s;
+    }
+    __syncthreads();
+    if (t < 49) {
+      const int a = t / 7, c = t % 7;
+      double *row = H + (size_t)(7 * r + a) * n;
+      const double h = Hjj[a][c];
+      // edge (i -> j): Hs[0]=Hs[3]=Hjj at (i,i),(j,j); Hs[1]=Hs[2]=-Hjj off-diagonal
+      if (i == r) {
+        row[7 * r + c] += h;
+        if (j >= 0) row[7 * j + c] -= h;
+      }
+      if (j == r) {
+        row[7 * r + c] += h;
+        if (i >= 0) row[7 * i + c] -= h;
+      }
+    } else if (t < 56) {
+      const int a = t - 49;
+      if (i == r) g[7 * r + a] -= gj[a];  // gs[0] = -M l
+      if (j == r) g[7 * r + a] += gj[a];  // gs[1] = +M l
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------- small dense Cholesky --
+// Thread (tr, tc) of a 16 x 32 grid owns A[lr*16 + tr][lc*32 + tc]. The RHS g
+// is appended as row n, so the factor's row n is y = L^-1 g. After the loop
+// the registers hold L (lower triangle). NBC = column blocks of 32.
+template <int NBC>
+__global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
+    const double *__restrict__ H, const double *__restrict__ g, int n, float *__restrict__ Twc,
+    int64_t N, float *__restrict__ dx_out, int32_t *__restrict__ info, int32_t *__restrict__ stop,
+    float delta_thresh) {
+  constexpr int NBR = 2 * NBC;
+  if (*stop) return;
+  const int tid = threadIdx.x;
+  const int tr = tid >> 5, tc = tid & 31;
+  __shared__ double colbuf[2][32 * NBC];
+  __shared__ double xbuf[32 * NBC];
+  __shared__ double ybuf[32 * NBC];
+  __shared__ double red[16][33];
+  __shared__ double dblk[32][33];
+  __shared__ float dxs[32 * NBC];
+  __shared__ float nrm[kCholThreads / 64];
+  __shared__ int failed_s;
+
+  double A[NBR][NBC];
+#pragma unroll
+  for (int lr = 0; lr < NBR; lr++)
+#pragma unroll
+    for (int lc = 0; lc < NBC; lc++) {
+      const int i = lr * 16 + tr, j = lc * 32 + tc;
+      double v;
+      if (i < n && j < n)
+        v = H[(size_t)i * n + j];
+      else if (i == n && j < n)
+        v = g[j];
+      else
+        v = (i == j) ? 1.0 : 0.0;
+      A[lr][lc] = v;
+    }
+  for (int k = tid; k < 32 * NBC; k += kCholThreads) xbuf[k] = 0.0, ybuf[k] = 0.0;
+  if (tid == 0) failed_s = 0;
+  bool failed = false;
+  int step = 0;
+
+#pragma unroll
+  for (int kb = 0; kb < NBC; kb++) {
+    for (int c = 0; c < 32; c++) {
+      const int k = kb * 32 + c;
+      if (k >= n || failed) break;
+      double *cb = colbuf[step & 1];
+      // owners of column k publish it (rows < k as 0)
+      if (tc == c) {
+#pragma unroll
+        for (int lr = 0; lr < NBR; lr++) {
+          const int i = lr * 16 + tr;
+          cb[i] = (i >= k) ? A[lr][kb] : 0.0;
+        }
+      }
+      __syncthreads();
+      const double d = cb[k];
+      if (!(d > 0.0)) {  // Eigen LLT: non-positive pivot -> failure (dx = 0)
+        failed = true;
+        break;
+      }
+      const double inv = 1.0 / sqrt(d);
+      double lj[NBC];
+#pragma unroll
+      for (int lc = 0; lc < NBC; lc++) lj[lc] = (lc >= kb) ? cb[lc * 32 + tc] * inv : 0.0;
+#pragma unroll
+      for (int lr = 2 * kb; lr < NBR; lr++) {
+        const double li = cb[lr * 16 + tr] * inv;
+#pragma unroll
+        for (int lc = kb; lc < NBC; lc++)
+          if (lc * 32 <= lr * 16 + 15) A[lr][lc] -= li * lj[lc];
+        if (tc == c) A[lr][kb] = li;  // column k of L
+      }
+      step++;
+    }
+  }
+
+  if (failed) {
+    // every thread saw the same pivot; write dx = 0
+    for (int k = tid; k < (int)(7 * (N - 1)); k += kCholThreads) dx_out[k] = 0.0f;
+    if (tid == 0) {
+      info[M3S_INFO_ITERS] += 1;
+      info[M3S_INFO_SOLVE_FAIL] += 1;
+      if (0.0f < delta_thresh) {
+        info[M3S_INFO_CONVERGED] = 1;
+        stop[0] = 1;
+      }
+    }
+    return;
+  }
+
+  // y = row n of the factor
+#pragma unroll
+  for (int lr = 0; lr < NBR; lr++)
+    if (lr * 16 + tr == n)
+#pragma unroll
+      for (int lc = 0; lc < NBC; lc++) {
+        const int j = lc * 32 + tc;
+        if (j < n) ybuf[j] = A[lr][lc];
+      }
+  __syncthreads();
+
+  // back-substitution L^T x = y, 32-column blocks from the bottom
+#pragma unroll
+  for (int kb = NBC - 1; kb >= 0; kb--) {
+    double s = 0.0;
+#pragma unroll
+    for (int lr = 0; lr < NBR; lr++)
+      if (lr * 16 >= (kb + 1) * 32) s += A[lr][kb] * xbuf[lr * 16 + tr];
+    red[tr][tc] = s;
+#pragma unroll
+    for (int lr = 2 * kb; lr < 2 * kb + 2; lr++) dblk[lr * 16 + tr - kb * 32][tc] = A[lr][kb];
+    __syncthreads();
+    if (tid < 64) {
+      const int cc = tid & 31;
+      double rhs = 0.0;
+      if (tid < 32) {
+        const int j = kb * 32 + cc;
+        double acc = 0.0;
+        for (int q = 0; q < 16; q++) acc += red[q][cc];
+        rhs = (j < n) ? ybuf[j] - acc : 0.0;
+      }
+      double x = 0.0;
+      for (int cp = 31; cp >= 0; cp--) {
+        const double xc = __shfl(rhs, cp, 64) / dblk[cp][cp];
+        if (kb * 32 + cp >= n) continue;  // uniform
+        if (cc < cp) rhs -= dblk[cp][cc] * xc;
+        if (cc == cp) x = xc;
+      }
+      if (tid < 32) {
+        const int j = kb * 32 + cc;
+        xbuf[j] = (j < n) ? x : 0.0;
+      }
+    }
+    __syncthreads();
+  }
+
+  // dx = -x (float), retraction of poses 1..N-1, ||dx||
+  float part = 0.0f;
+  for (int k = tid; k < n; k += kCholThreads) {
+    const float v = -(float)xbuf[k];
+    dxs[k] = v;
+    dx_out[k] = v;
+    part += v * v;
+  }
+  part = wave_sum(part);
+  if ((tid & 63) == 0) nrm[tid >> 6] = part;
+  __syncthreads();
+  for (int p = tid; p < (int)(N - 1); p += kCholThreads) {
+    const Sim3f T = load_sim3(Twc + 8 * (size_t)(p + 1));
+    store_sim3(Twc + 8 * (size_t)(p + 1), retract(dxs + 7 * p, T));
+  }
+  if (tid == 0) {
+    float s = 0.0f;
+    for (int w = 0; w < kCholThreads / 64; w++) s += nrm[w];
+    info[M3S_INFO_ITERS] += 1;
+    if (sqrtf(s) < delta_thresh) {
+      info[M3S_INFO_CONVERGED] = 1;
+      stop[0] = 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host --
+inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+int launch_ok() { return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH; }
+
+ResidualParams make_params(const m3s_gn_args *a) {
+  ResidualParams P;
+  P.inv_sig_a = a->sigma_a != 0.0f ? (float)(1.0 / (double)a->sigma_a) : 0.0f;
+  P.inv_sig_b = a->sigma_b != 0.0f ? (float)(1.0 / (double)a->sigma_b) : 0.0f;
+  P.C_thresh = a->C_thresh;
+  P.Q_thresh = a->Q_thresh;
+  P.fx = P.fy = P.cx = P.cy = 0.0f;
+  P.width = a->width;
+  P.height = a->height;
+  P.border = (float)a->pixel_border;
+  P.z_eps = a->z_eps;
+  P.huber_k = 1.345f;  // hard-coded in the reference kernels (gn_kernels.cu:172-175)
+  return P;
+}
+
+int check_args(const m3s_gn_args *a) {
+  if (!a || !a->Twc || !a->Xs || !a->Cs || !a->ii || !a->jj || !a->idx_ii2jj || !a->valid_match ||
+      !a->Q || !a->info || !a->workspace)
+    return M3S_EINVAL;
+  if (a->N < 1 || a->HW < 1 || a->E < 0) return M3S_EINVAL;
+  if (a->mode == M3S_MODE_CALIB && (!a->K || a->width < 1 || a->height < 1)) return M3S_EINVAL;
+  if (a->workspace_bytes < gn_layout(a->N, a->HW, a->E).total) return M3S_EINVAL;
+  if (a->HW * 3 >= ((int64_t)1 << 40)) return M3S_ETOOLARGE;
+  if (a->mode < 0 || a->mode > 2) return M3S_EINVAL;
+  return M3S_OK;
+}
+
+template <int MODE, bool TRACK>
+int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, hipStream_t st) {
+  if (blocks <= 0) return M3S_OK;
+  if (vec)
+    linearize_kernel<MODE, TRACK, true><<<dim3((unsigned)blocks), dim3(kThreads), 0, st>>>(L);
+  else
+    linearize_kernel<MODE, TRACK, false><<<dim3((unsigned)blocks), dim3(kThreads), 0, st>>>(L);
+  return launch_ok();
+}
+
+template <bool TRACK>
+int dispatch_linearize(int mode, const LinArgs &L, int64_t blocks, bool vec, hipStream_t st) {
+  switch (mode) {
+    case M3S_MODE_POINTS: return launch_linearize<M3S_MODE_POINTS, TRACK>(L, blocks, vec, st);
+    case M3S_MODE_RAYS: return launch_linearize<M3S_MODE_RAYS, TRACK>(L, blocks, vec, st);
+    case M3S_MODE_CALIB: return launch_linearize<M3S_MODE_CALIB, TRACK>(L, blocks, vec, st);
+  }
+  return M3S_EINVAL;
+}
+
+bool vec_ok(const void *p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+// K is a device pointer; read it once per call (tiny D2H copy, not on the
+// iteration path). For graph capture the caller can pass params instead.
+int read_K(const float *K, ResidualParams &P, hipStream_t st) {
+  float k[9];
+  if (hipMemcpyAsync(k, K, sizeof k, hipMemcpyDeviceToHost, st) != hipSuccess) return M3S_ELAUNCH;
+  if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
+  P.fx = k[0], P.fy = k[4], P.cx = k[2], P.cy = k[5];
+  return M3S_OK;
+}
+
+int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb, int64_t ee,
+                      double *edge_sums, hipStream_t st) {
+  const Layout Ly = gn_layout(a->N, a->HW, a->E);
+  void *ws = a->workspace;
+  const int64_t E_loc = ee - eb;
+  if (E_loc <= 0) return M3S_OK;
+  LinArgs L;
+  L.Twc = a->Twc;
+  L.T_rel = nullptr;
+  L.Xs = a->Xs;
+  L.Cs = a->Cs;
+  L.Xsrc = nullptr;
+  L.idx = a->idx_ii2jj;
+  L.valid = a->valid_match;
+  L.Q = a->Q;
+  L.rank_i = at<int32_t>(ws, Ly.rank_i);
+  L.rank_j = at<int32_t>(ws, Ly.rank_j);
+  L.stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
+  L.partials = at<float>(ws, Ly.partials);
+  L.HW = a->HW;
+  L.edge_begin = eb;
+  L.chunks = chunks_for(a->HW, E_loc);
+  L.chunk_pix = chunk_pixels(a->HW, L.chunks);
+  L.P = P;
+  const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xs, 16) && vec_ok(a->Cs, 16) && vec_ok(a->Q, 16) &&
+                   vec_ok(a->idx_ii2jj, 16) && vec_ok(a->valid_match, 4);
+  int rc = dispatch_linearize<false>(a->mode, L, E_loc * L.chunks, vec, st);
+  if (rc) return rc;
+  edge_reduce_kernel<<<dim3((unsigned)E_loc), dim3(64), 0, st>>>(L.partials, L.chunks, edge_sums, L.stop);
+  return launch_ok();
+}
+
+int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st) {
+  const Layout Ly = gn_layout(a->N, a->HW, a->E);
+  void *ws = a->workspace;
+  int32_t *stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
+  const int64_t n = 7 * (a->N - 1);
+  if (a->N <= 1) return M3S_OK;
+  double *H = at<double>(ws, Ly.H), *g = at<double>(ws, Ly.g);
+  assemble_kernel<<<dim3((unsigned)(a->N - 1)), dim3(256), 0, st>>>(
+      edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, H, g, stop);
+  int rc = launch_ok();
+  if (rc) return rc;
+  const int np = (int)n + 1;
+  if (np > kMaxSmallNp) return M3S_ETOOLARGE;
+  const int nbc = (np + 31) / 32;
+  float *dx = a->dx_out;
+#define M3S_CHOL(NB)                                                                                    \
+  case NB:                                                                                              \
+    chol_small_kernel<NB><<<dim3(1), dim3(kCholThreads), 0, st>>>(H, g, (int)n, a->Twc, a->N, dx,     \
+                                                                 a->info, stop, a->delta_thresh); \
+    break;
+  switch (nbc) {
+    M3S_CHOL(1)
+    M3S_CHOL(2)
+    M3S_CHOL(3)
+    M3S_CHOL(4)
+    M3S_CHOL(5)
+    M3S_CHOL(6)
+    M3S_CHOL(7)
+    default:
+      return M3S_ETOOLARGE;
+  }
+#undef M3S_CHOL
+  return launch_ok();
+}
+
+int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
+  const Layout Ly = gn_layout(a->N, a->HW, a->E);
+  void *ws = a->workspace;
+  if (hipMemsetAsync(at<int32_t>(ws, Ly.flags), 0, 64 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
+  if (hipMemsetAsync(a->info, 0, 8 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
+  if (a->N > 1 && a->dx_out && hipMemsetAsync(a->dx_out, 0, sizeof(float) * 7 * (a->N - 1), st) != hipSuccess)
+    return M3S_ELAUNCH;
+  if (a->E <= 0) return M3S_OK;
+  const int64_t n = 2 * a->E;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  int32_t *first = at<int32_t>(ws, Ly.first);
+  remap_first_kernel<<<dim3(blocks), dim3(256), 0, st>>>(a->ii, a->jj, a->E, first);
+  int rc = launch_ok();
+  if (rc) return rc;
+  remap_rank_kernel<<<dim3(blocks), dim3(256), 0, st>>>(a->ii, a->jj, a->E, a->N, first,
+                                                         at<int32_t>(ws, Ly.rank_i),
+                                                         at<int32_t>(ws, Ly.rank_j), a->info,
+                                                         at<int32_t>(ws, Ly.flags));
+  return launch_ok();
+}
+
+int gn_full(const m3s_gn_args *a, int mode, void *stream) {
+  int rc = check_args(a);
+  if (rc) return rc;
+  if (a->mode != mode) return M3S_EINVAL;
+  if (a->N > 1 && 7 * (a->N - 1) + 1 > kMaxSmallNp) return M3S_ETOOLARGE;
+  hipStream_t st = S(stream);
+  ResidualParams P = make_params(a);
+  if (mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, st))) return rc;
+  if ((rc = gn_prepare_impl(a, st))) return rc;
+  const Layout Ly = gn_layout(a->N, a->HW, a->E);
+  double *es = at<double>(a->workspace, Ly.edge_sums);
+  for (int it = 0; it < a->max_iter; it++) {
+    if ((rc = gn_linearize_impl(a, P, 0, a->E, es, st))) return rc;
+    if ((rc = gn_solve_impl(a, es, st))) return rc;
+  }
+  return M3S_OK;
+}
+
+// --------------------------------------------------------------- tracker --
+struct TrackState {
+  float T_rel[8];   // T_CkCf
+  float T_WCk[8];
+  double old_cost;
+  int32_t done;
+  int32_t pad;
+};
+
+constexpr size_t kTrackStateOff = 0;
+inline size_t track_partials_off() { return 256; }
+
+__global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackState *st, int32_t *info,
+                                  float *T_WCf_out, float *T_CkCf_out) {
+  if (threadIdx.x != 0) return;
+  const Sim3f Tk = load_sim3(T_WCk), Tf = load_sim3(T_WCf);
+  const Sim3f R = compose(inverse(Tk), Tf);
+  store_sim3(st->T_rel, R);
+  store_sim3(st->T_WCk, Tk);
+  st->old_cost = __builtin_inf();
+  st->done = 0;
+  for (int k = 0; k < 8; k++) info[k] = 0;
+  store_sim3(T_CkCf_out, R);
+  store_sim3(T_WCf_out, Tf);
+}
+
+// reduce chunk partials, 7x7 fp64 Cholesky, tau = -H^-1 g, retraction,
+// convergence (nonlinear_optimizer.py:5-25), outputs.
+__global__ void __launch_bounds__(64) track_solve_kernel(const float *__restrict__ partials, int64_t chunks,
+                                                         TrackState *st, int32_t *info, float rel_error,
+                                                         float delta_norm, float *T_WCf_out,
+                                                         float *T_CkCf_out) {
+  if (st->done) return;
+  __shared__ double s[kNP];
+  const int t = threadIdx.x;
+  if (t < kNP) {
+    double a = 0.0;
+    for (int64_t c = 0; c < chunks; c++) a += (double)partials[(size_t)c * kNP + t];
+    s[t] = a;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  double H[7][7], L[7][7], g[7], y[7], x[7];
+  for (int a = 0; a < 7; a++)
+    for (int c = 0; c < 7; c++) H[a][c] = s[kL + tri(a < c ? a : c, a < c ? c : a)];
+  for (int a = 0; a < 7; a++) g[a] = s[kG + a];
+  const double cost = 0.5 * s[kCost];
+  for (int a = 0; a < 7; a++)
+    for (int c = 0; c < 7; c++) L[a][c] = 0.0;
+  for (int k = 0; k < 7; k++) {
+    double d = H[k][k];
+    for (int p = 0; p < k; p++) d -= L[k][p] * L[k][p];
+    if (!(d > 0.0)) {  // torch.linalg.cholesky raises -> tracking failure
+      info[M3S_INFO_SOLVE_FAIL] = 1;
+      info[M3S_INFO_ITERS] += 1;
+      st->done = 1;
+      return;
+    }
+    L[k][k] = sqrt(d);
+    for (int i = k + 1; i < 7; i++) {
+      double v = H[i][k];
+      for (int p = 0; p < k; p++) v -= L[i][p] * L[k][p];
+      L[i][k] = v / L[k][k];
+    }
+  }
+  // tau = H^-1 (-g): kernel g = sum w e J with e = pred - meas  (tracker.py:165-169)
+  for (int i = 0; i < 7; i++) {
+    double v = -g[i];
+    for (int p = 0; p < i; p++) v -= L[i][p] * y[p];
+    y[i] = v / L[i][i];
+  }
+  for (int i = 6; i >= 0; i--) {
+    double v = y[i];
+    for (int p = i + 1; p < 7; p++) v -= L[p][i] * x[p];
+    x[i] = v / L[i][i];
+  }
+  float tau[7];
+  float n2 = 0.0f;
+  for (int k = 0; k < 7; k++) {
+    tau[k] = (float)x[k];
+    n2 += tau[k] * tau[k];
+  }
+  const Sim3f Tn = retract(tau, load_sim3(st->T_rel));
+  store_sim3(st->T_rel, Tn);
+  store_sim3(T_CkCf_out, Tn);
+  store_sim3(T_WCf_out, compose(load_sim3(st->T_WCk), Tn));
+  info[M3S_INFO_ITERS] += 1;
+  const float cost_f = (float)cost;  // the reference's cost is a python float of an fp32 .item()
+  const double old = st->old_cost;
+  const double rel = fabs((old - (double)cost_f) / old);  // NaN on the first step (old = inf)
+  if (rel < (double)rel_error || sqrtf(n2) < delta_norm) {
+    st->done = 1;
+    info[M3S_INFO_CONVERGED] = 1;
+  }
+  st->old_cost = (double)cost_f;
+}
+
+int track_impl(const m3s_track_args *a, int mode, void *stream) {
+  if (!a || !a->Xf || !a->Xk || !a->Qk || !a->valid || !a->T_WCf || !a->T_WCk || !a->T_WCf_out ||
+      !a->T_CkCf_out || !a->info || !a->workspace || a->HW < 1)
+    return M3S_EINVAL;
+  if (mode == M3S_MODE_CALIB && (!a->K || a->width < 1 || a->height < 1)) return M3S_EINVAL;
+  if (a->workspace_bytes < m3s_track_workspace_size(a->HW)) return M3S_EINVAL;
+  hipStream_t st = S(stream);
+  ResidualParams P;
+  P.inv_sig_a = (float)(1.0 / (double)a->sigma_a);
+  P.inv_sig_b = (float)(1.0 / (double)a->sigma_b);
+  P.C_thresh = P.Q_thresh = 0.0f;
+  P.fx = P.fy = P.cx = P.cy = 0.0f;
+  P.width = a->width;
+  P.height = a->height;
+  P.border = (float)a->pixel_border;
+  P.z_eps = a->z_eps;
+  P.huber_k = a->huber_k;
+  int rc;
+  if (mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, st))) return rc;
+  TrackState *ts = at<TrackState>(a->workspace, kTrackStateOff);
+  float *partials = at<float>(a->workspace, track_partials_off());
+  track_init_kernel<<<1, 64, 0, st>>>(a->T_WCf, a->T_WCk, ts, a->info, a->T_WCf_out, a->T_CkCf_out);
+  if ((rc = launch_ok())) return rc;
+  LinArgs L;
+  memset(&L, 0, sizeof L);
+  L.T_rel = ts->T_rel;
+  L.Xs = a->Xk;
+  L.Xsrc = a->Xf;
+  L.valid = a->valid;
+  L.Q = a->Qk;
+  L.stop = &ts->done;
+  L.partials = partials;
+  L.HW = a->HW;
+  L.edge_begin = 0;
+  L.chunks = chunks_for(a->HW, 1);
+  L.chunk_pix = chunk_pixels(a->HW, L.chunks);
+  L.P = P;
+  const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xf, 16) && vec_ok(a->Xk, 16) && vec_ok(a->Qk, 16) &&
+                   vec_ok(a->valid, 4);
+  for (int it = 0; it < a->max_iters; it++) {
+    if ((rc = dispatch_linearize<true>(mode, L, L.chunks, vec, st))) return rc;
+    track_solve_kernel<<<1, 64, 0, st>>>(partials, L.chunks, ts, a->info, a->rel_error, a->delta_norm,
+                                         a->T_WCf_out, a->T_CkCf_out);
+    if ((rc = launch_ok())) return rc;
+    if (a->sync_every > 0 && (it + 1) % a->sync_every == 0 && it + 1 < a->max_iters) {
+      int32_t done = 0;
+      if (hipMemcpyAsync(&done, &ts->done, sizeof done, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return M3S_ELAUNCH;
+      if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
+      if (done) break;
+    }
+  }
+  return M3S_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ C exports --
+extern "C" {
+
+size_t m3s_gn_workspace_size(int64_t N, int64_t HW, int64_t E) { return gn_layout(N, HW, E).total; }
+
+int m3s_gauss_newton_points(const m3s_gn_args *a, void *stream) { return gn_full(a, M3S_MODE_POINTS, stream); }
+int m3s_gauss_newton_rays(const m3s_gn_args *a, void *stream) { return gn_full(a, M3S_MODE_RAYS, stream); }
+int m3s_gauss_newton_calib(const m3s_gn_args *a, void *stream) { return gn_full(a, M3S_MODE_CALIB, stream); }
+
+int m3s_gn_prepare(const m3s_gn_args *a, void *stream) {
+  int rc = check_args(a);
+  if (rc) return rc;
+  return gn_prepare_impl(a, S(stream));
+}
+
+int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end, double *edge_sums,
+                     void *stream) {
+  int rc = check_args(a);
+  if (rc) return rc;
+  if (edge_begin < 0 || edge_end > a->E || edge_begin > edge_end || !edge_sums) return M3S_EINVAL;
+  ResidualParams P = make_params(a);
+  if (a->mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, S(stream)))) return rc;
+  return gn_linearize_impl(a, P, edge_begin, edge_end, edge_sums, S(stream));
+}
+
+int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
+  int rc = check_args(a);
+  if (rc) return rc;
+  if (!edge_sums) return M3S_EINVAL;
+  return gn_solve_impl(a, edge_sums, S(stream));
+}
+
+size_t m3s_track_workspace_size(int64_t HW) {
+  const int64_t chunks = chunks_for(HW, 1);
+  return track_partials_off() + align_up(sizeof(float) * kNP * (size_t)(chunks + 1), 256);
+}
+
+int m3s_track_rays_sim3(const m3s_track_args *a, void *stream) { return track_impl(a, M3S_MODE_RAYS, stream); }
+int m3s_track_calib_sim3(const m3s_track_args *a, void *stream) { return track_impl(a, M3S_MODE_CALIB, stream); }
+
+const char *m3s_version(void) { return "m3s-gn 0.1 gfx950"; }
+
+}  // extern "C"

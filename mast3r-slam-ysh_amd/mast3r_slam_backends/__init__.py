@@ -1,0 +1,319 @@
+"""``mast3r_slam_backends`` — drop-in for the reference's CUDA extension module,
+backed by the MI355X HIP library ``libm3s_gn.so`` through its C ABI
+(``include/m3s_gn.h``).
+
+Reference interface (``/root/reference/mast3r_slam/backend/src/gn.cpp:116-122``):
+same module name, same function names, same positional arguments, same
+in-place update of ``Twc`` and the same return value ``[dx]`` (the last GN step,
+``[N-1, 7]`` float32). Callers: ``global_opt.py:140-155`` (rays) and
+``global_opt.py:190-210`` (calib).
+
+Error behaviour: like ``TORCH_CHECK(x.is_contiguous())`` (``gn.cpp:14-21``) a
+non-contiguous input raises ``RuntimeError("<name> must be contiguous")``. In
+addition, tensors that are not on a ROCm device, or have the wrong dtype,
+raise ``RuntimeError`` — there is no CPU fallback: without the HIP library this
+module fails at import.
+
+New entry points (the reference tracker has no backend call, tracker.py:173-266):
+``track_rays_sim3`` and ``track_calib_sim3``.
+
+``iter_proj`` / ``refine_matches`` (matching kernels, SURVEY.md §8f "next" #1)
+are exported for interface completeness and raise ``NotImplementedError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libm3s_gn.so"
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+
+M3S_OK, M3S_EINVAL, M3S_ELAUNCH, M3S_ETOOLARGE = 0, 1, 2, 3
+MODE_POINTS, MODE_RAYS, MODE_CALIB = 0, 1, 2
+INFO_ITERS, INFO_SOLVE_FAIL, INFO_BAD_EDGE, INFO_CONVERGED, INFO_N_UNIQUE = 0, 1, 2, 3, 4
+EDGE_SUM_STRIDE = 36
+
+_VP = ctypes.c_void_p
+
+
+class GnArgs(ctypes.Structure):
+    """Mirror of ``m3s_gn_args`` (include/m3s_gn.h)."""
+
+    _fields_ = [
+        ("Twc", _VP), ("Xs", _VP), ("Cs", _VP), ("ii", _VP), ("jj", _VP),
+        ("idx_ii2jj", _VP), ("valid_match", _VP), ("Q", _VP), ("K", _VP),
+        ("N", ctypes.c_int64), ("HW", ctypes.c_int64), ("E", ctypes.c_int64),
+        ("mode", ctypes.c_int),
+        ("sigma_a", ctypes.c_float), ("sigma_b", ctypes.c_float),
+        ("C_thresh", ctypes.c_float), ("Q_thresh", ctypes.c_float),
+        ("height", ctypes.c_int), ("width", ctypes.c_int), ("pixel_border", ctypes.c_int),
+        ("z_eps", ctypes.c_float),
+        ("max_iter", ctypes.c_int), ("delta_thresh", ctypes.c_float),
+        ("dx_out", _VP), ("info", _VP),
+        ("workspace", _VP), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class TrackArgs(ctypes.Structure):
+    """Mirror of ``m3s_track_args`` (include/m3s_gn.h)."""
+
+    _fields_ = [
+        ("Xf", _VP), ("Xk", _VP), ("Qk", _VP), ("valid", _VP), ("T_WCf", _VP), ("T_WCk", _VP),
+        ("K", _VP), ("HW", ctypes.c_int64),
+        ("height", ctypes.c_int), ("width", ctypes.c_int), ("pixel_border", ctypes.c_int),
+        ("z_eps", ctypes.c_float), ("sigma_a", ctypes.c_float), ("sigma_b", ctypes.c_float),
+        ("huber_k", ctypes.c_float), ("max_iters", ctypes.c_int),
+        ("rel_error", ctypes.c_float), ("delta_norm", ctypes.c_float),
+        ("sync_every", ctypes.c_int),
+        ("T_WCf_out", _VP), ("T_CkCf_out", _VP), ("info", _VP),
+        ("workspace", _VP), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+# every symbol include/m3s_gn.h declares
+EXPORTS = (
+    "m3s_gn_workspace_size", "m3s_gauss_newton_points", "m3s_gauss_newton_rays",
+    "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve",
+    "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
+)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"mast3r_slam_backends: {LIB_PATH} is missing; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    lib.m3s_gn_workspace_size.restype = ctypes.c_size_t
+    lib.m3s_gn_workspace_size.argtypes = [ctypes.c_int64] * 3
+    for f in ("m3s_gauss_newton_points", "m3s_gauss_newton_rays", "m3s_gauss_newton_calib",
+              "m3s_gn_prepare"):
+        getattr(lib, f).restype = ctypes.c_int
+        getattr(lib, f).argtypes = [P(GnArgs), _VP]
+    lib.m3s_gn_linearize.restype = ctypes.c_int
+    lib.m3s_gn_linearize.argtypes = [P(GnArgs), ctypes.c_int64, ctypes.c_int64, _VP, _VP]
+    lib.m3s_gn_solve.restype = ctypes.c_int
+    lib.m3s_gn_solve.argtypes = [P(GnArgs), _VP, _VP]
+    lib.m3s_track_workspace_size.restype = ctypes.c_size_t
+    lib.m3s_track_workspace_size.argtypes = [ctypes.c_int64]
+    for f in ("m3s_track_rays_sim3", "m3s_track_calib_sim3"):
+        getattr(lib, f).restype = ctypes.c_int
+        getattr(lib, f).argtypes = [P(TrackArgs), _VP]
+    lib.m3s_version.restype = ctypes.c_char_p
+    lib.m3s_version.argtypes = []
+    return lib
+
+
+_lib = _load()
+
+
+def version() -> str:
+    return _lib.m3s_version().decode()
+
+
+# ------------------------------------------------------------------ checks --
+def _check(t: torch.Tensor, name: str, dtype=None):
+    if not isinstance(t, torch.Tensor):
+        raise RuntimeError(f"{name} must be a tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be on a ROCm device (got {t.device}); no CPU path")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {dtype} (got {t.dtype})")
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _raise(rc, fn):
+    if rc == M3S_OK:
+        return
+    msg = {M3S_EINVAL: "invalid argument", M3S_ELAUNCH: "HIP launch failed",
+           M3S_ETOOLARGE: "problem size exceeds this build's limits"}.get(rc, f"error {rc}")
+    raise RuntimeError(f"{fn}: {msg}")
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def make_gn_args(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, K=None, *, sigma_a=0.0,
+                 sigma_b=0.0, C_thresh=0.0, Q_thresh=0.0, height=0, width=0, pixel_border=0,
+                 z_eps=0.0, max_iter=0, delta_thresh=0.0, dx=None, info=None, workspace=None):
+    """Validate reference-layout tensors and fill an ``m3s_gn_args``. Returns
+    (args, keepalive) — keepalive holds every tensor the struct points to."""
+    _check(Twc, "Twc", torch.float32)
+    _check(Xs, "Xs", torch.float32)
+    _check(Cs, "Cs", torch.float32)
+    if K is not None:
+        _check(K, "K", torch.float32)
+    _check(ii, "ii", torch.int64)
+    _check(jj, "jj", torch.int64)
+    _check(idx_ii2jj, "idx_ii2jj", torch.int64)
+    _check(valid_match, "valid_match", torch.bool)
+    _check(Q, "Q", torch.float32)
+    N, HW = int(Xs.shape[0]), int(Xs.shape[1])
+    E = int(ii.shape[0])
+    if Xs.dim() != 3 or Xs.shape[2] != 3:
+        raise RuntimeError("Xs must be [N, HW, 3]")
+    if Twc.numel() != 8 * N:
+        raise RuntimeError(f"Twc must be [N, 8] with N = Xs.size(0) = {N}")
+    if Cs.numel() != N * HW:
+        raise RuntimeError("Cs must be [N, HW, 1]")
+    if jj.numel() != E or idx_ii2jj.numel() != E * HW or valid_match.numel() != E * HW or Q.numel() != E * HW:
+        raise RuntimeError("edge tensors must be [E, HW(,1)] with E = ii.size(0)")
+    dev = Xs.device
+    if dx is None:
+        dx = torch.zeros(max(N - 1, 0), 7, dtype=torch.float32, device=dev)
+    if info is None:
+        info = torch.zeros(8, dtype=torch.int32, device=dev)
+    ws_bytes = int(_lib.m3s_gn_workspace_size(N, HW, E))
+    if workspace is None or workspace.numel() < ws_bytes:
+        workspace = _workspace(ws_bytes, dev)
+    a = GnArgs()
+    a.Twc, a.Xs, a.Cs, a.ii, a.jj = _p(Twc), _p(Xs), _p(Cs), _p(ii), _p(jj)
+    a.idx_ii2jj, a.valid_match, a.Q, a.K = _p(idx_ii2jj), _p(valid_match), _p(Q), _p(K)
+    a.N, a.HW, a.E, a.mode = N, HW, E, mode
+    a.sigma_a, a.sigma_b = float(sigma_a), float(sigma_b)
+    a.C_thresh, a.Q_thresh = float(C_thresh), float(Q_thresh)
+    a.height, a.width, a.pixel_border = int(height), int(width), int(pixel_border)
+    a.z_eps = float(z_eps)
+    a.max_iter, a.delta_thresh = int(max_iter), float(delta_thresh)
+    a.dx_out, a.info = _p(dx), _p(info)
+    a.workspace, a.workspace_bytes = _p(workspace), workspace.numel()
+    keep = dict(Twc=Twc, Xs=Xs, Cs=Cs, ii=ii, jj=jj, idx=idx_ii2jj, valid=valid_match, Q=Q, K=K,
+                dx=dx, info=info, workspace=workspace)
+    return a, keep
+
+
+def _run_gn(fn_name, a, keep):
+    rc = getattr(_lib, fn_name)(ctypes.byref(a), _stream(keep["Xs"].device))
+    _raise(rc, fn_name)
+    return [keep["dx"]]
+
+
+# ------------------------------------------------- reference entry points --
+def gauss_newton_points(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_point, C_thresh,
+                        Q_thresh, max_iter, delta_thresh, *, info=None):
+    """gn.cpp:3-27 / gn_kernels.cu:725-811."""
+    a, keep = make_gn_args(MODE_POINTS, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q,
+                           sigma_a=sigma_point, C_thresh=C_thresh, Q_thresh=Q_thresh,
+                           max_iter=max_iter, delta_thresh=delta_thresh, info=info)
+    return _run_gn("m3s_gauss_newton_points", a, keep)
+
+
+def gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_ray, sigma_dist,
+                      C_thresh, Q_thresh, max_iter, delta_thresh, *, info=None):
+    """gn.cpp:29-54 / gn_kernels.cu:1140-1228."""
+    a, keep = make_gn_args(MODE_RAYS, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q,
+                           sigma_a=sigma_ray, sigma_b=sigma_dist, C_thresh=C_thresh,
+                           Q_thresh=Q_thresh, max_iter=max_iter, delta_thresh=delta_thresh,
+                           info=info)
+    return _run_gn("m3s_gauss_newton_rays", a, keep)
+
+
+def gauss_newton_calib(Twc, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q, height, width,
+                       pixel_border, z_eps, sigma_pixel, sigma_depth, C_thresh, Q_thresh, max_iter,
+                       delta_thresh, *, info=None):
+    """gn.cpp:56-85 / gn_kernels.cu:1546-1638."""
+    a, keep = make_gn_args(MODE_CALIB, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, K,
+                           sigma_a=sigma_pixel, sigma_b=sigma_depth, C_thresh=C_thresh,
+                           Q_thresh=Q_thresh, height=height, width=width,
+                           pixel_border=pixel_border, z_eps=z_eps, max_iter=max_iter,
+                           delta_thresh=delta_thresh, info=info)
+    return _run_gn("m3s_gauss_newton_calib", a, keep)
+
+
+def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh):
+    """matching_kernels.cu:119-315 — not part of this build's scope yet."""
+    raise NotImplementedError("iter_proj: matching kernels are not built yet (SURVEY.md §8f #1)")
+
+
+def refine_matches(D11, D21, p1, radius, dilation_max):
+    """matching_kernels.cu:25-116 — not part of this build's scope yet."""
+    raise NotImplementedError("refine_matches: matching kernels are not built yet (SURVEY.md §8f #1)")
+
+
+# ------------------------------------------------------------ tracker ---
+def _track(fn, Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size, sigma_a, sigma_b, huber_k,
+           max_iters, rel_error, delta_norm, pixel_border=0, z_eps=0.0, sync_every=5):
+    _check(Xf, "Xf", torch.float32)
+    _check(Xk, "Xk", torch.float32)
+    _check(Qk, "Qk", torch.float32)
+    _check(valid, "valid", torch.bool)
+    T_WCf = T_WCf.contiguous()
+    T_WCk = T_WCk.contiguous()
+    _check(T_WCf, "T_WCf", torch.float32)
+    _check(T_WCk, "T_WCk", torch.float32)
+    if K is not None:
+        _check(K, "K", torch.float32)
+    HW = int(Xk.shape[0])
+    if Xf.numel() != 3 * HW or Xk.numel() != 3 * HW or Qk.numel() != HW or valid.numel() != HW:
+        raise RuntimeError("tracker inputs must be Xf/Xk [HW,3], Qk/valid [HW,1]")
+    dev = Xk.device
+    out_f = torch.empty(1, 8, dtype=torch.float32, device=dev)
+    out_r = torch.empty(1, 8, dtype=torch.float32, device=dev)
+    info = torch.zeros(8, dtype=torch.int32, device=dev)
+    ws = _workspace(_lib.m3s_track_workspace_size(HW), dev)
+    a = TrackArgs()
+    a.Xf, a.Xk, a.Qk, a.valid = _p(Xf), _p(Xk), _p(Qk), _p(valid)
+    a.T_WCf, a.T_WCk, a.K = _p(T_WCf), _p(T_WCk), _p(K)
+    a.HW = HW
+    h, w = (int(img_size[0]), int(img_size[1])) if img_size is not None else (0, 0)
+    a.height, a.width, a.pixel_border, a.z_eps = h, w, int(pixel_border), float(z_eps)
+    a.sigma_a, a.sigma_b, a.huber_k = float(sigma_a), float(sigma_b), float(huber_k)
+    a.max_iters, a.rel_error, a.delta_norm = int(max_iters), float(rel_error), float(delta_norm)
+    a.sync_every = int(sync_every)
+    a.T_WCf_out, a.T_CkCf_out, a.info = _p(out_f), _p(out_r), _p(info)
+    a.workspace, a.workspace_bytes = _p(ws), ws.numel()
+    rc = getattr(_lib, fn)(ctypes.byref(a), _stream(dev))
+    _raise(rc, fn)
+    del ws  # stream-ordered by the caching allocator
+    return out_f, out_r, info
+
+
+def track_rays_sim3(Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma_ray, sigma_dist, huber_k, max_iters,
+                    rel_error, delta_norm, sync_every=5):
+    """Device form of FrameTracker.opt_pose_ray_dist_sim3 (tracker.py:173-214).
+    Returns (T_WCf [1,8], T_CkCf [1,8], info int32[8]); info[1] != 0 means the
+    Cholesky failed (the reference raises; tracker.py:91-93)."""
+    return _track("m3s_track_rays_sim3", Xf, Xk, T_WCf, T_WCk, Qk, valid, None, None, sigma_ray,
+                  sigma_dist, huber_k, max_iters, rel_error, delta_norm, sync_every=sync_every)
+
+
+def track_calib_sim3(Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size, sigma_pixel, sigma_depth,
+                     huber_k, max_iters, rel_error, delta_norm, pixel_border, z_eps, sync_every=5):
+    """Device form of FrameTracker.opt_pose_calib_sim3 (tracker.py:216-266);
+    Xf/Xk already constrained to rays, meas_k formed on device."""
+    return _track("m3s_track_calib_sim3", Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size,
+                  sigma_pixel, sigma_depth, huber_k, max_iters, rel_error, delta_norm,
+                  pixel_border=pixel_border, z_eps=z_eps, sync_every=sync_every)
+
+
+# -------------------------------------------------- stepwise (sharded) ---
+def gn_prepare(a, keep):
+    _raise(_lib.m3s_gn_prepare(ctypes.byref(a), _stream(keep["Xs"].device)), "m3s_gn_prepare")
+
+
+def gn_linearize(a, keep, edge_begin, edge_end, edge_sums):
+    _check(edge_sums, "edge_sums", torch.float64)
+    rc = _lib.m3s_gn_linearize(ctypes.byref(a), int(edge_begin), int(edge_end), _p(edge_sums),
+                               _stream(keep["Xs"].device))
+    _raise(rc, "m3s_gn_linearize")
+
+
+def gn_solve(a, keep, edge_sums):
+    _check(edge_sums, "edge_sums", torch.float64)
+    rc = _lib.m3s_gn_solve(ctypes.byref(a), _p(edge_sums), _stream(keep["Xs"].device))
+    _raise(rc, "m3s_gn_solve")

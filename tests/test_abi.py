@@ -1,0 +1,106 @@
+"""CPU-side checks of the C ABI boundary (no GPU needed):
+
+* libm3s_gn.so loads and exports every symbol include/m3s_gn.h declares;
+* the ctypes mirrors of m3s_gn_args / m3s_track_args have exactly the C
+  layout (a gcc-compiled probe prints sizeof/offsetof from the header);
+* workspace sizing is monotone and covers the documented sections;
+* the drop-in module exposes the reference's five entry points (gn.cpp:116-122)
+  and rejects CPU tensors / non-contiguous inputs before touching the device.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+HEADER = os.path.join(ROOT, "include", "m3s_gn.h")
+
+
+@pytest.fixture(scope="module")
+def be():
+    import mast3r_slam_backends as be
+
+    return be
+
+
+def test_library_exports_every_header_symbol(be):
+    src = open(HEADER).read()
+    declared = set(re.findall(r"\b(m3s_[a-z0-9_]+)\s*\(", src))
+    assert declared == set(be.EXPORTS)
+    for sym in declared:
+        assert hasattr(be._lib, sym), sym
+    assert "gfx950" in be.version()
+
+
+def test_reference_entry_points_present(be):
+    for f in ("gauss_newton_points", "gauss_newton_rays", "gauss_newton_calib", "iter_proj",
+              "refine_matches"):
+        assert callable(getattr(be, f))
+    with pytest.raises(NotImplementedError):
+        be.iter_proj(None, None, None, 10, 1e-8, 1e-6)
+
+
+PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "m3s_gn.h"
+#define F(T, m) printf(#T "." #m " %zu\n", offsetof(T, m))
+int main(void) {
+  printf("m3s_gn_args.size %zu\n", sizeof(m3s_gn_args));
+  F(m3s_gn_args, Twc); F(m3s_gn_args, K); F(m3s_gn_args, N); F(m3s_gn_args, mode);
+  F(m3s_gn_args, sigma_a); F(m3s_gn_args, z_eps); F(m3s_gn_args, max_iter);
+  F(m3s_gn_args, delta_thresh); F(m3s_gn_args, dx_out); F(m3s_gn_args, info);
+  F(m3s_gn_args, workspace); F(m3s_gn_args, workspace_bytes);
+  printf("m3s_track_args.size %zu\n", sizeof(m3s_track_args));
+  F(m3s_track_args, K); F(m3s_track_args, HW); F(m3s_track_args, height); F(m3s_track_args, z_eps);
+  F(m3s_track_args, huber_k); F(m3s_track_args, max_iters); F(m3s_track_args, sync_every);
+  F(m3s_track_args, T_WCf_out); F(m3s_track_args, workspace_bytes);
+  return 0;
+}
+"""
+
+
+def test_ctypes_struct_layout_matches_header(be, tmp_path):
+    c = tmp_path / "probe.c"
+    c.write_text(PROBE)
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode().split("\n")
+    got = dict(l.split() for l in out if l.strip())
+    mirror = {"m3s_gn_args": be.GnArgs, "m3s_track_args": be.TrackArgs}
+    for key, val in got.items():
+        t, m = key.split(".")
+        cls = mirror[t]
+        if m == "size":
+            assert int(val) == __import__("ctypes").sizeof(cls), key
+        else:
+            assert int(val) == getattr(cls, m).offset, key
+
+
+def test_workspace_size_monotone(be):
+    s1 = be._lib.m3s_gn_workspace_size(32, 262144, 96)
+    s2 = be._lib.m3s_gn_workspace_size(33, 262144, 96)
+    s3 = be._lib.m3s_gn_workspace_size(32, 262144, 200)
+    assert 0 < s1 < s2 and s1 < s3
+    # dense (N-1)*7 fp64 system dominates for large N
+    assert be._lib.m3s_gn_workspace_size(256, 262144, 1024) >= 8 * (7 * 255) ** 2
+    assert be._lib.m3s_track_workspace_size(262144) > 0
+
+
+def test_cpu_tensors_rejected(be):
+    N, HW, E = 3, 16, 2
+    Twc = torch.zeros(N, 8)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        be.gauss_newton_rays(Twc, torch.zeros(N, HW, 3), torch.zeros(N, HW, 1),
+                             torch.zeros(E, dtype=torch.long), torch.zeros(E, dtype=torch.long),
+                             torch.zeros(E, HW, dtype=torch.long),
+                             torch.zeros(E, HW, 1, dtype=torch.bool), torch.zeros(E, HW, 1),
+                             0.003, 10.0, 0.0, 1.5, 10, 1e-8)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        be.gauss_newton_rays(Twc.t(), torch.zeros(N, HW, 3), torch.zeros(N, HW, 1),
+                             torch.zeros(E, dtype=torch.long), torch.zeros(E, dtype=torch.long),
+                             torch.zeros(E, HW, dtype=torch.long),
+                             torch.zeros(E, HW, 1, dtype=torch.bool), torch.zeros(E, HW, 1),
+                             0.003, 10.0, 0.0, 1.5, 10, 1e-8)

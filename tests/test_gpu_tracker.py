@@ -1,0 +1,97 @@
+"""GPU tracker GN (track_rays_sim3 / track_calib_sim3) vs the reference
+tracker's own outputs (tests/golden/tracker_*.npz) and vs the numpy oracle at
+the C1 shape (512x384).
+
+Tolerance: 1e-5 + 1e-4 * sum of GN step lengths on every pose
+component; identical iteration count (the convergence rule is reproduced).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import tracker_oracle as tro  # noqa: E402
+
+DEV = torch.device("cuda:0")
+CFG = tro.TRACKING_CFG
+
+
+@pytest.fixture(scope="module")
+def be():
+    import mast3r_slam_backends as be
+
+    return be
+
+
+def pose_tol(taus):
+    return 1e-5 + 1e-4 * float(np.linalg.norm(np.asarray(taus, np.float64), axis=-1).sum())
+
+
+def run_gpu(be, d, max_iters=None, sync_every=5):
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k])).to(DEV)  # noqa: E731
+    mi = int(d["max_iters"]) if max_iters is None else max_iters
+    if int(d["calib"]):
+        out = be.track_calib_sim3(t("Xf"), t("Xk"), t("T_WCf_init"), t("T_WCk"), t("Qk"), t("valid"),
+                                  t("K"), (int(d["H"]), int(d["W"])), CFG["sigma_pixel"],
+                                  CFG["sigma_depth"], CFG["huber"], mi, CFG["rel_error"],
+                                  CFG["delta_norm"], CFG["pixel_border"], CFG["depth_eps"],
+                                  sync_every=sync_every)
+    else:
+        out = be.track_rays_sim3(t("Xf"), t("Xk"), t("T_WCf_init"), t("T_WCk"), t("Qk"), t("valid"),
+                                 CFG["sigma_ray"], CFG["sigma_dist"], CFG["huber"], mi,
+                                 CFG["rel_error"], CFG["delta_norm"], sync_every=sync_every)
+    torch.cuda.synchronize()
+    return [o.cpu().numpy() for o in out]
+
+
+@pytest.mark.parametrize(
+    "name",
+    ["tracker_rays_64x48", "tracker_calib_64x48", "tracker_rays_identity_64x48",
+     "tracker_calib_identity_64x48", "onestep_rays_identity_32x24", "onestep_calib_identity_32x24"],
+)
+@pytest.mark.parametrize("sync_every", [0, 1, 5])
+def test_tracker_matches_reference_fixture(be, golden_dir, name, sync_every):
+    d = dict(np.load(os.path.join(golden_dir, name + ".npz")))
+    T_WCf, T_CkCf, info = run_gpu(be, d, sync_every=sync_every)
+    assert info[1] == 0
+    assert info[0] == int(d["n_iters"])
+    tol = pose_tol(d["tau_iter"])
+    np.testing.assert_allclose(T_WCf[0], d["T_WCf"][0], atol=tol)
+    np.testing.assert_allclose(T_CkCf[0], d["T_CkCf"][0], atol=tol)
+
+
+def test_tracker_cholesky_failure_reported(be, golden_dir):
+    d = dict(np.load(os.path.join(golden_dir, "tracker_rays_allinvalid_32x24.npz")))
+    T_WCf, T_CkCf, info = run_gpu(be, d)
+    assert info[1] == 1  # the reference raises -> track() reports failure
+
+
+@pytest.mark.parametrize("calib", [False, True])
+def test_tracker_c1_shape_matches_oracle(be, calib):
+    """C1 shape (512x384), natural termination, vs the numpy restatement."""
+    from mast3r_slam_amd import synthetic
+
+    p = synthetic.make_pair(384, 512, seed=1001)
+    Xf, Xk = p.Xf.numpy(), p.Xk.numpy()
+    rec = []
+    if calib:
+        K = p.K.numpy()
+        Xf = tro.constrain_points_to_ray((384, 512), Xf, K)
+        Xk = tro.constrain_points_to_ray((384, 512), Xk, K)
+        meas, vm = tro.calib_meas(Xk, (384, 512), CFG["depth_eps"])
+        T_f, T_r, it = tro.track_calib(Xf, Xk, p.T_WCf_init.data.numpy(), p.T_WCk.data.numpy(),
+                                       p.Qk.numpy(), p.valid.numpy(), meas, vm, K, (384, 512),
+                                       dict(CFG), rec)
+    else:
+        T_f, T_r, it = tro.track_rays(Xf, Xk, p.T_WCf_init.data.numpy(), p.T_WCk.data.numpy(),
+                                      p.Qk.numpy(), p.valid.numpy(), dict(CFG), rec)
+    d = dict(calib=int(calib), Xf=Xf, Xk=Xk, T_WCf_init=p.T_WCf_init.data.numpy(),
+             T_WCk=p.T_WCk.data.numpy(), Qk=p.Qk.numpy(), valid=p.valid.numpy(), K=p.K.numpy(),
+             H=384, W=512, max_iters=CFG["max_iters"])
+    T_WCf, T_CkCf, info = run_gpu(be, d)
+    assert info[0] == it
+    tol = pose_tol([r["tau"][0] for r in rec])
+    np.testing.assert_allclose(T_WCf[0], T_f[0], atol=tol)

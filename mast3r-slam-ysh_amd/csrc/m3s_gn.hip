@@ -48,9 +48,11 @@ constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sw
 constexpr int kTargetBlocks = 2048;  // ~8 blocks per CU on 256 CUs
 constexpr int kMaxSmallNp = 224;     // register Cholesky limit (n + 1 <= 7 * 32)
 constexpr int kCholThreads = 512;    // 16 x 32 thread grid
+constexpr int64_t kMaxLd = 8192;     // tiled path: back-substitution keeps x in LDS
 
 // workspace-resident flags (int32)
 constexpr int kFlagStop = 0;  // set when converged / bad input: later launches no-op
+constexpr int kFlagFail = 1;  // set by the tiled Cholesky on a non-positive pivot (per iteration)
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -70,8 +72,12 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 }
 
 struct Layout {
-  size_t flags, rank_i, rank_j, first, partials, edge_sums, H, g, total;
+  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, total;
+  int64_t n, ld;  // system size 7(N-1); leading dim of the RHS-augmented matrix
 };
+
+constexpr int kTile = 64;  // tiled Cholesky tile (large systems)
+inline int64_t aug_ld(int64_t n) { return (n + 1 + kTile - 1) / kTile * kTile; }
 
 inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   Layout L;
@@ -90,10 +96,10 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(float) * kNP * (size_t)max_partials, 256);
   L.edge_sums = off;
   off = align_up(off + sizeof(double) * kNP * (size_t)(E + 1), 256);
-  L.H = off;
-  off = align_up(off + sizeof(double) * (size_t)(n * n + 1), 256);
-  L.g = off;
-  off = align_up(off + sizeof(double) * (size_t)(n + 1), 256);
+  L.n = n;
+  L.ld = aug_ld(n);
+  L.A = off;
+  off = align_up(off + sizeof(double) * (size_t)(L.ld * L.ld), 256);
   L.total = off;
   (void)HW;
   return L;
@@ -231,7 +237,8 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
     Cs_i = A.Cs + (size_t)ri * HW;
     Cs_j = A.Cs + (size_t)rj * HW;
   }
-  const size_t eoff = TRACK ? 0 : (size_t)e * HW;
+  // edge data (idx/valid/Q) is addressed relative to the launch's edge slice
+  const size_t eoff = TRACK ? 0 : (size_t)e_loc * HW;
   const int64_t* __restrict__ idx = TRACK ? nullptr : A.idx + eoff;
   const uint8_t* __restrict__ valid = A.valid + eoff;
   const float* __restrict__ Qe = A.Q + eoff;
@@ -308,18 +315,31 @@ __global__ void edge_reduce_kernel(const float *__restrict__ partials, int64_t c
 }
 
 // ------------------------------------------------------------- assemble --
-// Block r owns rows [7r, 7r+7) of the (N-1)*7 system (pose rank r+1).
+// RHS-augmented system in A (row-major, leading dim ld = roundup(n+1, 64)):
+//   A[0:n, 0:n] = H,  A[n, 0:n] = g^T,  rows > n = identity padding.
+// Block r < N-1 owns rows [7r, 7r+7) and the entries A[n, 7r:7r+7); block
+// N-1 initialises row n's tail and the padding rows.
 __global__ void __launch_bounds__(256) assemble_kernel(const double *__restrict__ edge_sums,
                                                        const int32_t *__restrict__ rank_i,
                                                        const int32_t *__restrict__ rank_j, int64_t E,
                                                        const float *__restrict__ Twc, int64_t n,
-                                                       double *__restrict__ H, double *__restrict__ g,
+                                                       int64_t ld, double *__restrict__ A,
                                                        const int32_t *__restrict__ stop) {
   if (*stop) return;
   const int r = blockIdx.x;
   const int t = threadIdx.x;
+  const int nb = (int)(n / 7);
+  if (r == nb) {  // padding block
+    for (int64_t k = n + t; k < ld; k += blockDim.x) A[(size_t)n * ld + k] = 0.0;
+    for (int64_t k = t; k < (ld - n - 1) * ld; k += blockDim.x) {
+      const int64_t i = n + 1 + k / ld, j = k % ld;
+      A[(size_t)i * ld + j] = (i == j) ? 1.0 : 0.0;
+    }
+    return;
+  }
   __shared__ double M[7][7], Lm[7][7], T1[7][7], Hjj[7][7], l[7], gj[7];
-  for (int64_t k = t; k < 7 * n; k += blockDim.x) H[(size_t)7 * r * n + k] = 0.0;
+  for (int64_t k = t; k < 7 * ld; k += blockDim.x) A[(size_t)7 * r * ld + k] = 0.0;
+  double *g = A + (size_t)n * ld;
   if (t < 7) g[7 * r + t] = 0.0;
   __syncthreads();
   for (int64_t e = 0; e < E; e++) {
@@ -355,7 +375,7 @@ __global__ void __launch_bounds__(256) assemble_kernel(const double *__restrict_
     __syncthreads();
     if (t < 49) {
       const int a = t / 7, c = t % 7;
-      double *row = H + (size_t)(7 * r + a) * n;
+      double *row = A + (size_t)(7 * r + a) * ld;
       const double h = Hjj[a][c];
       // edge (i -> j): Hs[0]=Hs[3]=Hjj at (i,i),(j,j); Hs[1]=Hs[2]=-Hjj off-diagonal
       if (i == r) {
@@ -375,14 +395,249 @@ __global__ void __launch_bounds__(256) assemble_kernel(const double *__restrict_
   }
 }
 
+// dx = -x, retraction of poses 1..N-1, ||dx|| test, info update. x in LDS.
+// Called by one whole block (blockDim.x threads, multiple of 64).
+__device__ void finish_step(const double *xs, float *dxs, float *nrm, int n, float *Twc, int64_t N,
+                            float *dx_out, int32_t *info, int32_t *stop, float delta_thresh) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  float part = 0.0f;
+  for (int k = tid; k < n; k += nt) {
+    const float v = -(float)xs[k];
+    dxs[k] = v;
+    dx_out[k] = v;
+    part += v * v;
+  }
+  part = wave_sum(part);
+  if ((tid & 63) == 0) nrm[tid >> 6] = part;
+  __syncthreads();
+  for (int p = tid; p < (int)(N - 1); p += nt) {
+    const Sim3f T = load_sim3(Twc + 8 * (size_t)(p + 1));
+    store_sim3(Twc + 8 * (size_t)(p + 1), retract(dxs + 7 * p, T));
+  }
+  if (tid == 0) {
+    float s = 0.0f;
+    for (int w = 0; w < nt / 64; w++) s += nrm[w];
+    info[M3S_INFO_ITERS] += 1;
+    if (sqrtf(s) < delta_thresh) {
+      info[M3S_INFO_CONVERGED] = 1;
+      stop[0] = 1;
+    }
+  }
+}
+
+// LLT failure: dx = 0 (poses unchanged), ||0|| < delta stops like the reference
+__device__ void fail_step(int n, float *dx_out, int32_t *info, int32_t *stop, float delta_thresh) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) dx_out[k] = 0.0f;
+  if (threadIdx.x == 0) {
+    info[M3S_INFO_ITERS] += 1;
+    info[M3S_INFO_SOLVE_FAIL] += 1;
+    if (0.0f < delta_thresh) {
+      info[M3S_INFO_CONVERGED] = 1;
+      stop[0] = 1;
+    }
+  }
+}
+
+// ------------------------------------------------- tiled dense Cholesky --
+// For systems beyond the register-resident kernel. Right-looking, 64x64
+// fp64 tiles, three launches per tile column: factor the diagonal tile,
+// triangular-solve the panel below it, update the trailing lower tiles.
+// Thread (ty, tx) of a 16x16 grid owns tile entries (ty + 16a, tx + 16b).
+__global__ void __launch_bounds__(256) potrf_tile_kernel(double *__restrict__ A, int64_t ld, int64_t n,
+                                                         int kb, int32_t *__restrict__ flags) {
+  if (flags[kFlagStop] || flags[kFlagFail]) return;
+  __shared__ double cb[2][kTile];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double *T = A + (size_t)kb * kTile * ld + (size_t)kb * kTile;
+  double v[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) v[a][b] = T[(size_t)(ty + 16 * a) * ld + tx + 16 * b];
+  int step = 0;
+#pragma unroll
+  for (int cbk = 0; cbk < 4; cbk++) {
+    for (int cc = 0; cc < 16; cc++) {
+      const int c = 16 * cbk + cc;
+      if ((int64_t)kb * kTile + c >= n) break;  // augmented row / padding: nothing to factor
+      double *col = cb[step & 1];
+      if (tx == cc) {
+#pragma unroll
+        for (int a = 0; a < 4; a++) col[ty + 16 * a] = (ty + 16 * a >= c) ? v[a][cbk] : 0.0;
+      }
+      __syncthreads();
+      const double d = col[c];
+      if (!(d > 0.0)) {
+        if (threadIdx.x == 0) flags[kFlagFail] = 1;
+        return;  // uniform: every thread read the same pivot
+      }
+      const double inv = 1.0 / sqrt(d);
+      double lj[4];
+#pragma unroll
+      for (int b = 0; b < 4; b++) lj[b] = col[tx + 16 * b] * inv;
+#pragma unroll
+      for (int a = 0; a < 4; a++) {
+        const double li = col[ty + 16 * a] * inv;
+#pragma unroll
+        for (int b = 0; b < 4; b++) v[a][b] -= li * lj[b];
+        if (tx == cc) v[a][cbk] = li;
+      }
+      step++;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) T[(size_t)(ty + 16 * a) * ld + tx + 16 * b] = v[a][b];
+}
+
+// X L_kk^T = A_ik for the row tiles i > kb (block b -> i = kb + 1 + b)
+__global__ void __launch_bounds__(256) trsm_tile_kernel(double *__restrict__ A, int64_t ld, int64_t n,
+                                                        int kb, int32_t *__restrict__ flags) {
+  if (flags[kFlagStop] || flags[kFlagFail]) return;
+  __shared__ double Lk[kTile][kTile + 1];
+  __shared__ double cb[2][kTile];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int i = kb + 1 + blockIdx.x;
+  const double *D = A + (size_t)kb * kTile * ld + (size_t)kb * kTile;
+  for (int k = threadIdx.x; k < kTile * kTile; k += 256) Lk[k / kTile][k % kTile] = D[(size_t)(k / kTile) * ld + k % kTile];
+  double *T = A + (size_t)i * kTile * ld + (size_t)kb * kTile;
+  double v[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) v[a][b] = T[(size_t)(ty + 16 * a) * ld + tx + 16 * b];
+  __syncthreads();
+  int step = 0;
+#pragma unroll
+  for (int cbk = 0; cbk < 4; cbk++) {
+    for (int cc = 0; cc < 16; cc++) {
+      const int c = 16 * cbk + cc;
+      if ((int64_t)kb * kTile + c >= n) break;
+      double *col = cb[step & 1];
+      const double inv = 1.0 / Lk[c][c];
+      if (tx == cc) {
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+          v[a][cbk] *= inv;
+          col[ty + 16 * a] = v[a][cbk];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int s = tx + 16 * b;
+        if (s > c) {
+          const double l = Lk[s][c];
+#pragma unroll
+          for (int a = 0; a < 4; a++) v[a][b] -= col[ty + 16 * a] * l;
+        }
+      }
+      step++;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) T[(size_t)(ty + 16 * a) * ld + tx + 16 * b] = v[a][b];
+}
+
+// A_ij -= L_ik L_jk^T for kb < j <= i < nt (block -> packed lower index)
+__global__ void __launch_bounds__(256) update_tiles_kernel(double *__restrict__ A, int64_t ld, int kb,
+                                                           const int32_t *__restrict__ flags) {
+  if (flags[kFlagStop] || flags[kFlagFail]) return;
+  __shared__ double Li[kTile][kTile + 1];
+  __shared__ double Lj[kTile][kTile + 1];
+  const int t = blockIdx.x;
+  int ip = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((ip + 1) * (ip + 2) / 2 <= t) ip++;
+  while (ip * (ip + 1) / 2 > t) ip--;
+  const int jp = t - ip * (ip + 1) / 2;
+  const int i = kb + 1 + ip, j = kb + 1 + jp;
+  const double *Pi = A + (size_t)i * kTile * ld + (size_t)kb * kTile;
+  const double *Pj = A + (size_t)j * kTile * ld + (size_t)kb * kTile;
+  for (int k = threadIdx.x; k < kTile * kTile; k += 256) {
+    Li[k / kTile][k % kTile] = Pi[(size_t)(k / kTile) * ld + k % kTile];
+    Lj[k / kTile][k % kTile] = Pj[(size_t)(k / kTile) * ld + k % kTile];
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[4][4] = {};
+  for (int s = 0; s < kTile; s++) {
+    double li[4], lj[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) li[a] = Li[ty + 16 * a][s];
+#pragma unroll
+    for (int b = 0; b < 4; b++) lj[b] = Lj[tx + 16 * b][s];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) acc[a][b] += li[a] * lj[b];
+  }
+  double *T = A + (size_t)i * kTile * ld + (size_t)j * kTile;
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) T[(size_t)(ty + 16 * a) * ld + tx + 16 * b] -= acc[a][b];
+}
+
+// L^T x = y (y = row n of the factor), tiles from the bottom; then the step.
+__global__ void __launch_bounds__(1024) backsolve_kernel(const double *__restrict__ A, int64_t ld, int n,
+                                                         float *__restrict__ Twc, int64_t N,
+                                                         float *__restrict__ dx_out, int32_t *__restrict__ info,
+                                                         int32_t *__restrict__ flags, float delta_thresh) {
+  if (flags[kFlagStop]) return;
+  const int failed = flags[kFlagFail];
+  __syncthreads();  // every wave has read the flag before thread 0 clears it
+  if (failed) {
+    fail_step(n, dx_out, info, flags + kFlagStop, delta_thresh);
+    if (threadIdx.x == 0) flags[kFlagFail] = 0;
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double *rhs = smem;              // ld
+  double *D = smem + ld;           // kTile x (kTile+1)
+  float *dxs = reinterpret_cast<float *>(D + kTile * (kTile + 1));  // ld floats
+  __shared__ float nrm[16];
+  const int tid = threadIdx.x;
+  for (int k = tid; k < ld; k += blockDim.x) rhs[k] = (k < n) ? A[(size_t)n * ld + k] : 0.0;
+  const int nt = (n + kTile - 1) / kTile;
+  for (int kb = nt - 1; kb >= 0; kb--) {
+    __syncthreads();
+    const double *T = A + (size_t)kb * kTile * ld + (size_t)kb * kTile;
+    for (int k = tid; k < kTile * kTile; k += blockDim.x) D[(k / kTile) * (kTile + 1) + k % kTile] = T[(size_t)(k / kTile) * ld + k % kTile];
+    __syncthreads();
+    if (tid < 64) {  // one wave: L_kk^T x = rhs_kb
+      double r = rhs[kb * kTile + tid];
+      double x = 0.0;
+      for (int c = kTile - 1; c >= 0; c--) {
+        if (kb * kTile + c >= n) continue;  // uniform
+        const double xc = __shfl(r, c, 64) / D[c * (kTile + 1) + c];
+        if (tid < c) r -= D[c * (kTile + 1) + tid] * xc;
+        if (tid == c) x = xc;
+      }
+      rhs[kb * kTile + tid] = (kb * kTile + tid < n) ? x : 0.0;  // rhs now holds x for this tile
+    }
+    __syncthreads();
+    // rhs_j -= sum_r L[kb*64 + r][j] x_r for all j < kb*64
+    for (int j = tid; j < kb * kTile; j += blockDim.x) {
+      double s = 0.0;
+      for (int r = 0; r < kTile; r++) s += A[(size_t)(kb * kTile + r) * ld + j] * rhs[kb * kTile + r];
+      rhs[j] -= s;
+    }
+  }
+  __syncthreads();
+  finish_step(rhs, dxs, nrm, n, Twc, N, dx_out, info, flags + kFlagStop, delta_thresh);
+}
+
 // ------------------------------------------------- small dense Cholesky --
 // Thread (tr, tc) of a 16 x 32 grid owns A[lr*16 + tr][lc*32 + tc]. The RHS g
 // is appended as row n, so the factor's row n is y = L^-1 g. After the loop
 // the registers hold L (lower triangle). NBC = column blocks of 32.
 template <int NBC>
 __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
-    const double *__restrict__ H, const double *__restrict__ g, int n, float *__restrict__ Twc,
-    int64_t N, float *__restrict__ dx_out, int32_t *__restrict__ info, int32_t *__restrict__ stop,
+    const double *__restrict__ Aug, int64_t ld, int n, float *__restrict__ Twc, int64_t N,
+    float *__restrict__ dx_out, int32_t *__restrict__ info, int32_t *__restrict__ stop,
     float delta_thresh) {
   constexpr int NBR = 2 * NBC;
   if (*stop) return;
@@ -395,7 +650,6 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
   __shared__ double dblk[32][33];
   __shared__ float dxs[32 * NBC];
   __shared__ float nrm[kCholThreads / 64];
-  __shared__ int failed_s;
 
   double A[NBR][NBC];
 #pragma unroll
@@ -403,17 +657,9 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
 #pragma unroll
     for (int lc = 0; lc < NBC; lc++) {
       const int i = lr * 16 + tr, j = lc * 32 + tc;
-      double v;
-      if (i < n && j < n)
-        v = H[(size_t)i * n + j];
-      else if (i == n && j < n)
-        v = g[j];
-      else
-        v = (i == j) ? 1.0 : 0.0;
-      A[lr][lc] = v;
+      A[lr][lc] = (i <= n && j < n) ? Aug[(size_t)i * ld + j] : ((i == j) ? 1.0 : 0.0);
     }
   for (int k = tid; k < 32 * NBC; k += kCholThreads) xbuf[k] = 0.0, ybuf[k] = 0.0;
-  if (tid == 0) failed_s = 0;
   bool failed = false;
   int step = 0;
 
@@ -453,17 +699,8 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
     }
   }
 
-  if (failed) {
-    // every thread saw the same pivot; write dx = 0
-    for (int k = tid; k < (int)(7 * (N - 1)); k += kCholThreads) dx_out[k] = 0.0f;
-    if (tid == 0) {
-      info[M3S_INFO_ITERS] += 1;
-      info[M3S_INFO_SOLVE_FAIL] += 1;
-      if (0.0f < delta_thresh) {
-        info[M3S_INFO_CONVERGED] = 1;
-        stop[0] = 1;
-      }
-    }
+  if (failed) {  // every thread saw the same pivot
+    fail_step(n, dx_out, info, stop, delta_thresh);
     return;
   }
 
@@ -512,31 +749,7 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
     }
     __syncthreads();
   }
-
-  // dx = -x (float), retraction of poses 1..N-1, ||dx||
-  float part = 0.0f;
-  for (int k = tid; k < n; k += kCholThreads) {
-    const float v = -(float)xbuf[k];
-    dxs[k] = v;
-    dx_out[k] = v;
-    part += v * v;
-  }
-  part = wave_sum(part);
-  if ((tid & 63) == 0) nrm[tid >> 6] = part;
-  __syncthreads();
-  for (int p = tid; p < (int)(N - 1); p += kCholThreads) {
-    const Sim3f T = load_sim3(Twc + 8 * (size_t)(p + 1));
-    store_sim3(Twc + 8 * (size_t)(p + 1), retract(dxs + 7 * p, T));
-  }
-  if (tid == 0) {
-    float s = 0.0f;
-    for (int w = 0; w < kCholThreads / 64; w++) s += nrm[w];
-    info[M3S_INFO_ITERS] += 1;
-    if (sqrtf(s) < delta_thresh) {
-      info[M3S_INFO_CONVERGED] = 1;
-      stop[0] = 1;
-    }
-  }
+  finish_step(xbuf, dxs, nrm, n, Twc, N, dx_out, info, stop, delta_thresh);
 }
 
 // ---------------------------------------------------------------- host --
@@ -630,7 +843,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xs, 16) && vec_ok(a->Cs, 16) && vec_ok(a->Q, 16) &&
                    vec_ok(a->idx_ii2jj, 16) && vec_ok(a->valid_match, 4);
   int rc = dispatch_linearize<false>(a->mode, L, E_loc * L.chunks, vec, st);
-  if (rc) return rc;
+  if (rc || !edge_sums) return rc;  // NULL edge_sums: partials only (kernel timing)
   edge_reduce_kernel<<<dim3((unsigned)E_loc), dim3(64), 0, st>>>(L.partials, L.chunks, edge_sums, L.stop);
   return launch_ok();
 }
@@ -638,35 +851,52 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
-  int32_t *stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
-  const int64_t n = 7 * (a->N - 1);
+  int32_t *flags = at<int32_t>(ws, Ly.flags);
+  int32_t *stop = flags + kFlagStop;
+  const int64_t n = Ly.n, ld = Ly.ld;
   if (a->N <= 1) return M3S_OK;
-  double *H = at<double>(ws, Ly.H), *g = at<double>(ws, Ly.g);
-  assemble_kernel<<<dim3((unsigned)(a->N - 1)), dim3(256), 0, st>>>(
-      edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, H, g, stop);
+  double *A = at<double>(ws, Ly.A);
+  assemble_kernel<<<dim3((unsigned)a->N), dim3(256), 0, st>>>(
+      edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, ld, A, stop);
   int rc = launch_ok();
   if (rc) return rc;
-  const int np = (int)n + 1;
-  if (np > kMaxSmallNp) return M3S_ETOOLARGE;
-  const int nbc = (np + 31) / 32;
   float *dx = a->dx_out;
-#define M3S_CHOL(NB)                                                                                    \
-  case NB:                                                                                              \
-    chol_small_kernel<NB><<<dim3(1), dim3(kCholThreads), 0, st>>>(H, g, (int)n, a->Twc, a->N, dx,     \
-                                                                 a->info, stop, a->delta_thresh); \
+  const int np = (int)n + 1;
+  if (np <= kMaxSmallNp) {
+    const int nbc = (np + 31) / 32;
+#define M3S_CHOL(NB)                                                                                   \
+  case NB:                                                                                             \
+    chol_small_kernel<NB><<<dim3(1), dim3(kCholThreads), 0, st>>>(A, ld, (int)n, a->Twc, a->N, dx, \
+                                                                 a->info, stop, a->delta_thresh);  \
     break;
-  switch (nbc) {
-    M3S_CHOL(1)
-    M3S_CHOL(2)
-    M3S_CHOL(3)
-    M3S_CHOL(4)
-    M3S_CHOL(5)
-    M3S_CHOL(6)
-    M3S_CHOL(7)
-    default:
-      return M3S_ETOOLARGE;
-  }
+    switch (nbc) {
+      M3S_CHOL(1)
+      M3S_CHOL(2)
+      M3S_CHOL(3)
+      M3S_CHOL(4)
+      M3S_CHOL(5)
+      M3S_CHOL(6)
+      M3S_CHOL(7)
+      default:
+        return M3S_ETOOLARGE;
+    }
 #undef M3S_CHOL
+    return launch_ok();
+  }
+  // tiled path
+  const int nt = (int)(ld / kTile);
+  for (int kb = 0; kb < nt; kb++) {
+    if ((int64_t)kb * kTile >= n) break;
+    potrf_tile_kernel<<<1, 256, 0, st>>>(A, ld, n, kb, flags);
+    const int m = nt - kb - 1;
+    if (m > 0) {
+      trsm_tile_kernel<<<m, 256, 0, st>>>(A, ld, n, kb, flags);
+      update_tiles_kernel<<<m * (m + 1) / 2, 256, 0, st>>>(A, ld, kb, flags);
+    }
+    if ((rc = launch_ok())) return rc;
+  }
+  const size_t smem = sizeof(double) * (size_t)(ld + kTile * (kTile + 1)) + sizeof(float) * (size_t)ld;
+  backsolve_kernel<<<1, 1024, smem, st>>>(A, ld, (int)n, a->Twc, a->N, dx, a->info, flags, a->delta_thresh);
   return launch_ok();
 }
 
@@ -695,7 +925,7 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   int rc = check_args(a);
   if (rc) return rc;
   if (a->mode != mode) return M3S_EINVAL;
-  if (a->N > 1 && 7 * (a->N - 1) + 1 > kMaxSmallNp) return M3S_ETOOLARGE;
+  if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
   hipStream_t st = S(stream);
   ResidualParams P = make_params(a);
   if (mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, st))) return rc;
@@ -882,7 +1112,7 @@ int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end,
                      void *stream) {
   int rc = check_args(a);
   if (rc) return rc;
-  if (edge_begin < 0 || edge_end > a->E || edge_begin > edge_end || !edge_sums) return M3S_EINVAL;
+  if (edge_begin < 0 || edge_end > a->E || edge_begin > edge_end) return M3S_EINVAL;
   ResidualParams P = make_params(a);
   if (a->mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, S(stream)))) return rc;
   return gn_linearize_impl(a, P, edge_begin, edge_end, edge_sums, S(stream));
@@ -892,6 +1122,7 @@ int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
   int rc = check_args(a);
   if (rc) return rc;
   if (!edge_sums) return M3S_EINVAL;
+  if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
   return gn_solve_impl(a, edge_sums, S(stream));
 }
 

@@ -172,9 +172,14 @@ def make_graph(
     edges=None,
     kf_ids=None,
     noise=True,
+    edge_range=None,
 ) -> Graph:
     """Build a synthetic FactorGraph problem (already in the two-way edge form
-    that ``FactorGraph.prep_two_way_edges`` hands to the backend)."""
+    that ``FactorGraph.prep_two_way_edges`` hands to the backend).
+
+    ``edge_range=(b, e)`` builds idx/valid/Q only for directed edges [b, e)
+    (a rank's shard); every per-edge random draw is seeded by the edge index,
+    so shards are slices of the full graph. ii/jj are always the full lists."""
     gen = torch.Generator().manual_seed(seed)
     K = intrinsics(H, W, device)
     T_gt = loop_trajectory(N, gen, device=device)
@@ -188,8 +193,8 @@ def make_graph(
         Xs = X_clean.contiguous()
     Cs = (1.0 + torch.exp(1.0 + 0.5 * torch.randn(N, H * W, 1, generator=gen))).to(device)
 
-    if edges is None:
-        ii_u, jj_u = make_edges(N, gen, loop_frac)
+    if edges is None:  # own generator: the edge set must not depend on H x W
+        ii_u, jj_u = make_edges(N, torch.Generator().manual_seed(seed + 7), loop_frac)
     else:
         ii_u, jj_u = edges
     # two-way edges: (i,j) then (j,i) — global_opt.py:104-110
@@ -197,15 +202,21 @@ def make_graph(
     jj_dir = jj_u + ii_u
     E = len(ii_dir)
     HW = H * W
-    idx = torch.empty(E, HW, dtype=torch.int64, device=device)
-    valid = torch.empty(E, HW, 1, dtype=torch.bool, device=device)
-    for e, (i, j) in enumerate(zip(ii_dir, jj_dir)):
+    eb, ee = (0, E) if edge_range is None else (max(0, edge_range[0]), min(E, edge_range[1]))
+    n_loc = max(ee - eb, 0)
+    idx = torch.empty(n_loc, HW, dtype=torch.int64, device=device)
+    valid = torch.empty(n_loc, HW, 1, dtype=torch.bool, device=device)
+    Q = torch.empty(n_loc, HW, 1, dtype=torch.float32, device=device)
+    for k in range(n_loc):
+        e = eb + k
+        i, j = ii_dir[e], jj_dir[e]
         Xw_j = T_gt[j : j + 1].act(X_clean[j])
         ie, ve = correspondences(Xw_j, T_gt[i : i + 1], depth[i], K, H, W)
-        idx[e] = ie
-        valid[e, :, 0] = ve
-    Q = (1.0 + torch.exp(0.3 + 0.8 * torch.randn(E, HW, 1, generator=gen))).to(device)
-    T_init = perturb(T_gt, gen) if noise else T_gt.clone()
+        idx[k] = ie
+        valid[k, :, 0] = ve
+        ge = torch.Generator().manual_seed(seed * 1000003 + e)
+        Q[k] = (1.0 + torch.exp(0.3 + 0.8 * torch.randn(HW, 1, generator=ge))).to(device)
+    T_init = perturb(T_gt, torch.Generator().manual_seed(seed + 13)) if noise else T_gt.clone()
     if kf_ids is None:
         kf_ids = torch.arange(N, dtype=torch.int64)
     kf_ids = torch.as_tensor(kf_ids, dtype=torch.int64)

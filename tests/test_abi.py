@@ -81,7 +81,7 @@ def test_ctypes_struct_layout_matches_header(be, tmp_path):
 
 def test_workspace_size_monotone(be):
     s1 = be._lib.m3s_gn_workspace_size(32, 262144, 96)
-    s2 = be._lib.m3s_gn_workspace_size(33, 262144, 96)
+    s2 = be._lib.m3s_gn_workspace_size(48, 262144, 96)
     s3 = be._lib.m3s_gn_workspace_size(32, 262144, 200)
     assert 0 < s1 < s2 and s1 < s3
     # dense (N-1)*7 fp64 system dominates for large N

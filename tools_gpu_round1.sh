@@ -1,0 +1,16 @@
+#!/bin/bash
+# GPU-box script: parity tests, bench, rocprofv3 kernel stats. Each GPU step
+# has its own time limit; any failure ends the script.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 600 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 600 python bench.py > $OUT/bench1.json 2> $OUT/bench1.err || { echo "bench failed"; tail -30 $OUT/bench1.err; exit 1; }
+cat $OUT/bench1.json
+cd /tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/prof1 -o run --output-format csv -- python $R/bench.py --steps 5 --warmup 1 --no-cpu --no-tracker > $OUT/prof1_bench.json 2> $OUT/prof1.err || { echo "rocprof failed"; tail -30 $OUT/prof1.err; exit 1; }
+find $OUT/prof1 -name "*stats*" | head

@@ -210,9 +210,11 @@ __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x)
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float flog(float x) { return __logf(x); }
 
+// branch-free: both sides are always computed, then selected
 __device__ __forceinline__ float huber_w(float r, float k) {
   const float a = fabsf(r);
-  return a < k ? 1.0f : k * frcp(a);
+  const float o = k * frcp(a);
+  return a < k ? 1.0f : o;
 }
 
 // ------------------------------------------------ normal-eq accumulation --
@@ -288,9 +290,12 @@ __device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &
     accum_row<kRayD>(acc, a3, w3, e3);
   } else if (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
     const bool vz = (Y[2] > P.z_eps) && (Xi[2] > P.z_eps);
-    const float zinv = vz ? frcp(Y[2]) : 0.0f;
-    const float lzj = vz ? flog(Y[2]) : 0.0f;
-    const float lzi = vz ? flog(Xi[2]) : 0.0f;
+    // computed unconditionally and selected (no exec-mask branches); the
+    // unselected values may be inf/NaN and never reach the sums
+    const float zr = frcp(Y[2]), lj_ = flog(Y[2]), li_ = flog(Xi[2]);
+    const float zinv = vz ? zr : 0.0f;
+    const float lzj = vz ? lj_ : 0.0f;
+    const float lzi = vz ? li_ : 0.0f;
     const float x = Y[0] * zinv, y = Y[1] * zinv;
     const float u = P.fx * x + P.cx, v = P.fy * y + P.cy;
     const bool vu = (u > P.border) && (u < (float)P.width - 1.0f - P.border);

@@ -214,8 +214,73 @@ __device__ __forceinline__ void do_pixel(float *acc, const LinArgs &A, const Sim
   pixel_contrib<MODE>(acc, A.P, Xi, Y, ok, q, u_t, v_t);
 }
 
+// Block reduction of the 36 per-thread sums through LDS: every thread stores
+// its row (16-B stores), then 252 threads each add a 1/7 slice of one column,
+// then 36 threads combine the 7 slices. ~100 instructions per thread instead
+// of 36 wave-wide shuffle trees.
+#ifndef M3S_RED_PASSES
+#define M3S_RED_PASSES 2  // 1: one 36 KB LDS pass; 2: two 18 KB passes (more blocks per CU)
+#endif
+constexpr int kRedW = kNP / M3S_RED_PASSES;  // values per pass (36 or 18)
+__device__ __forceinline__ void block_reduce_store(const float *acc, float *out) {
+  __shared__ __attribute__((aligned(16))) float red[kThreads * kRedW];
+  __shared__ float part[kRedW][8];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int pass = 0; pass < M3S_RED_PASSES; pass++) {
+    if (pass) __syncthreads();
+    float2 *row = reinterpret_cast<float2 *>(red + (size_t)t * kRedW);
+#pragma unroll
+    for (int k = 0; k < kRedW / 2; k++)
+      row[k] = make_float2(acc[pass * kRedW + 2 * k], acc[pass * kRedW + 2 * k + 1]);
+    __syncthreads();
+    constexpr int S = (kThreads + kRedW * 7 - 1) / (kRedW * 7) * 7 > 0 ? 7 : 7;
+    constexpr int per = (kThreads + S - 1) / S;
+    if (t < kRedW * S) {
+      const int v = t / S, s = t % S;
+      const int r0 = s * per, r1 = (r0 + per < kThreads) ? r0 + per : kThreads;
+      float x = 0.0f;
+      for (int r = r0; r < r1; r++) x += red[r * kRedW + v];
+      part[v][s] = x;
+    }
+    __syncthreads();
+    if (t < kRedW) {
+      float x = 0.0f;
+#pragma unroll
+      for (int s = 0; s < S; s++) x += part[t][s];
+      out[pass * kRedW + t] = x;
+    }
+  }
+}
+
+#ifndef M3S_NT
+#define M3S_NT 1  // non-temporal loads for the once-per-iteration edge stream
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+#if M3S_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
+#ifndef M3S_LIN_MINWAVES
+#define M3S_LIN_MINWAVES 0
+#endif
+#if M3S_LIN_MINWAVES > 0
+#define M3S_LIN_BOUNDS __launch_bounds__(kThreads, M3S_LIN_MINWAVES)
+#else
+#define M3S_LIN_BOUNDS __launch_bounds__(kThreads)
+#endif
+#ifndef M3S_LDS_REDUCE
+#define M3S_LDS_REDUCE 0
+#endif
+
+// Each lane owns 4 consecutive pixels (one 16-B vector per stream); a wave
+// sweeps 256 pixels per trip, a block 1024.
 template <int MODE, bool TRACK, bool VEC>
-__global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
+__global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
   if (*A.stop) return;
   const int64_t b = blockIdx.x;
   const int64_t e_loc = b / A.chunks;
@@ -239,9 +304,9 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   }
   // edge data (idx/valid/Q) is addressed relative to the launch's edge slice
   const size_t eoff = TRACK ? 0 : (size_t)e_loc * HW;
-  const int64_t* __restrict__ idx = TRACK ? nullptr : A.idx + eoff;
-  const uint8_t* __restrict__ valid = A.valid + eoff;
-  const float* __restrict__ Qe = A.Q + eoff;
+  const int64_t *__restrict__ idx = TRACK ? nullptr : A.idx + eoff;
+  const uint8_t *__restrict__ valid = A.valid + eoff;
+  const float *__restrict__ Qe = A.Q + eoff;
 
   float acc[kNP];
 #pragma unroll
@@ -254,12 +319,12 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
     for (int64_t p0 = p_begin + kPixPerThread * threadIdx.x; p0 < p_end; p0 += kBlockPix) {
       // edge data is read once per iteration: non-temporal, so the pointmaps
       // (re-read by every edge that touches a keyframe) keep the caches
-      const uint32_t vb = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(valid + p0));
-      const f32x4 q4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(Qe + p0));
+      const uint32_t vb = ld_stream(reinterpret_cast<const uint32_t *>(valid + p0));
+      const f32x4 q4 = ld_stream(reinterpret_cast<const f32x4 *>(Qe + p0));
       int64_t ids[4] = {0, 0, 0, 0};
       if (!TRACK) {
-        const i64x2 i01 = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(idx + p0));
-        const i64x2 i23 = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(idx + p0 + 2));
+        const i64x2 i01 = ld_stream(reinterpret_cast<const i64x2 *>(idx + p0));
+        const i64x2 i23 = ld_stream(reinterpret_cast<const i64x2 *>(idx + p0 + 2));
         ids[0] = i01.x, ids[1] = i01.y, ids[2] = i23.x, ids[3] = i23.y;
       }
       const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * p0);
@@ -283,8 +348,10 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
       do_pixel<MODE, TRACK>(acc, A, Tij, Xs_i, Cs_i, p, vm, id, Qe[p], Xj, cj);
     }
   }
-
-  // block reduction: wave64 butterfly, then 4 waves through LDS
+#if M3S_LDS_REDUCE
+  block_reduce_store(acc, A.partials + (size_t)b * kNP);
+#else
+  // wave64 butterfly, then the 4 waves through LDS
   __shared__ float red[kThreads / 64][kNP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -299,6 +366,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
     for (int w = 0; w < kThreads / 64; w++) s += red[w][threadIdx.x];
     A.partials[(size_t)b * kNP + threadIdx.x] = s;
   }
+#endif
 }
 
 // fp64 sum of each edge's chunk partials (fixed order)

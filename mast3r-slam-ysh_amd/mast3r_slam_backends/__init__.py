@@ -29,7 +29,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libm3s_gn.so"
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+LIB_PATH = os.environ.get("M3S_LIB") or os.path.join(_HERE, LIB_NAME)  # override: experiments only
 
 M3S_OK, M3S_EINVAL, M3S_ELAUNCH, M3S_ETOOLARGE = 0, 1, 2, 3
 MODE_POINTS, MODE_RAYS, MODE_CALIB = 0, 1, 2

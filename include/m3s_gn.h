@@ -15,12 +15,14 @@
  *   valid_match uint8 [E, HW]     (torch.bool, [E, HW, 1] in the reference)
  *   Q          float  [E, HW]     match quality
  *   K          float  [3, 3]      calib only
- * ii/jj are remapped on device to ranks in sorted-unique(cat(ii, jj)) as the
- * reference does (gn_kernels.cu:161-170); pose rank 0 is held fixed
- * (num_fix = 1, gn_kernels.cu:1157).
+ * ii/jj are remapped to ranks in sorted-unique(cat(ii, jj)) as the reference
+ * does (gn_kernels.cu:161-170); pose rank 0 is held fixed (num_fix = 1,
+ * gn_kernels.cu:1157).
  *
- * All launches are asynchronous on `stream`; the calls never synchronise the
- * host and never allocate (the caller passes a workspace of
+ * Per solve call the host reads ii/jj once (like the reference's _unique /
+ * searchsorted) to rank them and to build the block-sparse LLT plan; every GN
+ * iteration after that is launched asynchronously on `stream` with no host
+ * synchronisation. Nothing is allocated (the caller passes a workspace of
  * m3s_gn_workspace_size() bytes, 256-byte aligned). Device-side outcomes
  * (iterations run, solve failures, invalid edge ids) land in `info`.
  */
@@ -90,7 +92,8 @@ int m3s_gauss_newton_rays(const m3s_gn_args *a, void *stream);
 int m3s_gauss_newton_calib(const m3s_gn_args *a, void *stream);
 
 /* ---- stepwise API (edge-sharded multi-GPU path; same math as above) ----
- * m3s_gn_prepare:   remap ii/jj -> ranks, zero info/flags.
+ * m3s_gn_prepare:   rank ii/jj, build + upload the sparse plan, zero info/flags
+ *                   (synchronises the stream once).
  * m3s_gn_linearize: per-edge local normal equations for edges
  *                   [edge_begin, edge_end) into edge_sums (double[E_loc][36]:
  *                   28 upper-triangular J^T W J, 7 J^T W r, 1 cost, in the
@@ -144,6 +147,13 @@ int m3s_track_calib_sim3(const m3s_track_args *a, void *stream);
 
 /* build identification (for the loaded-library check) */
 const char *m3s_version(void);
+
+/* Diagnostic: the host symbolic plan of the block-sparse LLT for N poses and
+ * edge ranks (ri, rj) (pose rank 0 fixed). Writes the flattened int32 plan to
+ * out (if cap suffices) and meta[0..21] = {m, S, levels, 19 section offsets in
+ * the order of m3s_symbolic.h}. Returns the plan length in int32 words. */
+int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj,
+                              int32_t *out, int64_t cap, int32_t *meta);
 
 #ifdef __cplusplus
 }

@@ -32,8 +32,15 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
 #include "m3s_device.h"
 #include "m3s_gn.h"
+#include "m3s_symbolic.h"
 
 using namespace m3s;
 
@@ -72,8 +79,9 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 }
 
 struct Layout {
-  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, total;
-  int64_t n, ld;  // system size 7(N-1); leading dim of the RHS-augmented matrix
+  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, total;
+  int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
+  int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
 
 constexpr int kTile = 64;  // tiled Cholesky tile (large systems)
@@ -100,6 +108,17 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   L.ld = aug_ld(n);
   L.A = off;
   off = align_up(off + sizeof(double) * (size_t)(L.ld * L.ld), 256);
+  const int64_t m = N > 1 ? N - 1 : 0;
+  L.fin = off;
+  off = align_up(off + sizeof(double) * 56 * (size_t)(E + 1), 256);
+  L.slot_cap = std::min<int64_t>(m * (m + 1) / 2, 64 * m + 4096) + 1;
+  L.plan_cap = (int64_t(1) << 22) + 16 * E + 64 * m;
+  L.plan = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)L.plan_cap, 256);
+  L.Lblk = off;
+  off = align_up(off + sizeof(double) * 49 * (size_t)L.slot_cap, 256);
+  L.Dinv = off;
+  off = align_up(off + sizeof(double) * 49 * (size_t)(m + 1), 256);
   L.total = off;
   (void)HW;
   return L;
@@ -108,64 +127,6 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
 template <typename T>
 inline T *at(void *base, size_t off) {
   return reinterpret_cast<T *>(static_cast<char *>(base) + off);
-}
-
-// ------------------------------------------------------------- remapping --
-// rank of every ii/jj entry in sorted-unique(cat(ii, jj))  (gn_kernels.cu:161-170)
-__global__ void remap_first_kernel(const int64_t *__restrict__ ii, const int64_t *__restrict__ jj,
-                                   int64_t E, int32_t *__restrict__ first) {
-  __shared__ int64_t tile[1024];
-  const int64_t n = 2 * E;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t v = t < n ? (t < E ? ii[t] : jj[t - E]) : 0;
-  bool dup = false;
-  for (int64_t base = 0; base < n; base += 1024) {
-    __syncthreads();
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
-      const int64_t s = base + k;
-      tile[k] = s < n ? (s < E ? ii[s] : jj[s - E]) : 0;
-    }
-    __syncthreads();
-    if (t < n) {
-      const int64_t lim = (t - base) < 1024 ? (t - base) : 1024;
-      for (int64_t k = 0; k < lim; k++) dup |= (tile[k] == v);
-    }
-  }
-  if (t < n) first[t] = dup ? 0 : 1;
-}
-
-__global__ void remap_rank_kernel(const int64_t *__restrict__ ii, const int64_t *__restrict__ jj,
-                                  int64_t E, int64_t N, const int32_t *__restrict__ first,
-                                  int32_t *__restrict__ rank_i, int32_t *__restrict__ rank_j,
-                                  int32_t *__restrict__ info, int32_t *__restrict__ flags) {
-  __shared__ int64_t tile[1024];
-  __shared__ int32_t tfirst[1024];
-  const int64_t n = 2 * E;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t v = t < n ? (t < E ? ii[t] : jj[t - E]) : 0;
-  int32_t r = 0;
-  for (int64_t base = 0; base < n; base += 1024) {
-    __syncthreads();
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
-      const int64_t s = base + k;
-      tile[k] = s < n ? (s < E ? ii[s] : jj[s - E]) : 0;
-      tfirst[k] = s < n ? first[s] : 0;
-    }
-    __syncthreads();
-    if (t < n)
-      for (int k = 0; k < 1024; k++) r += (tfirst[k] && tile[k] < v) ? 1 : 0;
-  }
-  if (t < n) {
-    if (t < E)
-      rank_i[t] = r;
-    else
-      rank_j[t - E] = r;
-    atomicMax(&info[M3S_INFO_N_UNIQUE], r + 1);
-    if (r >= N) {
-      atomicExch(&info[M3S_INFO_BAD_EDGE], 1);
-      atomicExch(&flags[kFlagStop], 1);
-    }
-  }
 }
 
 // ------------------------------------------------------------- linearize --
@@ -698,6 +659,315 @@ __global__ void __launch_bounds__(1024) backsolve_kernel(const double *__restric
   finish_step(rhs, dxs, nrm, n, Twc, N, dx_out, info, flags + kFlagStop, delta_thresh);
 }
 
+// ------------------------------------------------- block-sparse LLT ----
+// Per edge: H_jj = M L M^T and g_j = M l in fp64 (M = Adj(T_i)^-T), written
+// as fin[e][0:49] (row-major) and fin[e][49:56]. One 64-thread block per edge.
+constexpr int kFin = 56;
+__global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__restrict__ edge_sums,
+                                                            const int32_t *__restrict__ rank_i,
+                                                            const float *__restrict__ Twc,
+                                                            double *__restrict__ fin,
+                                                            const int32_t *__restrict__ stop) {
+  if (*stop) return;
+  const int64_t e = blockIdx.x;
+  const int t = threadIdx.x;
+  __shared__ double M[7][7], Lm[7][7], T1[7][7], l[7];
+  const double *es = edge_sums + (size_t)e * kNP;
+  if (t == 0) adjT_inv_matrix(Twc + 8 * (size_t)rank_i[e], M);
+  if (t < 49) {
+    const int a = t / 7, c = t % 7;
+    Lm[a][c] = es[kL + tri(a < c ? a : c, a < c ? c : a)];
+  }
+  if (t < 7) l[t] = es[kG + t];
+  __syncthreads();
+  if (t < 49) {
+    const int a = t / 7, c = t % 7;
+    double s = 0.0;
+    for (int k = 0; k < 7; k++) s += M[a][k] * Lm[k][c];
+    T1[a][c] = s;
+  } else if (t < 56) {
+    const int a = t - 49;
+    double s = 0.0;
+    for (int k = 0; k < 7; k++) s += M[a][k] * l[k];
+    fin[(size_t)e * kFin + 49 + a] = s;
+  }
+  __syncthreads();
+  if (t < 49) {
+    const int a = t / 7, c = t % 7;
+    double s = 0.0;
+    for (int k = 0; k < 7; k++) s += T1[a][k] * M[c][k];
+    fin[(size_t)e * kFin + t] = s;
+  }
+}
+
+struct SparseDev {
+  const int32_t *plan;  // flattened plan (global); copied to LDS by the IN_LDS variant
+  int plan_len;
+  int off[19];          // section offsets, order of m3s_symbolic.h
+  int m, S, levels;
+  double *L;     // [S][49] (global variant)
+  double *Dinv;  // [m][49] (global variant)
+  const double *fin;
+  float *Twc;
+  int64_t N;
+  float *dx_out;
+  int32_t *info;
+  int32_t *flags;
+  float delta_thresh;
+};
+
+// Broadcast lane `l` (a compile-time / wave-uniform index) of a double:
+// two v_readlane_b32, no LDS round trip.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// 1/sqrt(d) for d > 0: hardware estimate + two Newton steps (~full fp64
+// precision, no IEEE division/sqrt sequences on the pivot chain)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double x = __builtin_amdgcn_rsq(d);
+  const double hd = 0.5 * d;
+  x = x * (1.5 - hd * x * x);
+  x = x * (1.5 - hd * x * x);
+  return x;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One 1024-thread workgroup: assemble -> left-looking block LLT by elimination-
+// tree level (phase A: diagonal blocks + RHS; phase B: off-diagonal blocks) ->
+// L^T x = y by levels in reverse -> dx, retraction, ||dx|| test.
+// Layouts inside a wave: "entry" lanes 0..48 hold (r, c) = (lane / 7, lane % 7)
+// of a 7x7 block (block GEMMs), "row" lanes 0..6 hold a whole row / column in
+// registers (7x7 Cholesky, inverse, substitution) with v_readlane broadcasts.
+template <bool IN_LDS>
+__global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
+  if (D.flags[kFlagStop]) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int fail_s;
+  __shared__ float nrm[16];
+  __shared__ double scratch[16][64];
+  const int m = D.m, S = D.S;
+  double *Lb = IN_LDS ? smem : D.L;
+  double *Di = IN_LDS ? smem + (size_t)S * 49 : D.Dinv;
+  double *y = IN_LDS ? smem + (size_t)(S + m) * 49 : smem;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // index arrays: LDS copy (IN_LDS) or global
+  const int32_t *pl = D.plan;
+  if (IN_LDS) {
+    int32_t *lp = reinterpret_cast<int32_t *>(y + (size_t)m * 7);
+    for (int q = tid; q < D.plan_len; q += 1024) lp[q] = D.plan[q];
+    pl = lp;
+  }
+  const int32_t *perm = pl + D.off[0], *col_ptr = pl + D.off[1], *col_row = pl + D.off[2],
+                *col_slot = pl + D.off[3], *lev_ptr = pl + D.off[4], *lev_col = pl + D.off[5],
+                *dtr_ptr = pl + D.off[6], *dtr_slot = pl + D.off[7], *dtr_p = pl + D.off[8],
+                *task_lev_ptr = pl + D.off[9], *task_dst = pl + D.off[10], *task_col = pl + D.off[11],
+                *task_tr_ptr = pl + D.off[12], *tr_a = pl + D.off[13], *tr_b = pl + D.off[14],
+                *asm_ptr = pl + D.off[15], *asm_edge = pl + D.off[16], *g_ptr = pl + D.off[17],
+                *g_edge = pl + D.off[18];
+  if (IN_LDS) __syncthreads();
+  const int r = lane / 7, c = lane % 7;
+  const bool act49 = lane < 49;
+  double *scr = scratch[wave];
+  constexpr int NW = 16;
+
+  // 0. assembly (edge order within each slot: deterministic)
+  for (int idx = tid; idx < S * 49; idx += 1024) {
+    const int s = idx / 49, q = idx - s * 49;
+    double v = 0.0;
+    for (int t = asm_ptr[s]; t < asm_ptr[s + 1]; t++) v += D.fin[(size_t)asm_edge[t] * kFin + q];
+    Lb[idx] = (s < m) ? v : -v;
+  }
+  for (int idx = tid; idx < m * 7; idx += 1024) {
+    const int vv = idx / 7, q = idx - vv * 7;
+    double v = 0.0;
+    for (int t = g_ptr[vv]; t < g_ptr[vv + 1]; t++) {
+      const int ent = g_edge[t];
+      const double gj = D.fin[(size_t)(ent >> 1) * kFin + 49 + q];
+      v += (ent & 1) ? gj : -gj;
+    }
+    y[idx] = v;
+  }
+  if (tid == 0) fail_s = 0;
+  __syncthreads();
+
+  // 1. factorisation + forward substitution
+  for (int l = 0; l < D.levels; l++) {
+    for (int t = lev_ptr[l] + wave; t < lev_ptr[l + 1]; t += NW) {  // phase A
+      const int k = lev_col[t];
+      double v = act49 ? Lb[(size_t)k * 49 + lane] : 0.0;
+      for (int q = dtr_ptr[k]; q < dtr_ptr[k + 1]; q++) {
+        const double *A = Lb + (size_t)dtr_slot[q] * 49;
+        if (act49) {
+          double s = 0.0;
+#pragma unroll
+          for (int mm = 0; mm < 7; mm++) s += A[r * 7 + mm] * A[c * 7 + mm];
+          v -= s;
+        }
+      }
+      // b_k - sum_p L_kp y_p on lanes 0..6
+      double bb = (lane < 7) ? y[k * 7 + lane] : 0.0;
+      for (int q = dtr_ptr[k]; q < dtr_ptr[k + 1]; q++) {
+        const double *A = Lb + (size_t)dtr_slot[q] * 49;
+        const int p = dtr_p[q];
+        if (lane < 7) {
+          double s = 0.0;
+#pragma unroll
+          for (int mm = 0; mm < 7; mm++) s += A[lane * 7 + mm] * y[p * 7 + mm];
+          bb -= s;
+        }
+      }
+      // entry layout -> row layout through the wave's scratch
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      double a[7];
+#pragma unroll
+      for (int q = 0; q < 7; q++) a[q] = (lane < 7) ? scr[lane * 7 + q] : 0.0;
+      wave_lds_fence();
+      // Cholesky: lane r holds row r; column j of L broadcast by readlane
+      bool bad = false;
+      double dinv[7];  // 1 / L_jj
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+        const double d = readlane_d(a[j], j);
+        bad |= !(d > 0.0);
+        const double inv = rsqrt_nr(d);
+        dinv[j] = inv;
+        a[j] = (lane > j) ? a[j] * inv : ((lane == j) ? d * inv : 0.0);
+#pragma unroll
+        for (int cc = j + 1; cc < 7; cc++) {
+          const double lcj = readlane_d(a[j], cc);
+          if (lane >= cc) a[cc] -= a[j] * lcj;
+        }
+      }
+      // forward substitution L y_k = bb (uniform values)
+      double yk[7];
+#pragma unroll
+      for (int rr = 0; rr < 7; rr++) {
+        double acc = readlane_d(bb, rr);
+#pragma unroll
+        for (int mm = 0; mm < rr; mm++) acc -= readlane_d(a[mm], rr) * yk[mm];
+        yk[rr] = acc * dinv[rr];
+      }
+      // W = L^-1: lane c computes column c
+      double w[7];
+#pragma unroll
+      for (int rr = 0; rr < 7; rr++) {
+        double acc = (rr == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int mm = 0; mm < rr; mm++) acc -= readlane_d(a[mm], rr) * w[mm];
+        w[rr] = (rr >= lane) ? acc * dinv[rr] : 0.0;
+      }
+      if (lane < 7) {
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+          Lb[(size_t)k * 49 + lane * 7 + q] = (q <= lane) ? a[q] : 0.0;  // row `lane` of L_kk
+          Di[(size_t)k * 49 + q * 7 + lane] = w[q];                      // column `lane` of W
+        }
+        double yo = 0.0;
+#pragma unroll
+        for (int q = 0; q < 7; q++) yo = (q == lane) ? yk[q] : yo;
+        y[k * 7 + lane] = yo;
+      }
+      if (bad && lane == 0) fail_s = 1;
+    }
+    __syncthreads();
+    if (fail_s) break;  // uniform
+    for (int t = task_lev_ptr[l] + wave; t < task_lev_ptr[l + 1]; t += NW) {  // phase B
+      const int dst = task_dst[t], k = task_col[t];
+      double v = act49 ? Lb[(size_t)dst * 49 + lane] : 0.0;
+      for (int q = task_tr_ptr[t]; q < task_tr_ptr[t + 1]; q++) {
+        const double *A = Lb + (size_t)tr_a[q] * 49;
+        const double *B = Lb + (size_t)tr_b[q] * 49;
+        if (act49) {
+          double s = 0.0;
+#pragma unroll
+          for (int mm = 0; mm < 7; mm++) s += A[r * 7 + mm] * B[c * 7 + mm];
+          v -= s;
+        }
+      }
+      // L_ik = A_ik W^T : x(r,c) = sum_m A(r,m) W(c,m)
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      if (act49) {
+        double x = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) x += scr[r * 7 + mm] * Di[(size_t)k * 49 + c * 7 + mm];
+        Lb[(size_t)dst * 49 + lane] = x;
+      }
+      wave_lds_fence();
+    }
+    __syncthreads();
+  }
+
+  if (fail_s) {
+    fail_step(7 * m, D.dx_out, D.info, D.flags + kFlagStop, D.delta_thresh);
+    return;
+  }
+
+  // 2. back-substitution L^T x = y, levels in reverse (x overwrites y)
+  for (int l = D.levels - 1; l >= 0; l--) {
+    for (int t = lev_ptr[l] + wave; t < lev_ptr[l + 1]; t += NW) {
+      const int k = lev_col[t];
+      double rr = (lane < 7) ? y[k * 7 + lane] : 0.0;
+      for (int q = col_ptr[k]; q < col_ptr[k + 1]; q++) {
+        const double *A = Lb + (size_t)col_slot[q] * 49;
+        const int i = col_row[q];
+        if (lane < 7) {
+          double s = 0.0;
+#pragma unroll
+          for (int mm = 0; mm < 7; mm++) s += A[mm * 7 + lane] * y[i * 7 + mm];
+          rr -= s;
+        }
+      }
+      double xk = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) {
+        const double rm = readlane_d(rr, mm);
+        if (lane < 7) xk += Di[(size_t)k * 49 + mm * 7 + lane] * rm;
+      }
+      if (lane < 7) y[k * 7 + lane] = xk;
+    }
+    __syncthreads();
+  }
+
+  // 3. dx = -x in the original variable order, retraction, ||dx||
+  float part = 0.0f;
+  for (int idx = tid; idx < m * 7; idx += 1024) {
+    const int vn = idx / 7, q = idx - vn * 7;
+    const int vo = perm[vn];
+    const float v = -(float)y[idx];
+    D.dx_out[vo * 7 + q] = v;
+    part += v * v;
+  }
+  part = wave_sum(part);
+  if (lane == 0) nrm[wave] = part;
+  __syncthreads();  // dx_out (global) written by this block is visible to it now
+  for (int p = tid; p < m; p += 1024) {
+    const Sim3f T = load_sim3(D.Twc + 8 * (size_t)(p + 1));
+    float xi[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) xi[q] = D.dx_out[p * 7 + q];
+    store_sim3(D.Twc + 8 * (size_t)(p + 1), retract(xi, T));
+  }
+  if (tid == 0) {
+    float s2 = 0.0f;
+    for (int w2 = 0; w2 < NW; w2++) s2 += nrm[w2];
+    D.info[M3S_INFO_ITERS] += 1;
+    if (sqrtf(s2) < D.delta_thresh) {
+      D.info[M3S_INFO_CONVERGED] = 1;
+      D.flags[kFlagStop] = 1;
+    }
+  }
+}
+
 // ------------------------------------------------- small dense Cholesky --
 // Thread (tr, tc) of a 16 x 32 grid owns A[lr*16 + tr][lc*32 + tc]. The RHS g
 // is appended as row n, so the factor's row n is y = L^-1 g. After the loop
@@ -916,6 +1186,20 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   return launch_ok();
 }
 
+// Host registry of the per-call plan (keyed by workspace): the stepwise API
+// calls prepare and solve separately.
+struct PlanMeta {
+  bool sparse = false;
+  bool lds = false;
+  size_t lds_bytes = 0;
+  int m = 0, S = 0, levels = 0, plan_len = 0;
+  PlanImage img;  // offsets (data vector cleared after upload)
+};
+std::mutex g_reg_mu;
+std::unordered_map<const void *, PlanMeta> g_reg;
+
+constexpr size_t kMaxLdsBytes = 150 * 1024;
+
 int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
@@ -923,12 +1207,54 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st)
   int32_t *stop = flags + kFlagStop;
   const int64_t n = Ly.n, ld = Ly.ld;
   if (a->N <= 1) return M3S_OK;
+  PlanMeta meta;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(ws);
+    if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
+    meta = it->second;
+  }
+  int rc;
+  float *dx = a->dx_out;
+  if (meta.sparse) {
+    double *fin = at<double>(ws, Ly.fin);
+    if (a->E > 0) {
+      finalize_edges_kernel<<<dim3((unsigned)a->E), dim3(64), 0, st>>>(edge_sums, at<int32_t>(ws, Ly.rank_i),
+                                                                      a->Twc, fin, stop);
+      if ((rc = launch_ok())) return rc;
+    }
+    const PlanImage &I = meta.img;
+    SparseDev D;
+    D.plan = at<int32_t>(ws, Ly.plan);
+    D.plan_len = meta.plan_len;
+    const int64_t offs[19] = {I.off_perm, I.off_col_ptr, I.off_col_row, I.off_col_slot, I.off_lev_ptr,
+                              I.off_lev_col, I.off_dtr_ptr, I.off_dtr_slot, I.off_dtr_p, I.off_task_lev_ptr,
+                              I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a, I.off_tr_b,
+                              I.off_asm_ptr, I.off_asm_edge, I.off_g_ptr, I.off_g_edge};
+    for (int q = 0; q < 19; q++) D.off[q] = (int)offs[q];
+    D.m = meta.m;
+    D.S = meta.S;
+    D.levels = meta.levels;
+    D.L = at<double>(ws, Ly.Lblk);
+    D.Dinv = at<double>(ws, Ly.Dinv);
+    D.fin = fin;
+    D.Twc = a->Twc;
+    D.N = a->N;
+    D.dx_out = dx;
+    D.info = a->info;
+    D.flags = flags;
+    D.delta_thresh = a->delta_thresh;
+    if (meta.lds)
+      sparse_llt_kernel<true><<<1, 1024, meta.lds_bytes, st>>>(D);
+    else
+      sparse_llt_kernel<false><<<1, 1024, meta.lds_bytes, st>>>(D);
+    return launch_ok();
+  }
+  // dense fallback: RHS-augmented system, register or tiled LLT
   double *A = at<double>(ws, Ly.A);
   assemble_kernel<<<dim3((unsigned)a->N), dim3(256), 0, st>>>(
       edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, ld, A, stop);
-  int rc = launch_ok();
-  if (rc) return rc;
-  float *dx = a->dx_out;
+  if ((rc = launch_ok())) return rc;
   const int np = (int)n + 1;
   if (np <= kMaxSmallNp) {
     const int nbc = (np + 31) / 32;
@@ -951,15 +1277,14 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st)
 #undef M3S_CHOL
     return launch_ok();
   }
-  // tiled path
   const int nt = (int)(ld / kTile);
   for (int kb = 0; kb < nt; kb++) {
     if ((int64_t)kb * kTile >= n) break;
     potrf_tile_kernel<<<1, 256, 0, st>>>(A, ld, n, kb, flags);
-    const int m = nt - kb - 1;
-    if (m > 0) {
-      trsm_tile_kernel<<<m, 256, 0, st>>>(A, ld, n, kb, flags);
-      update_tiles_kernel<<<m * (m + 1) / 2, 256, 0, st>>>(A, ld, kb, flags);
+    const int mt = nt - kb - 1;
+    if (mt > 0) {
+      trsm_tile_kernel<<<mt, 256, 0, st>>>(A, ld, n, kb, flags);
+      update_tiles_kernel<<<mt * (mt + 1) / 2, 256, 0, st>>>(A, ld, kb, flags);
     }
     if ((rc = launch_ok())) return rc;
   }
@@ -968,6 +1293,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st)
   return launch_ok();
 }
 
+// Per call: zero state, bring ii/jj to the host (the reference's _unique /
+// searchsorted also synchronise), rank them, build and upload the sparse plan.
 int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
@@ -975,18 +1302,67 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   if (hipMemsetAsync(a->info, 0, 8 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
   if (a->N > 1 && a->dx_out && hipMemsetAsync(a->dx_out, 0, sizeof(float) * 7 * (a->N - 1), st) != hipSuccess)
     return M3S_ELAUNCH;
-  if (a->E <= 0) return M3S_OK;
-  const int64_t n = 2 * a->E;
-  const unsigned blocks = (unsigned)((n + 255) / 256);
-  int32_t *first = at<int32_t>(ws, Ly.first);
-  remap_first_kernel<<<dim3(blocks), dim3(256), 0, st>>>(a->ii, a->jj, a->E, first);
-  int rc = launch_ok();
-  if (rc) return rc;
-  remap_rank_kernel<<<dim3(blocks), dim3(256), 0, st>>>(a->ii, a->jj, a->E, a->N, first,
-                                                         at<int32_t>(ws, Ly.rank_i),
-                                                         at<int32_t>(ws, Ly.rank_j), a->info,
-                                                         at<int32_t>(ws, Ly.flags));
-  return launch_ok();
+  const int64_t E = a->E;
+  std::vector<int64_t> hii(E), hjj(E);
+  if (E > 0) {
+    if (hipMemcpyAsync(hii.data(), a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(hjj.data(), a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return M3S_ELAUNCH;
+  }
+  std::vector<int32_t> ri, rj;
+  const int nu = host_remap(hii.data(), hjj.data(), E, ri, rj);
+  int32_t hinfo[8] = {0, 0, 0, 0, nu, 0, 0, 0};
+  int32_t hflags[2] = {0, 0};
+  const bool bad = nu > a->N;
+  if (bad) hinfo[M3S_INFO_BAD_EDGE] = 1, hflags[kFlagStop] = 1;
+  PlanMeta meta;
+  PlanImage img;
+  if (!bad && a->N > 1) {
+    const char *force_dense = std::getenv("M3S_DENSE");
+    SparsePlan P;
+    build_sparse_plan((int)a->N, ri, rj, P);
+    flatten_plan(P, img);
+    const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
+    if (fits && !(force_dense && force_dense[0] == '1')) {
+      meta.sparse = true;
+      meta.m = P.m;
+      meta.S = P.S;
+      meta.levels = P.levels;
+      meta.plan_len = (int)img.data.size();
+      const size_t lds_all = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) +
+                             sizeof(int32_t) * img.data.size();
+      meta.lds = lds_all <= kMaxLdsBytes;
+      meta.lds_bytes = meta.lds ? lds_all : sizeof(double) * (size_t)P.m * 7;
+    }
+  }
+  if (E > 0) {
+    if (hipMemcpyAsync(at<int32_t>(ws, Ly.rank_i), ri.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(at<int32_t>(ws, Ly.rank_j), rj.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice, st) != hipSuccess)
+      return M3S_ELAUNCH;
+  }
+  if (meta.sparse && !img.data.empty() &&
+      hipMemcpyAsync(at<int32_t>(ws, Ly.plan), img.data.data(), sizeof(int32_t) * img.data.size(),
+                     hipMemcpyHostToDevice, st) != hipSuccess)
+    return M3S_ELAUNCH;
+  if (hipMemcpyAsync(a->info, hinfo, sizeof hinfo, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(at<int32_t>(ws, Ly.flags), hflags, sizeof hflags, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)  // host buffers are released below
+    return M3S_ELAUNCH;
+  img.data.clear();
+  meta.img = img;
+  if (meta.sparse && meta.lds_bytes > 64 * 1024) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    });
+  }
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  g_reg[ws] = meta;
+  return M3S_OK;
 }
 
 int gn_full(const m3s_gn_args *a, int mode, void *stream) {
@@ -1202,6 +1578,26 @@ size_t m3s_track_workspace_size(int64_t HW) {
 int m3s_track_rays_sim3(const m3s_track_args *a, void *stream) { return track_impl(a, M3S_MODE_RAYS, stream); }
 int m3s_track_calib_sim3(const m3s_track_args *a, void *stream) { return track_impl(a, M3S_MODE_CALIB, stream); }
 
-const char *m3s_version(void) { return "m3s-gn 0.1 gfx950"; }
+const char *m3s_version(void) { return "m3s-gn 0.2 gfx950"; }
+
+int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj,
+                              int32_t *out, int64_t cap, int32_t *meta) {
+  std::vector<int32_t> a(ri, ri + E), b(rj, rj + E);
+  SparsePlan P;
+  build_sparse_plan(N, a, b, P);
+  PlanImage I;
+  flatten_plan(P, I);
+  const int64_t offs[19] = {I.off_perm, I.off_col_ptr, I.off_col_row, I.off_col_slot, I.off_lev_ptr,
+                            I.off_lev_col, I.off_dtr_ptr, I.off_dtr_slot, I.off_dtr_p, I.off_task_lev_ptr,
+                            I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a, I.off_tr_b,
+                            I.off_asm_ptr, I.off_asm_edge, I.off_g_ptr, I.off_g_edge};
+  if (meta) {
+    meta[0] = P.m, meta[1] = P.S, meta[2] = P.levels;
+    for (int k = 0; k < 19; k++) meta[3 + k] = (int32_t)offs[k];
+  }
+  const int64_t n = (int64_t)I.data.size();
+  if (out && cap >= n) std::copy(I.data.begin(), I.data.end(), out);
+  return n;
+}
 
 }  // extern "C"

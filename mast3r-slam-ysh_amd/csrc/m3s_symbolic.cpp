@@ -1,0 +1,197 @@
+// m3s_symbolic.cpp — host symbolic analysis for the block-sparse LLT
+// (see m3s_symbolic.h). Deterministic: every tie is broken by index.
+#include "m3s_symbolic.h"
+
+#include <algorithm>
+#include <set>
+#include <unordered_map>
+
+namespace m3s {
+
+int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int32_t> &ri,
+               std::vector<int32_t> &rj) {
+  std::vector<int64_t> u(ii, ii + E);
+  u.insert(u.end(), jj, jj + E);
+  std::sort(u.begin(), u.end());
+  u.erase(std::unique(u.begin(), u.end()), u.end());
+  ri.resize(E);
+  rj.resize(E);
+  for (int64_t e = 0; e < E; e++) {
+    ri[e] = (int32_t)(std::lower_bound(u.begin(), u.end(), ii[e]) - u.begin());
+    rj[e] = (int32_t)(std::lower_bound(u.begin(), u.end(), jj[e]) - u.begin());
+  }
+  return (int)u.size();
+}
+
+namespace {
+
+// minimum-degree elimination order on the variable graph (ties: lowest index)
+std::vector<int32_t> min_degree_order(int m, const std::vector<std::set<int>> &adj0) {
+  std::vector<std::set<int>> adj = adj0;
+  std::vector<char> alive(m, 1);
+  std::vector<int32_t> order;
+  order.reserve(m);
+  for (int step = 0; step < m; step++) {
+    int best = -1;
+    size_t bd = 0;
+    for (int v = 0; v < m; v++)
+      if (alive[v] && (best < 0 || adj[v].size() < bd)) best = v, bd = adj[v].size();
+    order.push_back(best);
+    alive[best] = 0;
+    const std::set<int> nb = adj[best];
+    for (int a : nb) {
+      adj[a].erase(best);
+      for (int b : nb)
+        if (b != a) adj[a].insert(b);
+    }
+    adj[best].clear();
+  }
+  return order;
+}
+
+}  // namespace
+
+void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
+                       SparsePlan &P) {
+  const int m = N > 1 ? N - 1 : 0;
+  const int64_t E = (int64_t)ri.size();
+  P = SparsePlan();
+  P.m = m;
+  std::vector<std::set<int>> adj(m);
+  for (int64_t e = 0; e < E; e++) {
+    const int a = ri[e] - 1, b = rj[e] - 1;
+    if (a >= 0 && b >= 0 && a != b) adj[a].insert(b), adj[b].insert(a);
+  }
+  P.perm = min_degree_order(m, adj);
+  P.iperm.assign(m, 0);
+  for (int k = 0; k < m; k++) P.iperm[P.perm[k]] = k;
+
+  // symbolic factorisation in the new order
+  std::vector<std::set<int>> S(m);
+  for (int v = 0; v < m; v++)
+    for (int u : adj[v]) {
+      const int i = P.iperm[v], j = P.iperm[u];
+      if (i > j) S[j].insert(i);
+    }
+  std::vector<std::vector<int>> st(m);
+  std::vector<int> parent(m, -1);
+  for (int k = 0; k < m; k++) {
+    st[k].assign(S[k].begin(), S[k].end());
+    if (!st[k].empty()) {
+      parent[k] = st[k][0];
+      for (size_t q = 1; q < st[k].size(); q++) S[parent[k]].insert(st[k][q]);
+    }
+  }
+  // slots: diagonals 0..m-1, then off-diagonals column by column
+  std::unordered_map<int64_t, int> slot;
+  int next = m;
+  P.col_ptr.assign(1, 0);
+  for (int k = 0; k < m; k++) {
+    for (int i : st[k]) {
+      P.col_row.push_back(i);
+      P.col_slot.push_back(next);
+      slot[(int64_t)i * m + k] = next++;
+    }
+    P.col_ptr.push_back((int32_t)P.col_row.size());
+  }
+  P.S = next;
+  auto sl = [&](int i, int k) { return slot.at((int64_t)i * m + k); };
+
+  // elimination-tree levels (children before parents)
+  std::vector<int> lev(m, 0);
+  for (int k = 0; k < m; k++)
+    if (parent[k] >= 0) lev[parent[k]] = std::max(lev[parent[k]], lev[k] + 1);
+  P.levels = m ? *std::max_element(lev.begin(), lev.end()) + 1 : 0;
+  P.lev_ptr.assign(P.levels + 1, 0);
+  for (int k = 0; k < m; k++) P.lev_ptr[lev[k] + 1]++;
+  for (int l = 0; l < P.levels; l++) P.lev_ptr[l + 1] += P.lev_ptr[l];
+  P.lev_col.assign(m, 0);
+  {
+    std::vector<int> fill(P.lev_ptr.begin(), P.lev_ptr.end() - 1);
+    for (int k = 0; k < m; k++) P.lev_col[fill[lev[k]]++] = k;
+  }
+  // row structure: rowst[k] = {p < k : k in struct(p)} (ascending)
+  std::vector<std::vector<int>> rowst(m);
+  for (int p = 0; p < m; p++)
+    for (int i : st[p]) rowst[i].push_back(p);
+  // left-looking updates
+  P.dtr_ptr.assign(1, 0);
+  for (int k = 0; k < m; k++) {
+    for (int p : rowst[k]) {
+      P.dtr_slot.push_back(sl(k, p));
+      P.dtr_p.push_back(p);
+    }
+    P.dtr_ptr.push_back((int32_t)P.dtr_slot.size());
+  }
+  P.task_lev_ptr.assign(1, 0);
+  P.task_tr_ptr.assign(1, 0);
+  for (int l = 0; l < P.levels; l++) {
+    for (int t = P.lev_ptr[l]; t < P.lev_ptr[l + 1]; t++) {
+      const int k = P.lev_col[t];
+      for (int i : st[k]) {
+        P.task_dst.push_back(sl(i, k));
+        P.task_col.push_back(k);
+        for (int p : rowst[k]) {
+          // i in struct(p)?  (struct lists are sorted)
+          if (std::binary_search(st[p].begin(), st[p].end(), i)) {
+            P.tr_a.push_back(sl(i, p));
+            P.tr_b.push_back(sl(k, p));
+          }
+        }
+        P.task_tr_ptr.push_back((int32_t)P.tr_a.size());
+      }
+    }
+    P.task_lev_ptr.push_back((int32_t)P.task_dst.size());
+  }
+  // assembly lists (edge order => deterministic sums)
+  std::vector<std::vector<int32_t>> asl(P.S), gl(m);
+  for (int64_t e = 0; e < E; e++) {
+    const int a = ri[e] - 1, b = rj[e] - 1;
+    if (a == b) continue;  // Hs[0]+Hs[1]+Hs[2]+Hs[3] = 0 on the same pose
+    const int pa = a >= 0 ? P.iperm[a] : -1, pb = b >= 0 ? P.iperm[b] : -1;
+    if (pa >= 0) asl[pa].push_back((int32_t)e), gl[pa].push_back((int32_t)(e << 1));
+    if (pb >= 0) asl[pb].push_back((int32_t)e), gl[pb].push_back((int32_t)(e << 1 | 1));
+    if (pa >= 0 && pb >= 0) asl[sl(std::max(pa, pb), std::min(pa, pb))].push_back((int32_t)e);
+  }
+  P.asm_ptr.assign(1, 0);
+  for (int s = 0; s < P.S; s++) {
+    P.asm_edge.insert(P.asm_edge.end(), asl[s].begin(), asl[s].end());
+    P.asm_ptr.push_back((int32_t)P.asm_edge.size());
+  }
+  P.g_ptr.assign(1, 0);
+  for (int v = 0; v < m; v++) {
+    P.g_edge.insert(P.g_edge.end(), gl[v].begin(), gl[v].end());
+    P.g_ptr.push_back((int32_t)P.g_edge.size());
+  }
+}
+
+void flatten_plan(const SparsePlan &P, PlanImage &img) {
+  img.data.clear();
+  auto put = [&](const std::vector<int32_t> &v) {
+    const int64_t off = (int64_t)img.data.size();
+    img.data.insert(img.data.end(), v.begin(), v.end());
+    while (img.data.size() % 4) img.data.push_back(0);  // 16-B aligned sections
+    return off;
+  };
+  img.off_perm = put(P.perm);
+  img.off_col_ptr = put(P.col_ptr);
+  img.off_col_row = put(P.col_row);
+  img.off_col_slot = put(P.col_slot);
+  img.off_lev_ptr = put(P.lev_ptr);
+  img.off_lev_col = put(P.lev_col);
+  img.off_dtr_ptr = put(P.dtr_ptr);
+  img.off_dtr_slot = put(P.dtr_slot);
+  img.off_dtr_p = put(P.dtr_p);
+  img.off_task_lev_ptr = put(P.task_lev_ptr);
+  img.off_task_dst = put(P.task_dst);
+  img.off_task_col = put(P.task_col);
+  img.off_task_tr_ptr = put(P.task_tr_ptr);
+  img.off_tr_a = put(P.tr_a);
+  img.off_tr_b = put(P.tr_b);
+  img.off_asm_ptr = put(P.asm_ptr);
+  img.off_asm_edge = put(P.asm_edge);
+  img.off_g_ptr = put(P.g_ptr);
+  img.off_g_edge = put(P.g_edge);
+}
+
+}  // namespace m3s

@@ -1,0 +1,54 @@
+// m3s_symbolic.h — host-side symbolic analysis for the block-sparse LLT.
+//
+// The reference solves the (N-1)*7 pose system with Eigen's SimplicialLLT
+// (gn_kernels.cu:132-153), i.e. a sparse Cholesky behind a fill-reducing
+// ordering. This is the same idea with 7x7 blocks: one variable per free pose,
+// a minimum-degree ordering, the block fill pattern, and a level schedule of
+// the elimination tree so the numeric phase (m3s_gn.hip, sparse_llt_kernel)
+// can factor independent columns concurrently. Computed once per solve call
+// (the edge structure is fixed across its GN iterations).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+namespace m3s {
+
+struct SparsePlan {
+  int m = 0;       // free poses (N - 1)
+  int S = 0;       // 7x7 block slots of L: [0, m) diagonals, then off-diagonals
+  int levels = 0;  // elimination-tree levels
+  std::vector<int32_t> perm;   // new -> old variable
+  std::vector<int32_t> iperm;  // old -> new
+  // per column k (new order): struct(k) = rows i > k with L_ik != 0
+  std::vector<int32_t> col_ptr, col_row, col_slot;
+  // columns grouped by level (leaves first)
+  std::vector<int32_t> lev_ptr, lev_col;
+  // left-looking diagonal updates of column k: D_k -= L_kp L_kp^T
+  std::vector<int32_t> dtr_ptr, dtr_slot, dtr_p;
+  // off-diagonal tasks (one output block L_ik each), grouped by level
+  std::vector<int32_t> task_lev_ptr, task_dst, task_col, task_tr_ptr, tr_a, tr_b;
+  // assembly: slot s receives sum over asm edges of (+H_jj diag, -H_jj off-diag)
+  std::vector<int32_t> asm_ptr, asm_edge;
+  // RHS of new variable v: sum over entries (edge << 1 | sign) of (sign ? +g_j : -g_j)
+  std::vector<int32_t> g_ptr, g_edge;
+};
+
+// ranks of (ii, jj) in sorted-unique(cat(ii, jj)); returns the unique count
+int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int32_t> &ri,
+               std::vector<int32_t> &rj);
+
+// Build the plan for N poses (rank 0 fixed) and edges with ranks (ri, rj).
+void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
+                       SparsePlan &P);
+
+// Flattened int32 image of the plan (offsets of each array into it).
+struct PlanImage {
+  std::vector<int32_t> data;
+  int64_t off_perm, off_col_ptr, off_col_row, off_col_slot, off_lev_ptr, off_lev_col, off_dtr_ptr,
+      off_dtr_slot, off_dtr_p, off_task_lev_ptr, off_task_dst, off_task_col, off_task_tr_ptr,
+      off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge;
+};
+void flatten_plan(const SparsePlan &P, PlanImage &img);
+
+}  // namespace m3s

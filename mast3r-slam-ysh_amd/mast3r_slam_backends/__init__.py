@@ -78,6 +78,7 @@ EXPORTS = (
     "m3s_gn_workspace_size", "m3s_gauss_newton_points", "m3s_gauss_newton_rays",
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
+    "m3s_sparse_plan_debug",
 )
 
 
@@ -106,6 +107,8 @@ def _load():
         getattr(lib, f).argtypes = [P(TrackArgs), _VP]
     lib.m3s_version.restype = ctypes.c_char_p
     lib.m3s_version.argtypes = []
+    lib.m3s_sparse_plan_debug.restype = ctypes.c_int64
+    lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, _VP, ctypes.c_int64, _VP]
     return lib
 
 
@@ -114,6 +117,46 @@ _lib = _load()
 
 def version() -> str:
     return _lib.m3s_version().decode()
+
+
+PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col", "dtr_ptr",
+                 "dtr_slot", "dtr_p", "task_lev_ptr", "task_dst", "task_col", "task_tr_ptr", "tr_a",
+                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge")
+
+
+def sparse_plan(N, ri, rj):
+    """Host symbolic plan of the block-sparse LLT (diagnostics/tests; CPU only)."""
+    import numpy as np
+
+    ri = np.ascontiguousarray(ri, dtype=np.int32)
+    rj = np.ascontiguousarray(rj, dtype=np.int32)
+    meta = np.zeros(22, np.int32)
+    P = ctypes.c_void_p
+    n = _lib.m3s_sparse_plan_debug(int(N), ri.size, P(ri.ctypes.data), P(rj.ctypes.data), None, 0,
+                                   P(meta.ctypes.data))
+    out = np.zeros(max(n, 1), np.int32)
+    _lib.m3s_sparse_plan_debug(int(N), ri.size, P(ri.ctypes.data), P(rj.ctypes.data),
+                               P(out.ctypes.data), n, P(meta.ctypes.data))
+    offs = list(meta[3:]) + [n]
+    plan = {"m": int(meta[0]), "S": int(meta[1]), "levels": int(meta[2])}
+    for k, name in enumerate(PLAN_SECTIONS):
+        plan[name] = out[offs[k]:]
+    m, S, L = plan["m"], plan["S"], plan["levels"]
+    T = int(plan["task_lev_ptr"][L])
+    lens = {"perm": m, "col_ptr": m + 1, "lev_ptr": L + 1, "lev_col": m, "dtr_ptr": m + 1,
+            "task_lev_ptr": L + 1, "task_dst": T, "task_col": T, "task_tr_ptr": T + 1,
+            "asm_ptr": S + 1, "g_ptr": m + 1}
+    for name, ln in lens.items():
+        plan[name] = plan[name][:ln]
+    nnz = int(plan["col_ptr"][m])
+    plan["col_row"], plan["col_slot"] = plan["col_row"][:nnz], plan["col_slot"][:nnz]
+    nd = int(plan["dtr_ptr"][m])
+    plan["dtr_slot"], plan["dtr_p"] = plan["dtr_slot"][:nd], plan["dtr_p"][:nd]
+    nt = int(plan["task_tr_ptr"][T])
+    plan["tr_a"], plan["tr_b"] = plan["tr_a"][:nt], plan["tr_b"][:nt]
+    plan["asm_edge"] = plan["asm_edge"][:int(plan["asm_ptr"][S])]
+    plan["g_edge"] = plan["g_edge"][:int(plan["g_ptr"][m])]
+    return plan
 
 
 # ------------------------------------------------------------------ checks --

@@ -278,3 +278,19 @@ def test_gn_tiled_cholesky_singular_zero_dx(be):
     assert info[be.INFO_SOLVE_FAIL] == 5 and info[be.INFO_ITERS] == 5
     assert np.all(dx == 0)
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
+
+
+@pytest.mark.parametrize("N", [6, 32, 70])
+def test_sparse_llt_matches_dense_llt(be, N, monkeypatch):
+    """Block-sparse LLT (default; LDS-resident for small plans, global for
+    N=70) against the dense fallback (M3S_DENSE=1) on identical inputs."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 24, 32, seed=90 + N)
+    T_s, dx_s, info_s = run_gpu(be, "rays", g, 3, 0.0)
+    monkeypatch.setenv("M3S_DENSE", "1")
+    T_d, dx_d, info_d = run_gpu(be, "rays", g, 3, 0.0)
+    monkeypatch.delenv("M3S_DENSE")
+    assert info_s[be.INFO_ITERS] == info_d[be.INFO_ITERS] == 3
+    np.testing.assert_allclose(dx_s, dx_d, atol=1e-6 + 1e-5 * np.abs(dx_d).max())
+    np.testing.assert_allclose(T_s, T_d, atol=1e-5)

@@ -150,10 +150,15 @@ const char *m3s_version(void);
 
 /* Diagnostic: the host symbolic plan of the block-sparse LLT for N poses and
  * edge ranks (ri, rj) (pose rank 0 fixed). Writes the flattened int32 plan to
- * out (if cap suffices) and meta[0..21] = {m, S, levels, 19 section offsets in
+ * out (if cap suffices) and meta[0..23] = {m, S, levels, 21 section offsets in
  * the order of m3s_symbolic.h}. Returns the plan length in int32 words. */
 int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj,
                               int32_t *out, int64_t cap, int32_t *meta);
+
+/* Diagnostic: byte offsets of the workspace sections for (N, HW, E), in the
+ * order flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk,
+ * Dinv, tasks, planes, total (offs[14]). Returns the total. */
+size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs);
 
 #ifdef __cplusplus
 }

@@ -254,24 +254,72 @@ struct ResidualParams {
   float huber_k;
 };
 
-// One (edge, pixel) contribution. Xi: target point (KF i, gathered),
-// Y = T_ij Xj: source point in frame i. `ok` = match/threshold validity.
-// u_t/v_t: target pixel (calib).
+// Per (edge, pixel) target-side inputs of the residual: everything that does
+// not depend on the poses. The backend computes them once per solve call and
+// stores them as per-edge planes (see linearize_packed_kernel), so later GN
+// iterations read 12-20 B per pixel and never gather from KF i. Both the
+// gathering and the packed kernels go through make_pixin + pixel_contrib (same
+// formulas; the sums differ only by FMA-contraction rounding between kernels).
+//   points: {Xi.x, Xi.y, Xi.z, sq}          rays: {ri.x, ri.y, ri.z, |Xi|, sq}
+//   calib:  {(v_t << 16 | u_t) as bits, sq, log z_i}
+// sq = sqrt(q) if the match is valid (valid_match, q > Q_thresh, ci/cj >
+// C_thresh; calib also z_i > z_eps), else 0: a zero weight zeroes the
+// pixel's contribution exactly as the reference's `valid ? ... : 0` does.
 template <int MODE>
-__device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &P, const float *Xi,
-                                              const float *Y, bool ok, float q, int u_t, int v_t) {
-  if (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
+struct PixIn;
+template <>
+struct PixIn<0> {
+  static constexpr int kPlanes = 4;
+  float v[4];
+};
+template <>
+struct PixIn<1> {
+  static constexpr int kPlanes = 5;
+  float v[5];
+};
+template <>
+struct PixIn<2> {
+  static constexpr int kPlanes = 3;
+  float v[3];
+};
+
+template <int MODE>
+__device__ __forceinline__ PixIn<MODE> make_pixin(const ResidualParams &P, const float *Xi, bool ok,
+                                                  float q, int u_t, int v_t) {
+  PixIn<MODE> r;
+  if (MODE == 1) {  // ray_align_kernel :924-963
     const float ni = fsqrt(Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2]);
     const float ini = frcp(ni);
+    r.v[0] = Xi[0] * ini, r.v[1] = Xi[1] * ini, r.v[2] = Xi[2] * ini, r.v[3] = ni;
+    r.v[4] = ok ? fsqrt(q) : 0.0f;
+  } else if (MODE == 2) {  // calib_proj_kernel :1360-1405
+    const bool vzi = Xi[2] > P.z_eps;
+    const float li = flog(Xi[2]);
+    r.v[0] = __int_as_float((v_t << 16) | u_t);
+    r.v[1] = (ok && vzi) ? fsqrt(q) : 0.0f;
+    r.v[2] = vzi ? li : 0.0f;
+  } else {  // point_align_kernel :564-586
+    r.v[0] = Xi[0], r.v[1] = Xi[1], r.v[2] = Xi[2];
+    r.v[3] = ok ? fsqrt(q) : 0.0f;
+  }
+  return r;
+}
+
+// One (edge, pixel) contribution from the target-side inputs and
+// Y = T_ij Xj (source point in frame i).
+template <int MODE>
+__device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &P, const PixIn<MODE> &in,
+                                              const float *Y) {
+  if (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
     const float nj2 = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
     const float nj = fsqrt(nj2);
     const float inj = frcp(nj);
     const float rx = Y[0] * inj, ry = Y[1] * inj, rz = Y[2] * inj;
-    const float e0 = rx - Xi[0] * ini, e1 = ry - Xi[1] * ini, e2 = rz - Xi[2] * ini;
-    const float e3 = nj - ni;
-    const float sq = fsqrt(q);
-    const float swr = ok ? P.inv_sig_a * sq : 0.0f;
-    const float swd = ok ? P.inv_sig_b * sq : 0.0f;
+    const float e0 = rx - in.v[0], e1 = ry - in.v[1], e2 = rz - in.v[2];
+    const float e3 = nj - in.v[3];
+    const float sq = in.v[4];
+    const float swr = P.inv_sig_a * sq;
+    const float swd = P.inv_sig_b * sq;
     const float kr = swr * swr, kd = swd * swd;
     const float w0 = huber_w(swr * e0, P.huber_k) * kr;
     const float w1 = huber_w(swr * e1, P.huber_k) * kr;
@@ -289,20 +337,22 @@ __device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &
     accum_row<kRayZ>(acc, a2, w2, e2);
     accum_row<kRayD>(acc, a3, w3, e3);
   } else if (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
-    const bool vz = (Y[2] > P.z_eps) && (Xi[2] > P.z_eps);
+    const bool vz = Y[2] > P.z_eps;  // z_i > z_eps is folded into sq
     // computed unconditionally and selected (no exec-mask branches); the
     // unselected values may be inf/NaN and never reach the sums
-    const float zr = frcp(Y[2]), lj_ = flog(Y[2]), li_ = flog(Xi[2]);
+    const float zr = frcp(Y[2]), lj_ = flog(Y[2]);
     const float zinv = vz ? zr : 0.0f;
     const float lzj = vz ? lj_ : 0.0f;
-    const float lzi = vz ? li_ : 0.0f;
+    const float lzi = vz ? in.v[2] : 0.0f;
+    const int uv = __float_as_int(in.v[0]);
+    const float u_t = (float)(uv & 0xffff), v_t = (float)(uv >> 16);
     const float x = Y[0] * zinv, y = Y[1] * zinv;
     const float u = P.fx * x + P.cx, v = P.fy * y + P.cy;
     const bool vu = (u > P.border) && (u < (float)P.width - 1.0f - P.border);
     const bool vv = (v > P.border) && (v < (float)P.height - 1.0f - P.border);
-    const float e0 = u - (float)u_t, e1 = v - (float)v_t, e2 = lzj - lzi;
-    const bool good = ok && vu && vv && vz;
-    const float sq = fsqrt(q);
+    const float e0 = u - u_t, e1 = v - v_t, e2 = lzj - lzi;
+    const bool good = vu && vv && vz;
+    const float sq = in.v[1];
     const float swp = good ? P.inv_sig_a * sq : 0.0f;
     const float swz = good ? P.inv_sig_b * sq : 0.0f;
     const float kp = swp * swp, kz = swz * swz;
@@ -317,8 +367,8 @@ __device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &
     accum_row<kCalV>(acc, a1, w1, e1);
     accum_row<kCalZ>(acc, a2, w2, e2);
   } else {  // 3D point (point_align_kernel :564-674)
-    const float e0 = Y[0] - Xi[0], e1 = Y[1] - Xi[1], e2 = Y[2] - Xi[2];
-    const float sw = ok ? P.inv_sig_a * fsqrt(q) : 0.0f;
+    const float e0 = Y[0] - in.v[0], e1 = Y[1] - in.v[1], e2 = Y[2] - in.v[2];
+    const float sw = P.inv_sig_a * in.v[3];
     const float k2 = sw * sw;
     const float w0 = huber_w(sw * e0, P.huber_k) * k2;
     const float w1 = huber_w(sw * e1, P.huber_k) * k2;

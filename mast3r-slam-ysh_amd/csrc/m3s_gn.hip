@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -52,7 +53,10 @@ namespace {
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
-constexpr int kTargetBlocks = 2048;  // ~8 blocks per CU on 256 CUs
+#ifndef M3S_TARGET_BLOCKS
+#define M3S_TARGET_BLOCKS 2048
+#endif
+constexpr int kTargetBlocks = M3S_TARGET_BLOCKS;  // linearize grid target (edges x chunks)
 constexpr int kMaxSmallNp = 224;     // register Cholesky limit (n + 1 <= 7 * 32)
 constexpr int kCholThreads = 512;    // 16 x 32 thread grid
 constexpr int64_t kMaxLd = 8192;     // tiled path: back-substitution keeps x in LDS
@@ -79,7 +83,8 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 }
 
 struct Layout {
-  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, total;
+  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, tasks, planes,
+      total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -119,8 +124,12 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 49 * (size_t)L.slot_cap, 256);
   L.Dinv = off;
   off = align_up(off + sizeof(double) * 49 * (size_t)(m + 1), 256);
+  L.tasks = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
+  // target-side planes of every edge (5 planes = rays, the widest mode)
+  L.planes = off;
+  off = align_up(off + sizeof(float) * 5 * (size_t)E * (size_t)HW, 256);
   L.total = off;
-  (void)HW;
   return L;
 }
 
@@ -142,18 +151,19 @@ struct LinArgs {
   const int32_t *rank_i;
   const int32_t *rank_j;
   const int32_t *stop;
-  float *partials;
+  const int32_t *tasks;    // block -> task (e_loc * chunks + c), -1 = idle; null = identity
+  float *planes;           // per-edge target-side planes (PixIn), [E_loc][kPlanes][HW]
+  float *partials;         // [task][36]
   int64_t HW, edge_begin, chunks, chunk_pix;
   ResidualParams P;
 };
 
-// one pixel's inputs -> contribution (shared by the vector and scalar paths)
+// one pixel's gathered inputs -> target-side inputs (shared by all paths)
 template <int MODE, bool TRACK>
-__device__ __forceinline__ void do_pixel(float *acc, const LinArgs &A, const Sim3f &Tij,
-                                         const float *Xs_i, const float *Cs_i, int64_t p, bool vm,
-                                         int64_t id_raw, float q, const float *Xj, float cj) {
+__device__ __forceinline__ PixIn<MODE> gather_pixel(const LinArgs &A, const float *Xs_i, const float *Cs_i,
+                                                    int64_t p, bool vm, int64_t id_raw, float q, float cj) {
   const int64_t id = TRACK ? p : (vm ? id_raw : 0);
-  float Xi[3] = {Xs_i[3 * id + 0], Xs_i[3 * id + 1], Xs_i[3 * id + 2]};
+  const float Xi[3] = {Xs_i[3 * id + 0], Xs_i[3 * id + 1], Xs_i[3 * id + 2]};
   bool ok;
   if (TRACK) {
     ok = vm;
@@ -161,10 +171,8 @@ __device__ __forceinline__ void do_pixel(float *acc, const LinArgs &A, const Sim
     const float ci = Cs_i[id];
     ok = vm && (q > A.P.Q_thresh) && (ci > A.P.C_thresh) && (cj > A.P.C_thresh);
   }
-  float Y[3];
-  act(Tij, Xj, Y);
   int u_t = 0, v_t = 0;
-  if (MODE == M3S_MODE_CALIB) {
+  if (MODE == M3S_MODE_CALIB) {  // ind_Xi % width, ind_Xi / width (gn_kernels.cu:1360-1361)
     const int iid = (int)id;
     int vv = (int)((float)iid * (1.0f / (float)A.P.width));
     if (vv * A.P.width > iid) vv--;
@@ -172,7 +180,12 @@ __device__ __forceinline__ void do_pixel(float *acc, const LinArgs &A, const Sim
     v_t = vv;
     u_t = iid - vv * A.P.width;
   }
-  pixel_contrib<MODE>(acc, A.P, Xi, Y, ok, q, u_t, v_t);
+  return make_pixin<MODE>(A.P, Xi, ok, q, u_t, v_t);
+}
+
+// block -> (edge, chunk) through the XCD-grouped task table
+__device__ __forceinline__ int64_t block_task(const LinArgs &A) {
+  return A.tasks ? (int64_t)A.tasks[blockIdx.x] : (int64_t)blockIdx.x;
 }
 
 // Block reduction of the 36 per-thread sums through LDS: every thread stores
@@ -240,10 +253,36 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 
 // Each lane owns 4 consecutive pixels (one 16-B vector per stream); a wave
 // sweeps 256 pixels per trip, a block 1024.
-template <int MODE, bool TRACK, bool VEC>
+// 36 per-thread sums -> one block partial
+__device__ __forceinline__ void store_partial(const float *acc, float *out) {
+#if M3S_LDS_REDUCE
+  block_reduce_store(acc, out);
+#else
+  // wave64 butterfly, then the 4 waves through LDS
+  __shared__ float red[kThreads / 64][kNP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kNP; k++) {
+    const float v = wave_sum(acc[k]);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNP) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) s += red[w][threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+#endif
+}
+
+// WPACK: also store the target-side planes for the packed kernel (first GN
+// iteration of a solve call).
+template <int MODE, bool TRACK, bool VEC, bool WPACK>
 __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
   if (*A.stop) return;
-  const int64_t b = blockIdx.x;
+  const int64_t b = block_task(A);
+  if (b < 0) return;
   const int64_t e_loc = b / A.chunks;
   const int64_t c = b - e_loc * A.chunks;
   const int64_t e = A.edge_begin + e_loc;
@@ -268,6 +307,8 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
   const int64_t *__restrict__ idx = TRACK ? nullptr : A.idx + eoff;
   const uint8_t *__restrict__ valid = A.valid + eoff;
   const float *__restrict__ Qe = A.Q + eoff;
+  constexpr int NPL = PixIn<MODE>::kPlanes;
+  float *__restrict__ pl = WPACK ? A.planes + (size_t)e_loc * NPL * HW : nullptr;
 
   float acc[kNP];
 #pragma unroll
@@ -295,10 +336,22 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
       const float Xj[4][3] = {{xa.x, xa.y, xa.z}, {xa.w, xb.x, xb.y}, {xb.z, xb.w, xc.x}, {xc.y, xc.z, xc.w}};
       const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
       const float cjs[4] = {c4.x, c4.y, c4.z, c4.w};
+      PixIn<MODE> in[4];
 #pragma unroll
-      for (int s = 0; s < 4; s++)
-        do_pixel<MODE, TRACK>(acc, A, Tij, Xs_i, Cs_i, p0 + s, ((vb >> (8 * s)) & 0xffu) != 0,
-                              ids[s], qs[s], Xj[s], cjs[s]);
+      for (int s = 0; s < 4; s++) {
+        in[s] = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p0 + s, ((vb >> (8 * s)) & 0xffu) != 0, ids[s],
+                                          qs[s], cjs[s]);
+        float Y[3];
+        act(Tij, Xj[s], Y);
+        pixel_contrib<MODE>(acc, A.P, in[s], Y);
+      }
+      if (WPACK) {
+#pragma unroll
+        for (int k = 0; k < NPL; k++) {
+          const f32x4 v = {in[0].v[k], in[1].v[k], in[2].v[k], in[3].v[k]};
+          *reinterpret_cast<f32x4 *>(pl + (size_t)k * HW + p0) = v;
+        }
+      }
     }
   } else {
     for (int64_t p = p_begin + threadIdx.x; p < p_end; p += kThreads) {
@@ -306,28 +359,103 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
       const int64_t id = TRACK ? p : idx[p];
       const float Xj[3] = {Xs_j[3 * p], Xs_j[3 * p + 1], Xs_j[3 * p + 2]};
       const float cj = TRACK ? 0.0f : Cs_j[p];
-      do_pixel<MODE, TRACK>(acc, A, Tij, Xs_i, Cs_i, p, vm, id, Qe[p], Xj, cj);
+      const PixIn<MODE> in = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p, vm, id, Qe[p], cj);
+      float Y[3];
+      act(Tij, Xj, Y);
+      pixel_contrib<MODE>(acc, A.P, in, Y);
+      if (WPACK) {
+#pragma unroll
+        for (int k = 0; k < NPL; k++) pl[(size_t)k * HW + p] = in.v[k];
+      }
     }
   }
-#if M3S_LDS_REDUCE
-  block_reduce_store(acc, A.partials + (size_t)b * kNP);
-#else
-  // wave64 butterfly, then the 4 waves through LDS
-  __shared__ float red[kThreads / 64][kNP];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  store_partial(acc, A.partials + (size_t)b * kNP);
+}
+
+// Later GN iterations of a solve call: target-side inputs from the planes the
+// first iteration stored, Xj streamed (shared through L2 by the edges of one
+// keyframe, which the task table places on one XCD back to back). No gathers.
+template <int MODE>
+__global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
+  if (*A.stop) return;
+  const int64_t b = block_task(A);
+  if (b < 0) return;
+  const int64_t e_loc = b / A.chunks;
+  const int64_t c = b - e_loc * A.chunks;
+  const int64_t e = A.edge_begin + e_loc;
+  const int64_t HW = A.HW;
+  const int ri = A.rank_i[e], rj = A.rank_j[e];
+  const Sim3f Tij = relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj));
+  const float *__restrict__ Xs_j = A.Xs + (size_t)rj * HW * 3;
+  constexpr int NPL = PixIn<MODE>::kPlanes;
+  const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
+
+  float acc[kNP];
 #pragma unroll
-  for (int k = 0; k < kNP; k++) {
-    const float v = wave_sum(acc[k]);
-    if (lane == 0) red[wave][k] = v;
+  for (int k = 0; k < kNP; k++) acc[k] = 0.0f;
+  const int64_t p_begin = c * A.chunk_pix;
+  const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
+#ifndef M3S_PK_GROUP
+#define M3S_PK_GROUP 1
+#endif
+#ifndef M3S_PK_PREFETCH
+#define M3S_PK_PREFETCH 0
+#endif
+  // one trip = 4 pixels per lane: NPL plane vectors + 3 Xj vectors (16 B each)
+  auto load_trip = [&](int64_t q, f32x4 *pv, f32x4 *xv) {
+#if M3S_PK_NOLOAD  // experiment: compute floor (no memory traffic)
+    const float f = (float)(q & 1023) * 1e-3f;
+    for (int k = 0; k < NPL; k++) pv[k] = f32x4{1.0f + f, 2.0f, 0.5f, f};
+    xv[0] = f32x4{f, 0.1f, 2.0f + f, 0.2f}, xv[1] = f32x4{0.3f, 2.1f, f, 0.1f}, xv[2] = f32x4{1.9f, f, 0.2f, 2.2f};
+    return;
+#endif
+#pragma unroll
+    for (int k = 0; k < NPL; k++) pv[k] = ld_stream(reinterpret_cast<const f32x4 *>(pl + (size_t)k * HW + q));
+    const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * q);
+    xv[0] = xj4[0], xv[1] = xj4[1], xv[2] = xj4[2];
+  };
+  auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
+#if M3S_PK_NOCOMPUTE  // experiment: memory floor
+    for (int k = 0; k < NPL; k++) acc[k] += pv[k].x + pv[k].y + pv[k].z + pv[k].w;
+    acc[8] += xv[0].x + xv[1].y + xv[2].z;
+    return;
+#endif
+    const float Xj[4][3] = {{xv[0].x, xv[0].y, xv[0].z}, {xv[0].w, xv[1].x, xv[1].y},
+                            {xv[1].z, xv[1].w, xv[2].x}, {xv[2].y, xv[2].z, xv[2].w}};
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      PixIn<MODE> in;
+#pragma unroll
+      for (int k = 0; k < NPL; k++) in.v[k] = pv[k][s];
+      float Y[3];
+      act(Tij, Xj[s], Y);
+      pixel_contrib<MODE>(acc, A.P, in, Y);
+      // one pixel at a time: keeps the packed kernel at ~90 VGPRs (5 waves/SIMD)
+      if ((s + 1) % M3S_PK_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#if M3S_PK_PREFETCH
+  // software pipeline: the next trip's loads are in flight during this trip's math
+  int64_t p0 = p_begin + kPixPerThread * threadIdx.x;
+  f32x4 pv[NPL], xv[3];
+  if (p0 < p_end) load_trip(p0, pv, xv);
+  for (; p0 < p_end; p0 += kBlockPix) {
+    f32x4 pn[NPL], xn[3];
+    const int64_t q = p0 + kBlockPix;
+    if (q < p_end) load_trip(q, pn, xn);
+    do_trip(pv, xv);
+#pragma unroll
+    for (int k = 0; k < NPL; k++) pv[k] = pn[k];
+    xv[0] = xn[0], xv[1] = xn[1], xv[2] = xn[2];
   }
-  __syncthreads();
-  if (threadIdx.x < kNP) {
-    float s = 0.0f;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; w++) s += red[w][threadIdx.x];
-    A.partials[(size_t)b * kNP + threadIdx.x] = s;
+#else
+  for (int64_t p0 = p_begin + kPixPerThread * threadIdx.x; p0 < p_end; p0 += kBlockPix) {
+    f32x4 pv[NPL], xv[3];
+    load_trip(p0, pv, xv);
+    do_trip(pv, xv);
   }
 #endif
+  store_partial(acc, A.partials + (size_t)b * kNP);
 }
 
 // fp64 sum of each edge's chunk partials (fixed order)
@@ -662,8 +790,13 @@ __global__ void __launch_bounds__(1024) backsolve_kernel(const double *__restric
 // ------------------------------------------------- block-sparse LLT ----
 // Per edge: H_jj = M L M^T and g_j = M l in fp64 (M = Adj(T_i)^-T), written
 // as fin[e][0:49] (row-major) and fin[e][49:56]. One 64-thread block per edge.
+// The edge's local sums come from edge_sums, or (single-GPU path) straight
+// from the linearize chunk partials, summed in fp64 in chunk order exactly as
+// edge_reduce_kernel does.
 constexpr int kFin = 56;
 __global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__restrict__ edge_sums,
+                                                            const float *__restrict__ partials,
+                                                            int64_t chunks,
                                                             const int32_t *__restrict__ rank_i,
                                                             const float *__restrict__ Twc,
                                                             double *__restrict__ fin,
@@ -671,8 +804,18 @@ __global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__rest
   if (*stop) return;
   const int64_t e = blockIdx.x;
   const int t = threadIdx.x;
-  __shared__ double M[7][7], Lm[7][7], T1[7][7], l[7];
+  __shared__ double M[7][7], Lm[7][7], T1[7][7], l[7], esl[kNP];
   const double *es = edge_sums + (size_t)e * kNP;
+  if (partials) {
+    if (t < kNP) {
+      double acc = 0.0;
+      const float *p = partials + (size_t)e * chunks * kNP + t;
+      for (int64_t c = 0; c < chunks; c++) acc += (double)p[(size_t)c * kNP];
+      esl[t] = acc;
+    }
+    __syncthreads();
+    es = esl;
+  }
   if (t == 0) adjT_inv_matrix(Twc + 8 * (size_t)rank_i[e], M);
   if (t < 49) {
     const int a = t / 7, c = t % 7;
@@ -703,8 +846,8 @@ __global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__rest
 struct SparseDev {
   const int32_t *plan;  // flattened plan (global); copied to LDS by the IN_LDS variant
   int plan_len;
-  int off[19];          // section offsets, order of m3s_symbolic.h
-  int m, S, levels;
+  int off[kPlanSections];  // section offsets, order of m3s_symbolic.h
+  int m, S, levels, n_items;
   double *L;     // [S][49] (global variant)
   double *Dinv;  // [m][49] (global variant)
   const double *fin;
@@ -735,6 +878,22 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   return x;
 }
 
+// Wait (whole wave) for a workgroup-scope completion flag. Bounded: a schedule
+// bug can never hang the GPU; it shows up as a solve failure instead.
+__device__ __forceinline__ void wait_flag(int32_t *flag, int *fail) {
+  int it = 0;
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && it < (1 << 21)) {
+    __builtin_amdgcn_s_sleep(1);
+    it++;
+  }
+  if (it >= (1 << 21)) {
+    *fail = 1;
+#if M3S_LLT_DEBUG
+    printf("wait timeout on %p\n", (void *)flag);
+#endif
+  }
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -760,6 +919,9 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // index arrays: LDS copy (IN_LDS) or global
   const int32_t *pl = D.plan;
+#if M3S_LLT_DEBUG
+  if (tid == 0) printf("llt start IN_LDS=%d m=%d S=%d plan_len=%d levels=%d\n", (int)IN_LDS, m, S, D.plan_len, D.levels);
+#endif
   if (IN_LDS) {
     int32_t *lp = reinterpret_cast<int32_t *>(y + (size_t)m * 7);
     for (int q = tid; q < D.plan_len; q += 1024) lp[q] = D.plan[q];
@@ -771,10 +933,26 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
                 *task_lev_ptr = pl + D.off[9], *task_dst = pl + D.off[10], *task_col = pl + D.off[11],
                 *task_tr_ptr = pl + D.off[12], *tr_a = pl + D.off[13], *tr_b = pl + D.off[14],
                 *asm_ptr = pl + D.off[15], *asm_edge = pl + D.off[16], *g_ptr = pl + D.off[17],
-                *g_edge = pl + D.off[18];
-  if (IN_LDS) __syncthreads();
+                *g_edge = pl + D.off[18], *items = pl + D.off[20];
+  // completion flags of the dataflow schedule: sdone[slot] (factorisation,
+  // diagonal slot k = DIAG(k)), done2[column] (back-substitution)
+  int32_t *sdone = IN_LDS ? const_cast<int32_t *>(pl) + ((D.plan_len + 1) & ~1)
+                          : reinterpret_cast<int32_t *>(y + (size_t)m * 7);
+  int32_t *done2 = sdone + S;
+  for (int q = tid; q < S + m; q += 1024) sdone[q] = 0;
+  __syncthreads();  // plan copy complete
   const int r = lane / 7, c = lane % 7;
   const bool act49 = lane < 49;
+  // clamped row offsets: lanes >= 49 (>= 7) load valid entries and discard them
+  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
+  const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
+#if M3S_LLT_TIMING  // experiment: phase timestamps (100 MHz wall clock) into flags[16..]
+  int64_t *tsv = reinterpret_cast<int64_t *>(D.flags + 16);
+  if (tid == 0) tsv[0] = wall_clock64();
+#define M3S_TS(i) if (tid == 0) tsv[i] = wall_clock64();
+#else
+#define M3S_TS(i)
+#endif
   double *scr = scratch[wave];
   constexpr int NW = 16;
 
@@ -797,39 +975,60 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
   if (tid == 0) fail_s = 0;
   __syncthreads();
+  M3S_TS(1)
 
-  // 1. factorisation + forward substitution
-  for (int l = 0; l < D.levels; l++) {
-    for (int t = lev_ptr[l] + wave; t < lev_ptr[l + 1]; t += NW) {  // phase A
-      const int k = lev_col[t];
-      double v = act49 ? Lb[(size_t)k * 49 + lane] : 0.0;
-      for (int q = dtr_ptr[k]; q < dtr_ptr[k + 1]; q++) {
-        const double *A = Lb + (size_t)dtr_slot[q] * 49;
-        if (act49) {
-          double s = 0.0;
+  // 1. factorisation + forward substitution as a dataflow over work items:
+  // DIAG(k) (diagonal block, W_k = L_kk^-1, forward step of y_k) and OFF(i,k)
+  // (one off-diagonal block). Items are listed column by column in
+  // elimination-tree level order (items[]); wave w runs items w, w+16, ...
+  // Each item waits on LDS completion flags of exactly the blocks it reads
+  // (sdone[slot]) and publishes its own block. Every dependency points to an
+  // earlier item, so the lowest unfinished item can always run: no deadlock,
+  // and no workgroup barriers inside the factorisation.
+  const int n_items = D.n_items;
+  for (int it = wave; it < n_items; it += NW) {
+    const int item = items[it];
+    if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k, y_k
+      const int k = -1 - item;
+      const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
+      for (int q = q0; q < q1; q++) wait_flag(&sdone[dtr_slot[q]], &fail_s);
+      double v = Lb[(size_t)k * 49 + lane49];
+      double bb = y[k * 7 + lane7];
+      int q = q0;
+      for (; q + 1 < q1; q += 2) {  // two updates in flight
+        const double *A0 = Lb + (size_t)dtr_slot[q] * 49, *A1 = Lb + (size_t)dtr_slot[q + 1] * 49;
+        const double *y0 = y + dtr_p[q] * 7, *y1 = y + dtr_p[q + 1] * 7;
+        double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
 #pragma unroll
-          for (int mm = 0; mm < 7; mm++) s += A[r * 7 + mm] * A[c * 7 + mm];
-          v -= s;
+        for (int mm = 0; mm < 7; mm++) {
+          s0 += A0[r7 + mm] * A0[c7 + mm];
+          s1 += A1[r7 + mm] * A1[c7 + mm];
+          t0 += A0[l7 + mm] * y0[mm];
+          t1 += A1[l7 + mm] * y1[mm];
         }
+        v -= s0;
+        v -= s1;
+        bb -= t0;
+        bb -= t1;
       }
-      // b_k - sum_p L_kp y_p on lanes 0..6
-      double bb = (lane < 7) ? y[k * 7 + lane] : 0.0;
-      for (int q = dtr_ptr[k]; q < dtr_ptr[k + 1]; q++) {
-        const double *A = Lb + (size_t)dtr_slot[q] * 49;
-        const int p = dtr_p[q];
-        if (lane < 7) {
-          double s = 0.0;
+      if (q < q1) {
+        const double *A0 = Lb + (size_t)dtr_slot[q] * 49;
+        const double *y0 = y + dtr_p[q] * 7;
+        double s0 = 0.0, t0 = 0.0;
 #pragma unroll
-          for (int mm = 0; mm < 7; mm++) s += A[lane * 7 + mm] * y[p * 7 + mm];
-          bb -= s;
+        for (int mm = 0; mm < 7; mm++) {
+          s0 += A0[r7 + mm] * A0[c7 + mm];
+          t0 += A0[l7 + mm] * y0[mm];
         }
+        v -= s0;
+        bb -= t0;
       }
       // entry layout -> row layout through the wave's scratch
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double a[7];
 #pragma unroll
-      for (int q = 0; q < 7; q++) a[q] = (lane < 7) ? scr[lane * 7 + q] : 0.0;
+      for (int qq = 0; qq < 7; qq++) a[qq] = (lane < 7) ? scr[lane * 7 + qq] : 0.0;
       wave_lds_fence();
       // Cholesky: lane r holds row r; column j of L broadcast by readlane
       bool bad = false;
@@ -867,77 +1066,95 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       }
       if (lane < 7) {
 #pragma unroll
-        for (int q = 0; q < 7; q++) {
-          Lb[(size_t)k * 49 + lane * 7 + q] = (q <= lane) ? a[q] : 0.0;  // row `lane` of L_kk
-          Di[(size_t)k * 49 + q * 7 + lane] = w[q];                      // column `lane` of W
+        for (int qq = 0; qq < 7; qq++) {
+          Lb[(size_t)k * 49 + lane * 7 + qq] = (qq <= lane) ? a[qq] : 0.0;  // row `lane` of L_kk
+          Di[(size_t)k * 49 + qq * 7 + lane] = w[qq];                       // column `lane` of W
         }
         double yo = 0.0;
 #pragma unroll
-        for (int q = 0; q < 7; q++) yo = (q == lane) ? yk[q] : yo;
+        for (int qq = 0; qq < 7; qq++) yo = (qq == lane) ? yk[qq] : yo;
         y[k * 7 + lane] = yo;
       }
-      if (bad && lane == 0) fail_s = 1;
-    }
-    __syncthreads();
-    if (fail_s) break;  // uniform
-    for (int t = task_lev_ptr[l] + wave; t < task_lev_ptr[l + 1]; t += NW) {  // phase B
-      const int dst = task_dst[t], k = task_col[t];
-      double v = act49 ? Lb[(size_t)dst * 49 + lane] : 0.0;
-      for (int q = task_tr_ptr[t]; q < task_tr_ptr[t + 1]; q++) {
-        const double *A = Lb + (size_t)tr_a[q] * 49;
-        const double *B = Lb + (size_t)tr_b[q] * 49;
-        if (act49) {
-          double s = 0.0;
+      if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
+      const int t2 = item;
+      const int dst = task_dst[t2], k = task_col[t2];
+      const int q0 = task_tr_ptr[t2], q1 = task_tr_ptr[t2 + 1];
+      wait_flag(&sdone[k], &fail_s);  // W_k and (through DIAG(k)) every L_kp
+      for (int q = q0; q < q1; q++) wait_flag(&sdone[tr_a[q]], &fail_s);
+      double v = Lb[(size_t)dst * 49 + lane49];
+      int q = q0;
+      for (; q + 1 < q1; q += 2) {
+        const double *A0 = Lb + (size_t)tr_a[q] * 49, *B0 = Lb + (size_t)tr_b[q] * 49;
+        const double *A1 = Lb + (size_t)tr_a[q + 1] * 49, *B1 = Lb + (size_t)tr_b[q + 1] * 49;
+        double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-          for (int mm = 0; mm < 7; mm++) s += A[r * 7 + mm] * B[c * 7 + mm];
-          v -= s;
+        for (int mm = 0; mm < 7; mm++) {
+          s0 += A0[r7 + mm] * B0[c7 + mm];
+          s1 += A1[r7 + mm] * B1[c7 + mm];
         }
+        v -= s0;
+        v -= s1;
       }
-      // L_ik = A_ik W^T : x(r,c) = sum_m A(r,m) W(c,m)
+      if (q < q1) {
+        const double *A0 = Lb + (size_t)tr_a[q] * 49, *B0 = Lb + (size_t)tr_b[q] * 49;
+        double s0 = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) s0 += A0[r7 + mm] * B0[c7 + mm];
+        v -= s0;
+      }
       if (act49) scr[lane] = v;
       wave_lds_fence();
-      if (act49) {
-        double x = 0.0;
+      double x = 0.0;
 #pragma unroll
-        for (int mm = 0; mm < 7; mm++) x += scr[r * 7 + mm] * Di[(size_t)k * 49 + c * 7 + mm];
-        Lb[(size_t)dst * 49 + lane] = x;
-      }
+      for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * Di[(size_t)k * 49 + c7 + mm];
+      if (act49) Lb[(size_t)dst * 49 + lane] = x;
       wave_lds_fence();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __syncthreads();
   }
+  __syncthreads();
 
   if (fail_s) {
     fail_step(7 * m, D.dx_out, D.info, D.flags + kFlagStop, D.delta_thresh);
     return;
   }
+  M3S_TS(2)
 
-  // 2. back-substitution L^T x = y, levels in reverse (x overwrites y)
-  for (int l = D.levels - 1; l >= 0; l--) {
-    for (int t = lev_ptr[l] + wave; t < lev_ptr[l + 1]; t += NW) {
-      const int k = lev_col[t];
-      double rr = (lane < 7) ? y[k * 7 + lane] : 0.0;
-      for (int q = col_ptr[k]; q < col_ptr[k + 1]; q++) {
-        const double *A = Lb + (size_t)col_slot[q] * 49;
-        const int i = col_row[q];
-        if (lane < 7) {
-          double s = 0.0;
-#pragma unroll
-          for (int mm = 0; mm < 7; mm++) s += A[mm * 7 + lane] * y[i * 7 + mm];
-          rr -= s;
-        }
-      }
-      double xk = 0.0;
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) {
-        const double rm = readlane_d(rr, mm);
-        if (lane < 7) xk += Di[(size_t)k * 49 + mm * 7 + lane] * rm;
-      }
-      if (lane < 7) y[k * 7 + lane] = xk;
+  // 2. back-substitution L^T x = y in reverse level order (x overwrites y),
+  // dataflow: column k waits for x_i of every i in struct(k)
+  for (int t = wave; t < m; t += NW) {
+    const int k = lev_col[m - 1 - t];
+    for (int q = col_ptr[k]; q < col_ptr[k + 1]; q++) {
+      wait_flag(&done2[col_row[q]], &fail_s);
     }
-    __syncthreads();
+    double rr = (lane < 7) ? y[k * 7 + lane] : 0.0;
+    for (int q = col_ptr[k]; q < col_ptr[k + 1]; q++) {
+      const double *A = Lb + (size_t)col_slot[q] * 49;
+      const int i = col_row[q];
+      if (lane < 7) {
+        double s = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) s += A[mm * 7 + lane] * y[i * 7 + mm];
+        rr -= s;
+      }
+    }
+    double xk = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) {
+      const double rm = readlane_d(rr, mm);
+      if (lane < 7) xk += Di[(size_t)k * 49 + mm * 7 + lane] * rm;
+    }
+    if (lane < 7) y[k * 7 + lane] = xk;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&done2[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  __syncthreads();
 
+  M3S_TS(3)
   // 3. dx = -x in the original variable order, retraction, ||dx||
   float part = 0.0f;
   for (int idx = tid; idx < m * 7; idx += 1024) {
@@ -961,6 +1178,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     float s2 = 0.0f;
     for (int w2 = 0; w2 < NW; w2++) s2 += nrm[w2];
     D.info[M3S_INFO_ITERS] += 1;
+    M3S_TS(4)
     if (sqrtf(s2) < D.delta_thresh) {
       D.info[M3S_INFO_CONVERGED] = 1;
       D.flags[kFlagStop] = 1;
@@ -1122,22 +1340,34 @@ int check_args(const m3s_gn_args *a) {
   return M3S_OK;
 }
 
+// pack: 0 gathering kernel, 1 gathering kernel that stores the planes,
+// 2 packed kernel (reads the planes; VEC layout only)
 template <int MODE, bool TRACK>
-int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, hipStream_t st) {
+int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipStream_t st) {
   if (blocks <= 0) return M3S_OK;
-  if (vec)
-    linearize_kernel<MODE, TRACK, true><<<dim3((unsigned)blocks), dim3(kThreads), 0, st>>>(L);
-  else
-    linearize_kernel<MODE, TRACK, false><<<dim3((unsigned)blocks), dim3(kThreads), 0, st>>>(L);
+  const dim3 g((unsigned)blocks), b(kThreads);
+  if (TRACK || pack == 0) {
+    if (vec)
+      linearize_kernel<MODE, TRACK, true, false><<<g, b, 0, st>>>(L);
+    else
+      linearize_kernel<MODE, TRACK, false, false><<<g, b, 0, st>>>(L);
+  } else if (pack == 1) {
+    if (vec)
+      linearize_kernel<MODE, false, true, true><<<g, b, 0, st>>>(L);
+    else
+      linearize_kernel<MODE, false, false, true><<<g, b, 0, st>>>(L);
+  } else {
+    linearize_packed_kernel<MODE><<<g, b, 0, st>>>(L);
+  }
   return launch_ok();
 }
 
 template <bool TRACK>
-int dispatch_linearize(int mode, const LinArgs &L, int64_t blocks, bool vec, hipStream_t st) {
+int dispatch_linearize(int mode, const LinArgs &L, int64_t blocks, bool vec, int pack, hipStream_t st) {
   switch (mode) {
-    case M3S_MODE_POINTS: return launch_linearize<M3S_MODE_POINTS, TRACK>(L, blocks, vec, st);
-    case M3S_MODE_RAYS: return launch_linearize<M3S_MODE_RAYS, TRACK>(L, blocks, vec, st);
-    case M3S_MODE_CALIB: return launch_linearize<M3S_MODE_CALIB, TRACK>(L, blocks, vec, st);
+    case M3S_MODE_POINTS: return launch_linearize<M3S_MODE_POINTS, TRACK>(L, blocks, vec, pack, st);
+    case M3S_MODE_RAYS: return launch_linearize<M3S_MODE_RAYS, TRACK>(L, blocks, vec, pack, st);
+    case M3S_MODE_CALIB: return launch_linearize<M3S_MODE_CALIB, TRACK>(L, blocks, vec, pack, st);
   }
   return M3S_EINVAL;
 }
@@ -1152,6 +1382,53 @@ int read_K(const float *K, ResidualParams &P, hipStream_t st) {
   if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
   P.fx = k[0], P.fy = k[4], P.cx = k[2], P.cy = k[5];
   return M3S_OK;
+}
+
+// Host registry of the per-call plan (keyed by workspace): the stepwise API
+// calls prepare and solve separately.
+struct PlanMeta {
+  bool sparse = false;
+  bool lds = false;
+  size_t lds_bytes = 0;
+  int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0;
+  PlanImage img;  // offsets (data vector cleared after upload)
+  // linearize state of this solve call: edge ranks, the task table of the
+  // edge range last linearized (host copy stays alive for the async upload)
+  // and whether that range's planes are stored
+  std::vector<int32_t> rj;
+  int64_t range_b = -1, range_e = -1, n_blocks = 0;
+  bool planes_ok = false;
+  std::vector<int32_t> tasks;
+};
+std::mutex g_reg_mu;
+std::unordered_map<const void *, PlanMeta> g_reg;
+
+#ifndef M3S_PACK
+#define M3S_PACK 1  // store target-side planes on the first iteration, read them after
+#endif
+#ifndef M3S_TASKS
+#define M3S_TASKS 1  // XCD-grouped task table
+#endif
+// Task table: the E_loc x chunks (edge, chunk) tasks sorted by (chunk, KF j),
+// cut into 8 contiguous runs, run x dealt to blocks x, x+8, x+16, ... so the
+// edges that stream the same Xj chunk run back to back on one XCD (blocks b
+// and b+8 share an XCD under round-robin placement; speed only).
+void build_tasks(const std::vector<int32_t> &rj, int64_t eb, int64_t E_loc, int64_t chunks,
+                 std::vector<int32_t> &out) {
+  const int64_t T = E_loc * chunks;
+  std::vector<int64_t> order(T);
+  for (int64_t t = 0; t < T; t++) order[t] = t;
+  auto key = [&](int64_t t) {
+    const int64_t e = t / chunks, c = t - e * chunks;
+    return std::make_tuple(c, rj[eb + e], e);
+  };
+  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return key(x) < key(y); });
+  const int64_t per = (T + 7) / 8;
+  out.assign(8 * per, -1);
+  for (int64_t t = 0; t < T; t++) {
+    const int64_t x = t / per, pos = t - x * per;
+    out[8 * pos + x] = (int32_t)order[t];
+  }
 }
 
 int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb, int64_t ee,
@@ -1173,6 +1450,8 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.rank_j = at<int32_t>(ws, Ly.rank_j);
   L.stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
   L.partials = at<float>(ws, Ly.partials);
+  L.planes = at<float>(ws, Ly.planes);
+  L.tasks = nullptr;
   L.HW = a->HW;
   L.edge_begin = eb;
   L.chunks = chunks_for(a->HW, E_loc);
@@ -1180,27 +1459,48 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.P = P;
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xs, 16) && vec_ok(a->Cs, 16) && vec_ok(a->Q, 16) &&
                    vec_ok(a->idx_ii2jj, 16) && vec_ok(a->valid_match, 4);
-  int rc = dispatch_linearize<false>(a->mode, L, E_loc * L.chunks, vec, st);
+  const char *no_pack = std::getenv("M3S_NO_PACK"), *no_tasks = std::getenv("M3S_NO_TASKS");
+  const bool can_pack = M3S_PACK && vec && !(no_pack && no_pack[0] == '1') &&
+                        (a->mode != M3S_MODE_CALIB || (a->width < 65536 && a->height < 32768));
+  int64_t blocks = E_loc * L.chunks;
+  int pack = 0;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(ws);
+    if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
+    PlanMeta &M = it->second;
+    if (M.range_b != eb || M.range_e != ee) {
+      M.range_b = eb, M.range_e = ee, M.planes_ok = false;
+      M.n_blocks = 0;
+      if (M3S_TASKS && !(no_tasks && no_tasks[0] == '1') && (int64_t)M.rj.size() >= ee) {
+        build_tasks(M.rj, eb, E_loc, L.chunks, M.tasks);
+        if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), M.tasks.data(), sizeof(int32_t) * M.tasks.size(),
+                           hipMemcpyHostToDevice, st) != hipSuccess)
+          return M3S_ELAUNCH;
+        M.n_blocks = (int64_t)M.tasks.size();
+      }
+    }
+    if (M.n_blocks > 0) {
+      L.tasks = at<int32_t>(ws, Ly.tasks);
+      blocks = M.n_blocks;
+    }
+    if (can_pack) {
+      pack = M.planes_ok ? 2 : 1;
+      M.planes_ok = true;
+    }
+  }
+  int rc = dispatch_linearize<false>(a->mode, L, blocks, vec, pack, st);
   if (rc || !edge_sums) return rc;  // NULL edge_sums: partials only (kernel timing)
   edge_reduce_kernel<<<dim3((unsigned)E_loc), dim3(64), 0, st>>>(L.partials, L.chunks, edge_sums, L.stop);
   return launch_ok();
 }
 
-// Host registry of the per-call plan (keyed by workspace): the stepwise API
-// calls prepare and solve separately.
-struct PlanMeta {
-  bool sparse = false;
-  bool lds = false;
-  size_t lds_bytes = 0;
-  int m = 0, S = 0, levels = 0, plan_len = 0;
-  PlanImage img;  // offsets (data vector cleared after upload)
-};
-std::mutex g_reg_mu;
-std::unordered_map<const void *, PlanMeta> g_reg;
-
 constexpr size_t kMaxLdsBytes = 150 * 1024;
 
-int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st) {
+// edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
+// `chunks` chunks per edge (single-GPU call: no separate reduce launch).
+int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *partials, int64_t chunks,
+                  hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
   int32_t *flags = at<int32_t>(ws, Ly.flags);
@@ -1219,19 +1519,22 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st)
   if (meta.sparse) {
     double *fin = at<double>(ws, Ly.fin);
     if (a->E > 0) {
-      finalize_edges_kernel<<<dim3((unsigned)a->E), dim3(64), 0, st>>>(edge_sums, at<int32_t>(ws, Ly.rank_i),
-                                                                      a->Twc, fin, stop);
+      finalize_edges_kernel<<<dim3((unsigned)a->E), dim3(64), 0, st>>>(
+          edge_sums, edge_sums ? nullptr : partials, chunks, at<int32_t>(ws, Ly.rank_i), a->Twc, fin, stop);
       if ((rc = launch_ok())) return rc;
     }
     const PlanImage &I = meta.img;
     SparseDev D;
     D.plan = at<int32_t>(ws, Ly.plan);
     D.plan_len = meta.plan_len;
-    const int64_t offs[19] = {I.off_perm, I.off_col_ptr, I.off_col_row, I.off_col_slot, I.off_lev_ptr,
-                              I.off_lev_col, I.off_dtr_ptr, I.off_dtr_slot, I.off_dtr_p, I.off_task_lev_ptr,
-                              I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a, I.off_tr_b,
-                              I.off_asm_ptr, I.off_asm_edge, I.off_g_ptr, I.off_g_edge};
-    for (int q = 0; q < 19; q++) D.off[q] = (int)offs[q];
+    const int64_t offs[kPlanSections] = {
+        I.off_perm,     I.off_col_ptr,      I.off_col_row,  I.off_col_slot, I.off_lev_ptr,
+        I.off_lev_col,  I.off_dtr_ptr,      I.off_dtr_slot, I.off_dtr_p,    I.off_task_lev_ptr,
+        I.off_task_dst, I.off_task_col,     I.off_task_tr_ptr, I.off_tr_a,  I.off_tr_b,
+        I.off_asm_ptr,  I.off_asm_edge,     I.off_g_ptr,    I.off_g_edge,   I.off_ctask_ptr,
+        I.off_items};
+    for (int q = 0; q < kPlanSections; q++) D.off[q] = (int)offs[q];
+    D.n_items = meta.n_items;
     D.m = meta.m;
     D.S = meta.S;
     D.levels = meta.levels;
@@ -1251,6 +1554,12 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, hipStream_t st)
     return launch_ok();
   }
   // dense fallback: RHS-augmented system, register or tiled LLT
+  if (!edge_sums && a->E > 0) {
+    double *es = at<double>(ws, Ly.edge_sums);
+    edge_reduce_kernel<<<dim3((unsigned)a->E), dim3(64), 0, st>>>(partials, chunks, es, stop);
+    if ((rc = launch_ok())) return rc;
+    edge_sums = es;
+  }
   double *A = at<double>(ws, Ly.A);
   assemble_kernel<<<dim3((unsigned)a->N), dim3(256), 0, st>>>(
       edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, ld, A, stop);
@@ -1330,10 +1639,12 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       meta.S = P.S;
       meta.levels = P.levels;
       meta.plan_len = (int)img.data.size();
+      meta.n_items = (int)P.items.size();
+      const size_t flags_bytes = sizeof(int32_t) * (size_t)(P.S + P.m);
       const size_t lds_all = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) +
-                             sizeof(int32_t) * img.data.size();
+                             sizeof(int32_t) * ((img.data.size() + 1) & ~size_t(1)) + flags_bytes;
       meta.lds = lds_all <= kMaxLdsBytes;
-      meta.lds_bytes = meta.lds ? lds_all : sizeof(double) * (size_t)P.m * 7;
+      meta.lds_bytes = meta.lds ? lds_all : sizeof(double) * (size_t)P.m * 7 + flags_bytes;
     }
   }
   if (E > 0) {
@@ -1351,6 +1662,18 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
     return M3S_ELAUNCH;
   img.data.clear();
   meta.img = img;
+  meta.rj = std::move(rj);
+  // task table of the full edge range (the single-GPU call and world size 1);
+  // a sharded rank's first m3s_gn_linearize builds its own
+  if (M3S_TASKS && E > 0 && !bad) {
+    const int64_t chunks = chunks_for(a->HW, E);
+    build_tasks(meta.rj, 0, E, chunks, meta.tasks);
+    if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), meta.tasks.data(), sizeof(int32_t) * meta.tasks.size(),
+                       hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return M3S_ELAUNCH;
+    meta.range_b = 0, meta.range_e = E, meta.n_blocks = (int64_t)meta.tasks.size();
+  }
   if (meta.sparse && meta.lds_bytes > 64 * 1024) {
     static std::once_flag once;
     std::call_once(once, [] {
@@ -1375,10 +1698,11 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   if (mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, st))) return rc;
   if ((rc = gn_prepare_impl(a, st))) return rc;
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
-  double *es = at<double>(a->workspace, Ly.edge_sums);
+  const float *partials = at<float>(a->workspace, Ly.partials);
+  const int64_t chunks = chunks_for(a->HW, a->E);
   for (int it = 0; it < a->max_iter; it++) {
-    if ((rc = gn_linearize_impl(a, P, 0, a->E, es, st))) return rc;
-    if ((rc = gn_solve_impl(a, es, st))) return rc;
+    if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st))) return rc;
+    if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st))) return rc;
   }
   return M3S_OK;
 }
@@ -1520,7 +1844,7 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xf, 16) && vec_ok(a->Xk, 16) && vec_ok(a->Qk, 16) &&
                    vec_ok(a->valid, 4);
   for (int it = 0; it < a->max_iters; it++) {
-    if ((rc = dispatch_linearize<true>(mode, L, L.chunks, vec, st))) return rc;
+    if ((rc = dispatch_linearize<true>(mode, L, L.chunks, vec, 0, st))) return rc;
     track_solve_kernel<<<1, 64, 0, st>>>(partials, L.chunks, ts, a->info, a->rel_error, a->delta_norm,
                                          a->T_WCf_out, a->T_CkCf_out);
     if ((rc = launch_ok())) return rc;
@@ -1567,7 +1891,8 @@ int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
   if (rc) return rc;
   if (!edge_sums) return M3S_EINVAL;
   if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
-  return gn_solve_impl(a, edge_sums, S(stream));
+  if (!edge_sums) return M3S_EINVAL;
+  return gn_solve_impl(a, edge_sums, nullptr, 0, S(stream));
 }
 
 size_t m3s_track_workspace_size(int64_t HW) {
@@ -1587,17 +1912,27 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
   build_sparse_plan(N, a, b, P);
   PlanImage I;
   flatten_plan(P, I);
-  const int64_t offs[19] = {I.off_perm, I.off_col_ptr, I.off_col_row, I.off_col_slot, I.off_lev_ptr,
-                            I.off_lev_col, I.off_dtr_ptr, I.off_dtr_slot, I.off_dtr_p, I.off_task_lev_ptr,
-                            I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a, I.off_tr_b,
-                            I.off_asm_ptr, I.off_asm_edge, I.off_g_ptr, I.off_g_edge};
+  const int64_t offs[kPlanSections] = {
+      I.off_perm,     I.off_col_ptr,  I.off_col_row,     I.off_col_slot, I.off_lev_ptr,
+      I.off_lev_col,  I.off_dtr_ptr,  I.off_dtr_slot,    I.off_dtr_p,    I.off_task_lev_ptr,
+      I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a,     I.off_tr_b,
+      I.off_asm_ptr,  I.off_asm_edge, I.off_g_ptr,       I.off_g_edge,   I.off_ctask_ptr,
+      I.off_items};
   if (meta) {
     meta[0] = P.m, meta[1] = P.S, meta[2] = P.levels;
-    for (int k = 0; k < 19; k++) meta[3 + k] = (int32_t)offs[k];
+    for (int k = 0; k < kPlanSections; k++) meta[3 + k] = (int32_t)offs[k];
   }
   const int64_t n = (int64_t)I.data.size();
   if (out && cap >= n) std::copy(I.data.begin(), I.data.end(), out);
   return n;
+}
+
+size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs) {
+  const Layout L = gn_layout(N, HW, E);
+  const size_t o[14] = {L.flags, L.rank_i, L.rank_j, L.first, L.partials, L.edge_sums, L.A,
+                        L.fin,   L.plan,   L.Lblk,   L.Dinv,  L.tasks,    L.planes, L.total};
+  if (offs) std::copy(o, o + 14, offs);
+  return L.total;
 }
 
 }  // extern "C"

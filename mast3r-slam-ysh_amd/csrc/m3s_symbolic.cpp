@@ -125,9 +125,13 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   }
   P.task_lev_ptr.assign(1, 0);
   P.task_tr_ptr.assign(1, 0);
+  P.ctask_ptr.assign(1, 0);
   for (int l = 0; l < P.levels; l++) {
     for (int t = P.lev_ptr[l]; t < P.lev_ptr[l + 1]; t++) {
       const int k = P.lev_col[t];
+      P.ctask_ptr.push_back(P.ctask_ptr.back() + (int32_t)st[k].size());
+      P.items.push_back(-1 - k);
+      for (size_t q = 0; q < st[k].size(); q++) P.items.push_back((int32_t)P.task_dst.size() + (int32_t)q);
       for (int i : st[k]) {
         P.task_dst.push_back(sl(i, k));
         P.task_col.push_back(k);
@@ -192,6 +196,8 @@ void flatten_plan(const SparsePlan &P, PlanImage &img) {
   img.off_asm_edge = put(P.asm_edge);
   img.off_g_ptr = put(P.g_ptr);
   img.off_g_edge = put(P.g_edge);
+  img.off_ctask_ptr = put(P.ctask_ptr);
+  img.off_items = put(P.items);
 }
 
 }  // namespace m3s

@@ -32,6 +32,10 @@ struct SparsePlan {
   std::vector<int32_t> asm_ptr, asm_edge;
   // RHS of new variable v: sum over entries (edge << 1 | sign) of (sign ? +g_j : -g_j)
   std::vector<int32_t> g_ptr, g_edge;
+  // off-diagonal tasks of the column at level-order position t: [ctask_ptr[t], ctask_ptr[t+1])
+  std::vector<int32_t> ctask_ptr;
+  // dataflow work items in level order: -1-k = DIAG(k), t >= 0 = off-diagonal task t
+  std::vector<int32_t> items;
 };
 
 // ranks of (ii, jj) in sorted-unique(cat(ii, jj)); returns the unique count
@@ -47,8 +51,10 @@ struct PlanImage {
   std::vector<int32_t> data;
   int64_t off_perm, off_col_ptr, off_col_row, off_col_slot, off_lev_ptr, off_lev_col, off_dtr_ptr,
       off_dtr_slot, off_dtr_p, off_task_lev_ptr, off_task_dst, off_task_col, off_task_tr_ptr,
-      off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge;
+      off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge, off_ctask_ptr,
+      off_items;
 };
+constexpr int kPlanSections = 21;
 void flatten_plan(const SparsePlan &P, PlanImage &img);
 
 }  // namespace m3s

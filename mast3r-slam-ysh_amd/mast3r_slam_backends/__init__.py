@@ -78,7 +78,7 @@ EXPORTS = (
     "m3s_gn_workspace_size", "m3s_gauss_newton_points", "m3s_gauss_newton_rays",
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
-    "m3s_sparse_plan_debug",
+    "m3s_sparse_plan_debug", "m3s_gn_layout_debug",
 )
 
 
@@ -109,6 +109,8 @@ def _load():
     lib.m3s_version.argtypes = []
     lib.m3s_sparse_plan_debug.restype = ctypes.c_int64
     lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, _VP, ctypes.c_int64, _VP]
+    lib.m3s_gn_layout_debug.restype = ctypes.c_size_t
+    lib.m3s_gn_layout_debug.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP]
     return lib
 
 
@@ -121,7 +123,18 @@ def version() -> str:
 
 PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col", "dtr_ptr",
                  "dtr_slot", "dtr_p", "task_lev_ptr", "task_dst", "task_col", "task_tr_ptr", "tr_a",
-                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge")
+                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items")
+
+
+LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
+                   "plan", "Lblk", "Dinv", "tasks", "planes", "total")
+
+
+def workspace_layout(N, HW, E):
+    """Byte offsets of the GN workspace sections (diagnostics/tests)."""
+    offs = (ctypes.c_size_t * 14)()
+    _lib.m3s_gn_layout_debug(int(N), int(HW), int(E), offs)
+    return dict(zip(LAYOUT_SECTIONS, list(offs)))
 
 
 def sparse_plan(N, ri, rj):
@@ -130,7 +143,7 @@ def sparse_plan(N, ri, rj):
 
     ri = np.ascontiguousarray(ri, dtype=np.int32)
     rj = np.ascontiguousarray(rj, dtype=np.int32)
-    meta = np.zeros(22, np.int32)
+    meta = np.zeros(3 + len(PLAN_SECTIONS), np.int32)
     P = ctypes.c_void_p
     n = _lib.m3s_sparse_plan_debug(int(N), ri.size, P(ri.ctypes.data), P(rj.ctypes.data), None, 0,
                                    P(meta.ctypes.data))
@@ -145,7 +158,8 @@ def sparse_plan(N, ri, rj):
     T = int(plan["task_lev_ptr"][L])
     lens = {"perm": m, "col_ptr": m + 1, "lev_ptr": L + 1, "lev_col": m, "dtr_ptr": m + 1,
             "task_lev_ptr": L + 1, "task_dst": T, "task_col": T, "task_tr_ptr": T + 1,
-            "asm_ptr": S + 1, "g_ptr": m + 1}
+            "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1,
+            "items": m + T}
     for name, ln in lens.items():
         plan[name] = plan[name][:ln]
     nnz = int(plan["col_ptr"][m])

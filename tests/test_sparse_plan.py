@@ -1,9 +1,10 @@
 """CPU check of the host symbolic plan of the block-sparse LLT (the part of the
 solver that replaces Eigen's SimplicialLLT analysis, gn_kernels.cu:132-153).
 
-The plan is executed in numpy exactly as sparse_llt_kernel executes it
-(assembly lists -> level-ordered left-looking 7x7 block Cholesky -> forward and
-back substitution) on random SPD edge blocks, and the solution is compared with
+The plan is executed in numpy in the order of sparse_llt_kernel's dataflow
+work items (assembly lists -> DIAG(k) / OFF(i,k) items in list order -> back
+substitution in reverse level order), asserting that every block an item
+reads is already complete on random SPD edge blocks, and the solution is compared with
 a dense fp64 solve of the same assembled system.
 """
 import numpy as np
@@ -46,12 +47,16 @@ def run_plan(p, Hjj, gj):
             ent = p["g_edge"][t]
             y[v] += gj[ent >> 1] * (1 if ent & 1 else -1)
     W = np.zeros((m, 7, 7))
-    for l in range(p["levels"]):
-        for t in range(p["lev_ptr"][l], p["lev_ptr"][l + 1]):
-            k = p["lev_col"][t]
+    # the kernel's dataflow work items in list order; each asserts that the
+    # blocks it reads are complete (the LDS flags the kernel waits on)
+    sdone = np.zeros(S, bool)
+    for item in p["items"]:
+        if item < 0:
+            k = -1 - item
             D = L[k].copy()
             b = y[k].copy()
             for q in range(p["dtr_ptr"][k], p["dtr_ptr"][k + 1]):
+                assert sdone[p["dtr_slot"][q]], "DIAG reads an unfinished block"
                 A = L[p["dtr_slot"][q]]
                 D -= A @ A.T
                 b -= A @ y[p["dtr_p"][q]]
@@ -59,19 +64,27 @@ def run_plan(p, Hjj, gj):
             L[k] = Lk
             W[k] = np.linalg.inv(Lk)
             y[k] = W[k] @ b
-        for t in range(p["task_lev_ptr"][l], p["task_lev_ptr"][l + 1]):
-            dst, k = p["task_dst"][t], p["task_col"][t]
+            sdone[k] = True
+        else:
+            dst, k = p["task_dst"][item], p["task_col"][item]
+            assert sdone[k], "OFF before its DIAG"
             A = L[dst].copy()
-            for q in range(p["task_tr_ptr"][t], p["task_tr_ptr"][t + 1]):
+            for q in range(p["task_tr_ptr"][item], p["task_tr_ptr"][item + 1]):
+                assert sdone[p["tr_a"][q]] and sdone[p["tr_b"][q]], "OFF reads an unfinished block"
                 A -= L[p["tr_a"][q]] @ L[p["tr_b"][q]].T
             L[dst] = A @ W[k].T
-    for l in range(p["levels"] - 1, -1, -1):
-        for t in range(p["lev_ptr"][l], p["lev_ptr"][l + 1]):
-            k = p["lev_col"][t]
-            r = y[k].copy()
-            for q in range(p["col_ptr"][k], p["col_ptr"][k + 1]):
-                r -= L[p["col_slot"][q]].T @ y[p["col_row"][q]]
-            y[k] = W[k].T @ r
+            sdone[dst] = True
+    assert sdone.all()
+    done = np.zeros(m, bool)
+    done[:] = False
+    for t in range(m - 1, -1, -1):
+        k = p["lev_col"][t]
+        r = y[k].copy()
+        for q in range(p["col_ptr"][k], p["col_ptr"][k + 1]):
+            assert done[p["col_row"][q]]
+            r -= L[p["col_slot"][q]].T @ y[p["col_row"][q]]
+        y[k] = W[k].T @ r
+        done[k] = True
     x = np.zeros((m, 7))
     for vn in range(m):
         x[p["perm"][vn]] = y[vn]

@@ -1,0 +1,30 @@
+"""Phase timing of sparse_llt_kernel (lib built with -DM3S_LLT_TIMING=1):
+assembly / factorisation / back-substitution / retraction, in microseconds."""
+import ctypes, os, sys
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mast3r-slam-ysh_amd")]
+import torch
+import mast3r_slam_backends as be
+from mast3r_slam_amd import synthetic
+dev = torch.device("cuda:0")
+for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
+    H = W = 64
+    g = synthetic.make_graph(N, H, W, seed=1003, device=dev)
+    E, HW = g.n_edges, H * W
+    wst = torch.zeros(int(be._lib.m3s_gn_workspace_size(N, HW, E)), dtype=torch.uint8, device=dev)
+    Twc = g.T_init.data.contiguous()
+    a, keep = be.make_gn_args(be.MODE_RAYS, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match,
+                              g.Q, None, sigma_a=0.003, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5,
+                              max_iter=1, delta_thresh=0.0, workspace=wst)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    lay = be.workspace_layout(N, HW, E)
+    res = []
+    for rep in range(6):
+        assert be._lib.m3s_gauss_newton_rays(ctypes.byref(a), st) == 0
+        torch.cuda.synchronize()
+        ts = wst[lay["flags"] + 64: lay["flags"] + 64 + 40].clone().view(torch.int64).cpu().tolist()
+        res.append([(ts[i + 1] - ts[i]) / 100.0 for i in range(4)])
+    r = res[-1]
+    plan = be.sparse_plan(N, *[torch.searchsorted(torch.unique(torch.cat([g.ii, g.jj])), t).cpu().numpy() for t in (g.ii, g.jj)])
+    print(f"N={N} levels={plan['levels']} S={plan['S']}: assembly {r[0]:.1f} us, factor {r[1]:.1f} us, "
+          f"backsub {r[2]:.1f} us, retract {r[3]:.1f} us")

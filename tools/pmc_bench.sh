@@ -1,18 +1,19 @@
 #!/bin/bash
-# PMC passes on the linearize kernel (one counter group per rocprofv3 run).
+# PMC passes on the linearize kernels (one counter group per rocprofv3 run),
+# bench.py's roofline leg (packed kernel launches) plus its GN steps.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/pmc
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-ARGS="--steps 2 --warmup 1 --no-cpu --no-tracker --lin-reps 5"
+ARGS="--steps 2 --warmup 1 --no-cpu --no-tracker --lin-reps 10"
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" \
-           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "TCP_TCC_READ_REQ_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" ; do
+for grp in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" \
+           "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "linearize|chol|assemble" -T -d $OUT/p$i -o run --output-format csv -- python $R/bench.py $ARGS > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pass $i failed: $grp"; tail -5 $OUT/p$i.err; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "linearize" -T -d $OUT/p$i -o run --output-format csv -- python $R/bench.py $ARGS > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pass $i failed: $grp"; tail -5 $OUT/p$i.err; }
 done
 ls -R $OUT | head -50

@@ -848,6 +848,7 @@ struct SparseDev {
   int plan_len;
   int off[kPlanSections];  // section offsets, order of m3s_symbolic.h
   int m, S, levels, n_items;
+  int64_t *dbg;  // M3S_LLT_TIMING: per-column DIAG completion stamps
   double *L;     // [S][49] (global variant)
   double *Dinv;  // [m][49] (global variant)
   const double *fin;
@@ -1076,6 +1077,9 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
         y[k * 7 + lane] = yo;
       }
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
+#if M3S_LLT_TIMING
+      if (lane == 0) D.dbg[k] = wall_clock64();
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
@@ -1535,6 +1539,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         I.off_items};
     for (int q = 0; q < kPlanSections; q++) D.off[q] = (int)offs[q];
     D.n_items = meta.n_items;
+    D.dbg = at<int64_t>(ws, Ly.A);
     D.m = meta.m;
     D.S = meta.S;
     D.levels = meta.levels;

@@ -10,9 +10,14 @@ is an all-gather of the per-edge normal-equation sums (36 fp64 per edge:
 retracted poses agree bitwise across ranks and nothing is broadcast.
 
 Per GN iteration on each rank:
-    m3s_gn_linearize(slice)  ->  all_gather_into_tensor  ->  m3s_gn_solve
+    linearize(slice)  ->  all_gather_into_tensor  ->  solve
 all enqueued asynchronously; convergence (||dx|| < delta) is a device flag
 that makes the remaining launches no-ops, exactly like the single-GPU call.
+
+The per-rank compute is behind a small ops object (prepare / linearize /
+solve + the per-edge payload width). ``HipOps`` is the product path (the
+m3s_gn stepwise C ABI, include/m3s_gn.h); tests substitute a CPU
+implementation to exercise the slicing and the collective on gloo.
 """
 from __future__ import annotations
 
@@ -21,53 +26,45 @@ import ctypes
 import torch
 import torch.distributed as dist
 
-import mast3r_slam_backends as be
-
 
 def edge_slice(E: int, rank: int, world: int):
-    per = (E + world - 1) // world
+    """Contiguous edge range [b, e) of `rank` and the per-rank stride `per`.
+
+    Rank r owns rows [r*per, r*per + (e-b)) of the gathered [per*world, S]
+    payload, so row k of the gather is edge k for every k < E."""
+    per = (E + world - 1) // world if world > 0 else E
     b = min(rank * per, E)
     e = min(b + per, E)
     return b, e, per
 
 
-class ShardedGN:
-    """Holds the per-rank state of one sharded GN problem.
-
-    Edge data tensors (idx, valid, Q) are this rank's slice [e_end - e_begin,
-    HW(,1)]; ii/jj are the full [E] id lists (every rank needs all of them to
-    assemble the system); Xs/Cs/Twc are replicated.
-    """
+class HipOps:
+    """Stepwise m3s_gn C ABI on this rank's device (m3s_gn_prepare /
+    m3s_gn_linearize / m3s_gn_solve)."""
 
     def __init__(self, mode, Twc, Xs, Cs, ii, jj, idx_loc, valid_loc, Q_loc, E, K=None, *,
                  sigma_a, sigma_b=0.0, C_thresh=0.0, Q_thresh=1.5, height=0, width=0,
-                 pixel_border=0, z_eps=0.0, group=None):
-        self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.E = int(E)
-        self.eb, self.ee, self.per = edge_slice(self.E, self.rank, self.world)
-        n_loc = self.ee - self.eb
-        HW = int(Xs.shape[1])
-        assert idx_loc.shape[0] == n_loc and valid_loc.shape[0] == n_loc and Q_loc.shape[0] == n_loc
+                 pixel_border=0, z_eps=0.0):
+        import mast3r_slam_backends as be
+
+        self.be = be
+        self.stride = be.EDGE_SUM_STRIDE
         for name, t in (("Twc", Twc), ("Xs", Xs), ("Cs", Cs), ("ii", ii), ("jj", jj),
                         ("idx", idx_loc), ("valid", valid_loc), ("Q", Q_loc)):
             be._check(t, name)
         dev = Xs.device
-        N = int(Xs.shape[0])
+        self.device = dev
+        N, HW = int(Xs.shape[0]), int(Xs.shape[1])
         self.dx = torch.zeros(max(N - 1, 0), 7, dtype=torch.float32, device=dev)
         self.info = torch.zeros(8, dtype=torch.int32, device=dev)
-        self.ws = be._workspace(be._lib.m3s_gn_workspace_size(N, HW, self.E), dev)
-        self.es_loc = torch.zeros(self.per, be.EDGE_SUM_STRIDE, dtype=torch.float64, device=dev)
-        self.es_all = torch.zeros(self.per * self.world, be.EDGE_SUM_STRIDE, dtype=torch.float64,
-                                  device=dev)
+        self.ws = be._workspace(be._lib.m3s_gn_workspace_size(N, HW, int(E)), dev)
         a = be.GnArgs()
         P = be._p
         a.Twc, a.Xs, a.Cs, a.ii, a.jj = P(Twc), P(Xs), P(Cs), P(ii), P(jj)
         # edge-slice base pointers: the C side addresses edge data relative to
         # edge_begin (include/m3s_gn.h, stepwise API)
         a.idx_ii2jj, a.valid_match, a.Q, a.K = P(idx_loc), P(valid_loc), P(Q_loc), P(K)
-        a.N, a.HW, a.E, a.mode = N, HW, self.E, mode
+        a.N, a.HW, a.E, a.mode = N, HW, int(E), mode
         a.sigma_a, a.sigma_b, a.C_thresh, a.Q_thresh = sigma_a, sigma_b, C_thresh, Q_thresh
         a.height, a.width, a.pixel_border, a.z_eps = height, width, pixel_border, z_eps
         a.max_iter, a.delta_thresh = 0, 0.0
@@ -78,31 +75,85 @@ class ShardedGN:
                          Q=Q_loc, K=K)
         self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
+    def prepare(self, delta_thresh: float):
+        self.args.delta_thresh = float(delta_thresh)
+        self.be._raise(self.be._lib.m3s_gn_prepare(ctypes.byref(self.args), self.stream),
+                       "m3s_gn_prepare")
+
+    def linearize(self, eb: int, ee: int, es_loc):
+        ptr = self.be._p(es_loc) if es_loc is not None else None
+        self.be._raise(self.be._lib.m3s_gn_linearize(ctypes.byref(self.args), eb, ee, ptr,
+                                                     self.stream), "m3s_gn_linearize")
+
+    def solve(self, es):
+        self.be._raise(self.be._lib.m3s_gn_solve(ctypes.byref(self.args), self.be._p(es),
+                                                 self.stream), "m3s_gn_solve")
+
+
+class ShardedGN:
+    """Per-rank state of one sharded GN problem.
+
+    Edge data tensors (idx, valid, Q) are this rank's slice [e_end - e_begin,
+    HW(,1)]; ii/jj are the full [E] id lists (every rank needs all of them to
+    assemble the system); Xs/Cs/Twc are replicated. ``ops`` defaults to
+    :class:`HipOps` over the same arguments.
+    """
+
+    def __init__(self, mode, Twc, Xs, Cs, ii, jj, idx_loc, valid_loc, Q_loc, E, K=None, *,
+                 sigma_a, sigma_b=0.0, C_thresh=0.0, Q_thresh=1.5, height=0, width=0,
+                 pixel_border=0, z_eps=0.0, group=None, ops=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.E = int(E)
+        self.eb, self.ee, self.per = edge_slice(self.E, self.rank, self.world)
+        n_loc = self.ee - self.eb
+        if not (idx_loc.shape[0] == n_loc and valid_loc.shape[0] == n_loc
+                and Q_loc.shape[0] == n_loc):
+            raise ValueError(f"rank {self.rank}: edge data must hold this rank's {n_loc} edges "
+                             f"[{self.eb}, {self.ee})")
+        if ops is None:
+            ops = HipOps(mode, Twc, Xs, Cs, ii, jj, idx_loc, valid_loc, Q_loc, self.E, K,
+                         sigma_a=sigma_a, sigma_b=sigma_b, C_thresh=C_thresh, Q_thresh=Q_thresh,
+                         height=height, width=width, pixel_border=pixel_border, z_eps=z_eps)
+        self.ops = ops
+        dev = getattr(ops, "device", Xs.device)
+        self.es_loc = torch.zeros(self.per, ops.stride, dtype=torch.float64, device=dev)
+        self.es_all = torch.zeros(self.per * self.world, ops.stride, dtype=torch.float64, device=dev)
+
+    # convenience views of the HIP ops state (bench / tests)
+    @property
+    def args(self):
+        return self.ops.args
+
+    @property
+    def keep(self):
+        return self.ops.keep
+
+    @property
+    def dx(self):
+        return self.ops.dx
+
+    @property
+    def info(self):
+        return self.ops.info
+
     def solve(self, max_iter: int, delta_thresh: float):
         """gauss_newton_{mode} semantics over the sharded edges; Twc in place."""
-        a = self.args
-        a.delta_thresh = float(delta_thresh)
-        be._raise(be._lib.m3s_gn_prepare(ctypes.byref(a), self.stream), "m3s_gn_prepare")
+        self.ops.prepare(delta_thresh)
         n_loc = self.ee - self.eb
         for _ in range(int(max_iter)):
             if n_loc > 0:
-                be._raise(
-                    be._lib.m3s_gn_linearize(ctypes.byref(a), self.eb, self.ee,
-                                             be._p(self.es_loc), self.stream),
-                    "m3s_gn_linearize",
-                )
+                self.ops.linearize(self.eb, self.ee, self.es_loc)
             if self.world > 1:
                 dist.all_gather_into_tensor(self.es_all, self.es_loc, group=self.group)
                 es = self.es_all
             else:
                 es = self.es_loc
-            be._raise(be._lib.m3s_gn_solve(ctypes.byref(a), be._p(es), self.stream), "m3s_gn_solve")
-        return [self.dx]
+            self.ops.solve(es)
+        return [self.ops.dx]
 
     def linearize_only(self):
         """Timing hook: just the linearize kernel on this rank's slice."""
         if self.ee > self.eb:
-            be._raise(
-                be._lib.m3s_gn_linearize(ctypes.byref(self.args), self.eb, self.ee, None, self.stream),
-                "m3s_gn_linearize",
-            )
+            self.ops.linearize(self.eb, self.ee, None)

@@ -26,5 +26,15 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
         res.append([(ts[i + 1] - ts[i]) / 100.0 for i in range(4)])
     r = res[-1]
     plan = be.sparse_plan(N, *[torch.searchsorted(torch.unique(torch.cat([g.ii, g.jj])), t).cpu().numpy() for t in (g.ii, g.jj)])
+    import numpy as np
+    m = N - 1
+    stamps = wst[lay["A"]: lay["A"] + 8 * m].clone().view(torch.int64).cpu().numpy()
+    ts0 = wst[lay["flags"] + 64: lay["flags"] + 72].clone().view(torch.int64).cpu().item()
+    lev = np.zeros(m, int)
+    lp, lc = plan["lev_ptr"], plan["lev_col"]
+    for l in range(plan["levels"]):
+        lev[lc[lp[l]:lp[l + 1]]] = l
+    fin_by_level = [max((stamps[k] - ts0) / 100.0 for k in lc[lp[l]:lp[l + 1]]) for l in range(plan["levels"])]
+    print("  DIAG completion (us since kernel start) by level:", " ".join(f"{x:.0f}" for x in fin_by_level))
     print(f"N={N} levels={plan['levels']} S={plan['S']}: assembly {r[0]:.1f} us, factor {r[1]:.1f} us, "
           f"backsub {r[2]:.1f} us, retract {r[3]:.1f} us")

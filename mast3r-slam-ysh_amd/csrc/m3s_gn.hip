@@ -1400,6 +1400,8 @@ struct PlanMeta {
   // edge range last linearized (host copy stays alive for the async upload)
   // and whether that range's planes are stored
   std::vector<int32_t> rj;
+  bool has_K = false;
+  float K4[4] = {0.f, 0.f, 0.f, 0.f};  // fx, fy, cx, cy (calib; read once per call)
   int64_t range_b = -1, range_e = -1, n_blocks = 0;
   bool planes_ok = false;
   std::vector<int32_t> tasks;
@@ -1612,18 +1614,20 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
 int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
+  float hK[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // calib intrinsics, read with ii/jj
+  if (a->mode == M3S_MODE_CALIB &&
+      hipMemcpyAsync(hK, a->K, sizeof hK, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return M3S_ELAUNCH;
   if (hipMemsetAsync(at<int32_t>(ws, Ly.flags), 0, 64 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
   if (hipMemsetAsync(a->info, 0, 8 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
   if (a->N > 1 && a->dx_out && hipMemsetAsync(a->dx_out, 0, sizeof(float) * 7 * (a->N - 1), st) != hipSuccess)
     return M3S_ELAUNCH;
   const int64_t E = a->E;
   std::vector<int64_t> hii(E), hjj(E);
-  if (E > 0) {
-    if (hipMemcpyAsync(hii.data(), a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(hjj.data(), a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return M3S_ELAUNCH;
-  }
+  if (E > 0 && (hipMemcpyAsync(hii.data(), a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(hjj.data(), a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess))
+    return M3S_ELAUNCH;
+  if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
   std::vector<int32_t> ri, rj;
   const int nu = host_remap(hii.data(), hjj.data(), E, ri, rj);
   int32_t hinfo[8] = {0, 0, 0, 0, nu, 0, 0, 0};
@@ -1668,6 +1672,10 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   img.data.clear();
   meta.img = img;
   meta.rj = std::move(rj);
+  if (a->mode == M3S_MODE_CALIB) {  // K row-major: fx = K[0][0], fy = K[1][1], cx = K[0][2], cy = K[1][2]
+    meta.has_K = true;
+    meta.K4[0] = hK[0], meta.K4[1] = hK[4], meta.K4[2] = hK[2], meta.K4[3] = hK[5];
+  }
   // task table of the full edge range (the single-GPU call and world size 1);
   // a sharded rank's first m3s_gn_linearize builds its own
   if (M3S_TASKS && E > 0 && !bad) {
@@ -1700,8 +1708,12 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
   hipStream_t st = S(stream);
   ResidualParams P = make_params(a);
-  if (mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, st))) return rc;
   if ((rc = gn_prepare_impl(a, st))) return rc;
+  if (mode == M3S_MODE_CALIB) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    const PlanMeta &M = g_reg.at(a->workspace);
+    P.fx = M.K4[0], P.fy = M.K4[1], P.cx = M.K4[2], P.cy = M.K4[3];
+  }
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   const float *partials = at<float>(a->workspace, Ly.partials);
   const int64_t chunks = chunks_for(a->HW, a->E);
@@ -1887,7 +1899,12 @@ int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end,
   if (rc) return rc;
   if (edge_begin < 0 || edge_end > a->E || edge_begin > edge_end) return M3S_EINVAL;
   ResidualParams P = make_params(a);
-  if (a->mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, S(stream)))) return rc;
+  if (a->mode == M3S_MODE_CALIB) {  // intrinsics read once by m3s_gn_prepare (no sync here)
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(a->workspace);
+    if (it == g_reg.end() || !it->second.has_K) return M3S_EINVAL;
+    P.fx = it->second.K4[0], P.fy = it->second.K4[1], P.cx = it->second.K4[2], P.cy = it->second.K4[3];
+  }
   return gn_linearize_impl(a, P, edge_begin, edge_end, edge_sums, S(stream));
 }
 
@@ -1896,7 +1913,6 @@ int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
   if (rc) return rc;
   if (!edge_sums) return M3S_EINVAL;
   if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
-  if (!edge_sums) return M3S_EINVAL;
   return gn_solve_impl(a, edge_sums, nullptr, 0, S(stream));
 }
 

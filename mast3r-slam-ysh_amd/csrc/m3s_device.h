@@ -71,6 +71,32 @@ __device__ __forceinline__ void act(const Sim3f &T, const float *X, float *Y) {
   Y[2] = Y[2] * T.s + T.t[2];
 }
 
+// Y = s R(q) X + t as a 3x4 matrix: 9 FMAs per point instead of the
+// quaternion form's ~24 operations (same map; rounding differs at the ulp level).
+struct Sim3Mat {
+  float m[9], t[3];
+};
+__device__ __forceinline__ Sim3Mat sim3_matrix(const Sim3f &T) {
+  const float x = T.q[0], y = T.q[1], z = T.q[2], w = T.q[3], s = T.s;
+  Sim3Mat M;
+  M.m[0] = s * (1.0f - 2.0f * (y * y + z * z));
+  M.m[1] = s * (2.0f * (x * y - z * w));
+  M.m[2] = s * (2.0f * (x * z + y * w));
+  M.m[3] = s * (2.0f * (x * y + z * w));
+  M.m[4] = s * (1.0f - 2.0f * (x * x + z * z));
+  M.m[5] = s * (2.0f * (y * z - x * w));
+  M.m[6] = s * (2.0f * (x * z - y * w));
+  M.m[7] = s * (2.0f * (y * z + x * w));
+  M.m[8] = s * (1.0f - 2.0f * (x * x + y * y));
+  M.t[0] = T.t[0], M.t[1] = T.t[1], M.t[2] = T.t[2];
+  return M;
+}
+__device__ __forceinline__ void act(const Sim3Mat &M, const float *X, float *Y) {
+  Y[0] = __builtin_fmaf(M.m[0], X[0], __builtin_fmaf(M.m[1], X[1], __builtin_fmaf(M.m[2], X[2], M.t[0])));
+  Y[1] = __builtin_fmaf(M.m[3], X[0], __builtin_fmaf(M.m[4], X[1], __builtin_fmaf(M.m[5], X[2], M.t[1])));
+  Y[2] = __builtin_fmaf(M.m[6], X[0], __builtin_fmaf(M.m[7], X[1], __builtin_fmaf(M.m[8], X[2], M.t[2])));
+}
+
 __device__ __forceinline__ Sim3f inverse(const Sim3f &T) {
   Sim3f R;
   R.q[0] = -T.q[0], R.q[1] = -T.q[1], R.q[2] = -T.q[2], R.q[3] = T.q[3];
@@ -208,7 +234,18 @@ __device__ inline void adjT_inv_matrix(const float *Tp, double M[7][7]) {
 // the difference is below the fp32 summation noise (DESIGN.md tolerances).
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-__device__ __forceinline__ float flog(float x) { return __logf(x); }
+#ifndef M3S_FAST_LOG
+#define M3S_FAST_LOG 1
+#endif
+// natural log: v_log_f32 (log2, ~1 ulp on normal inputs) * ln 2; callers only
+// use it on z > z_eps (>= FLT_MIN) or select the result away
+__device__ __forceinline__ float flog(float x) {
+#if M3S_FAST_LOG
+  return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
+#else
+  return __logf(x);
+#endif
+}
 
 // branch-free: both sides are always computed, then selected
 __device__ __forceinline__ float huber_w(float r, float k) {

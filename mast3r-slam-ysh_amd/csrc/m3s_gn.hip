@@ -302,6 +302,14 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
     Cs_i = A.Cs + (size_t)ri * HW;
     Cs_j = A.Cs + (size_t)rj * HW;
   }
+#ifndef M3S_MAT_ACT
+#define M3S_MAT_ACT 1
+#endif
+#if M3S_MAT_ACT
+  const Sim3Mat Tm = sim3_matrix(Tij);
+#else
+  const Sim3f &Tm = Tij;
+#endif
   // edge data (idx/valid/Q) is addressed relative to the launch's edge slice
   const size_t eoff = TRACK ? 0 : (size_t)e_loc * HW;
   const int64_t *__restrict__ idx = TRACK ? nullptr : A.idx + eoff;
@@ -342,7 +350,7 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
         in[s] = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p0 + s, ((vb >> (8 * s)) & 0xffu) != 0, ids[s],
                                           qs[s], cjs[s]);
         float Y[3];
-        act(Tij, Xj[s], Y);
+        act(Tm, Xj[s], Y);
         pixel_contrib<MODE>(acc, A.P, in[s], Y);
       }
       if (WPACK) {
@@ -361,7 +369,7 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
       const float cj = TRACK ? 0.0f : Cs_j[p];
       const PixIn<MODE> in = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p, vm, id, Qe[p], cj);
       float Y[3];
-      act(Tij, Xj, Y);
+      act(Tm, Xj, Y);
       pixel_contrib<MODE>(acc, A.P, in, Y);
       if (WPACK) {
 #pragma unroll
@@ -386,6 +394,11 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
   const int64_t HW = A.HW;
   const int ri = A.rank_i[e], rj = A.rank_j[e];
   const Sim3f Tij = relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj));
+#if M3S_MAT_ACT
+  const Sim3Mat Tm = sim3_matrix(Tij);
+#else
+  const Sim3f &Tm = Tij;
+#endif
   const float *__restrict__ Xs_j = A.Xs + (size_t)rj * HW * 3;
   constexpr int NPL = PixIn<MODE>::kPlanes;
   const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
@@ -428,7 +441,7 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
 #pragma unroll
       for (int k = 0; k < NPL; k++) in.v[k] = pv[k][s];
       float Y[3];
-      act(Tij, Xj[s], Y);
+      act(Tm, Xj[s], Y);
       pixel_contrib<MODE>(acc, A.P, in, Y);
       // one pixel at a time: keeps the packed kernel at ~90 VGPRs (5 waves/SIMD)
       if ((s + 1) % M3S_PK_GROUP == 0) __builtin_amdgcn_sched_barrier(0);

@@ -150,7 +150,7 @@ const char *m3s_version(void);
 
 /* Diagnostic: the host symbolic plan of the block-sparse LLT for N poses and
  * edge ranks (ri, rj) (pose rank 0 fixed). Writes the flattened int32 plan to
- * out (if cap suffices) and meta[0..23] = {m, S, levels, 21 section offsets in
+ * out (if cap suffices) and meta[0..25] = {m, S, levels, 23 section offsets in
  * the order of m3s_symbolic.h}. Returns the plan length in int32 words. */
 int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj,
                               int32_t *out, int64_t cap, int32_t *meta);

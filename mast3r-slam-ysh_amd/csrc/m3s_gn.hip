@@ -888,7 +888,9 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   double x = __builtin_amdgcn_rsq(d);
   const double hd = 0.5 * d;
   x = x * (1.5 - hd * x * x);
+#if !M3S_RSQ_ONE_NR
   x = x * (1.5 - hd * x * x);
+#endif
   return x;
 }
 
@@ -919,41 +921,157 @@ __device__ __forceinline__ void wave_lds_fence() {
 // Layouts inside a wave: "entry" lanes 0..48 hold (r, c) = (lane / 7, lane % 7)
 // of a 7x7 block (block GEMMs), "row" lanes 0..6 hold a whole row / column in
 // registers (7x7 Cholesky, inverse, substitution) with v_readlane broadcasts.
-template <bool IN_LDS>
+// Block products of the left-looking updates. Entry layout: lane = 7r + c of
+// a 7x7 block (lanes >= 49 compute discarded values on clamped indices).
+// LDS-resident factors read the operand rows straight from LDS, two updates in
+// flight. Global factors (large graphs) are staged: every lane loads its own
+// entry of up to kStage blocks at once (one memory latency per batch), the
+// wave parks them in its LDS stage area and the products run from LDS.
+constexpr int kStage = 8;                  // updates per staged batch
+constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
+
+// v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
+template <bool STAGE, bool SAME>
+__device__ __forceinline__ double sub_products(double v, const double *Lb, const int32_t *sa,
+                                               const int32_t *sb, int q0, int q1, int r7, int c7,
+                                               int lane49, int lane, double *stg) {
+  if (!STAGE) {
+    int q = q0;
+    for (; q + 1 < q1; q += 2) {
+      const double *A0 = Lb + (size_t)sa[q] * 49, *A1 = Lb + (size_t)sa[q + 1] * 49;
+      const double *B0 = SAME ? A0 : Lb + (size_t)sb[q] * 49, *B1 = SAME ? A1 : Lb + (size_t)sb[q + 1] * 49;
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) {
+        s0 += A0[r7 + mm] * B0[c7 + mm];
+        s1 += A1[r7 + mm] * B1[c7 + mm];
+      }
+      v -= s0;
+      v -= s1;
+    }
+    if (q < q1) {
+      const double *A0 = Lb + (size_t)sa[q] * 49, *B0 = SAME ? A0 : Lb + (size_t)sb[q] * 49;
+      double s0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) s0 += A0[r7 + mm] * B0[c7 + mm];
+      v -= s0;
+    }
+    return v;
+  }
+  double *SA = stg, *SB = SAME ? stg : stg + kStage * 49;
+  for (int q = q0; q < q1; q += kStage) {
+    const int nb = (q1 - q < kStage) ? q1 - q : kStage;
+    double va[kStage], vb[kStage];
+#pragma unroll
+    for (int bq = 0; bq < kStage; bq++) {
+      if (bq < nb) {
+        va[bq] = Lb[(size_t)sa[q + bq] * 49 + lane49];
+        if (!SAME) vb[bq] = Lb[(size_t)sb[q + bq] * 49 + lane49];
+      }
+    }
+    if (lane < 49) {
+#pragma unroll
+      for (int bq = 0; bq < kStage; bq++)
+        if (bq < nb) {
+          SA[bq * 49 + lane] = va[bq];
+          if (!SAME) SB[bq * 49 + lane] = vb[bq];
+        }
+    }
+    wave_lds_fence();
+    for (int bq = 0; bq < nb; bq++) {
+      double s0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) s0 += SA[bq * 49 + r7 + mm] * SB[bq * 49 + c7 + mm];
+      v -= s0;
+    }
+    wave_lds_fence();
+  }
+  return v;
+}
+
+// Rows (lanes 0..6): acc -= sum_q op(A_q) y_{p_q}, op(A) = A (TRANS false:
+// row l7 of A) or A^T (TRANS: column `lane` of A). y lives in LDS.
+template <bool STAGE, bool TRANS>
+__device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const int32_t *slot,
+                                             const int32_t *vidx, int q0, int q1, const double *y,
+                                             int lane7, int lane49, int lane, double *stg) {
+  if (!STAGE) {
+    for (int q = q0; q < q1; q++) {
+      const double *A = Lb + (size_t)slot[q] * 49;
+      const double *yv = y + (size_t)vidx[q] * 7;
+      double t0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) t0 += (TRANS ? A[mm * 7 + lane7] : A[lane7 * 7 + mm]) * yv[mm];
+      acc -= t0;
+    }
+    return acc;
+  }
+  for (int q = q0; q < q1; q += kStage) {
+    const int nb = (q1 - q < kStage) ? q1 - q : kStage;
+    double va[kStage];
+#pragma unroll
+    for (int bq = 0; bq < kStage; bq++)
+      if (bq < nb) va[bq] = Lb[(size_t)slot[q + bq] * 49 + lane49];
+    if (lane < 49) {
+#pragma unroll
+      for (int bq = 0; bq < kStage; bq++)
+        if (bq < nb) stg[bq * 49 + lane] = va[bq];
+    }
+    wave_lds_fence();
+    for (int bq = 0; bq < nb; bq++) {
+      const double *A = stg + bq * 49;
+      const double *yv = y + (size_t)vidx[q + bq] * 7;
+      double t0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) t0 += (TRANS ? A[mm * 7 + lane7] : A[lane7 * 7 + mm]) * yv[mm];
+      acc -= t0;
+    }
+    wave_lds_fence();
+  }
+  return acc;
+}
+
+// One 1024-thread workgroup: assembly -> dataflow block LLT + forward
+// substitution -> dataflow back-substitution -> dx, retraction, ||dx||.
+// STORE: 1 = factor, plan and flags in LDS (small graphs); 2 = factor and
+// flags in LDS, plan in global memory; 0 = factor in global memory, flags and
+// the per-wave stage areas in LDS (large graphs).
+template <int STORE>
 __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   if (D.flags[kFlagStop]) return;
+  constexpr bool IN_LDS = STORE != 0;
+  constexpr bool STAGE = STORE == 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int fail_s;
   __shared__ float nrm[16];
   __shared__ double scratch[16][64];
   const int m = D.m, S = D.S;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  constexpr int NW = 16;
   double *Lb = IN_LDS ? smem : D.L;
   double *Di = IN_LDS ? smem + (size_t)S * 49 : D.Dinv;
   double *y = IN_LDS ? smem + (size_t)(S + m) * 49 : smem;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // index arrays: LDS copy (IN_LDS) or global
+  int32_t *after_y = reinterpret_cast<int32_t *>(y + (size_t)m * 7);
+  // index arrays: LDS copy (STORE 1) or global
   const int32_t *pl = D.plan;
-#if M3S_LLT_DEBUG
-  if (tid == 0) printf("llt start IN_LDS=%d m=%d S=%d plan_len=%d levels=%d\n", (int)IN_LDS, m, S, D.plan_len, D.levels);
-#endif
-  if (IN_LDS) {
-    int32_t *lp = reinterpret_cast<int32_t *>(y + (size_t)m * 7);
-    for (int q = tid; q < D.plan_len; q += 1024) lp[q] = D.plan[q];
-    pl = lp;
+  if (STORE == 1) {
+    for (int q = tid; q < D.plan_len; q += 1024) after_y[q] = D.plan[q];
+    pl = after_y;
   }
   const int32_t *perm = pl + D.off[0], *col_ptr = pl + D.off[1], *col_row = pl + D.off[2],
-                *col_slot = pl + D.off[3], *lev_ptr = pl + D.off[4], *lev_col = pl + D.off[5],
-                *dtr_ptr = pl + D.off[6], *dtr_slot = pl + D.off[7], *dtr_p = pl + D.off[8],
-                *task_lev_ptr = pl + D.off[9], *task_dst = pl + D.off[10], *task_col = pl + D.off[11],
-                *task_tr_ptr = pl + D.off[12], *tr_a = pl + D.off[13], *tr_b = pl + D.off[14],
-                *asm_ptr = pl + D.off[15], *asm_edge = pl + D.off[16], *g_ptr = pl + D.off[17],
-                *g_edge = pl + D.off[18], *items = pl + D.off[20];
-  // completion flags of the dataflow schedule: sdone[slot] (factorisation,
-  // diagonal slot k = DIAG(k)), done2[column] (back-substitution)
-  int32_t *sdone = IN_LDS ? const_cast<int32_t *>(pl) + ((D.plan_len + 1) & ~1)
-                          : reinterpret_cast<int32_t *>(y + (size_t)m * 7);
-  int32_t *done2 = sdone + S;
-  for (int q = tid; q < S + m; q += 1024) sdone[q] = 0;
+                *col_slot = pl + D.off[3], *lev_col = pl + D.off[5], *dtr_ptr = pl + D.off[6],
+                *dtr_slot = pl + D.off[7], *dtr_p = pl + D.off[8], *task_dst = pl + D.off[10],
+                *task_col = pl + D.off[11], *task_tr_ptr = pl + D.off[12], *tr_a = pl + D.off[13],
+                *tr_b = pl + D.off[14], *asm_ptr = pl + D.off[15], *asm_edge = pl + D.off[16],
+                *g_ptr = pl + D.off[17], *g_edge = pl + D.off[18], *wave_ptr = pl + D.off[21],
+                *witems = pl + D.off[22];
+  // completion flags: sdone[slot] (factor block final; diagonal slot k also
+  // means W_k final), ydone[k] (forward value y_k final), done2[k] (x_k final)
+  int32_t *sdone = after_y + (STORE == 1 ? ((D.plan_len + 1) & ~1) : 0);
+  int32_t *ydone = sdone + S;
+  int32_t *done2 = ydone + m;
+  double *stg = reinterpret_cast<double *>(sdone + ((S + 2 * m + 1) & ~1)) + (size_t)wave * kStageDoubles;
+  for (int q = tid; q < S + 2 * m; q += 1024) sdone[q] = 0;
   __syncthreads();  // plan copy complete
   const int r = lane / 7, c = lane % 7;
   const bool act49 = lane < 49;
@@ -968,7 +1086,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #define M3S_TS(i)
 #endif
   double *scr = scratch[wave];
-  constexpr int NW = 16;
 
   // 0. assembly (edge order within each slot: deterministic)
   for (int idx = tid; idx < S * 49; idx += 1024) {
@@ -988,61 +1105,51 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     y[idx] = v;
   }
   if (tid == 0) fail_s = 0;
+  if (!IN_LDS) __threadfence_block();
   __syncthreads();
   M3S_TS(1)
 
   // 1. factorisation + forward substitution as a dataflow over work items:
-  // DIAG(k) (diagonal block, W_k = L_kk^-1, forward step of y_k) and OFF(i,k)
-  // (one off-diagonal block). Items are listed column by column in
-  // elimination-tree level order (items[]); wave w runs items w, w+16, ...
-  // Each item waits on LDS completion flags of exactly the blocks it reads
-  // (sdone[slot]) and publishes its own block. Every dependency points to an
-  // earlier item, so the lowest unfinished item can always run: no deadlock,
-  // and no workgroup barriers inside the factorisation.
-  const int n_items = D.n_items;
-  for (int it = wave; it < n_items; it += NW) {
-    const int item = items[it];
-    if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k, y_k
+  // DIAG(k) (diagonal block and W_k = L_kk^-1, then the forward step of y_k)
+  // and OFF(i,k) (one off-diagonal block). The host list-schedules the items
+  // onto the 16 waves (m3s_symbolic.cpp, schedule_items); each item waits on
+  // LDS completion flags of exactly the blocks it reads and publishes its
+  // own. No workgroup barriers inside the factorisation; the schedule's
+  // assignment order guarantees progress.
+#if M3S_LLT_CYC
+  uint64_t cyc_wait = 0, cyc_trip = 0;
+  const uint64_t cyc_start = __builtin_amdgcn_s_memtime();
+#define M3S_WAIT(f)                                   \
+  {                                                   \
+    const uint64_t w0_ = __builtin_amdgcn_s_memtime(); \
+    wait_flag(f, &fail_s);                            \
+    cyc_wait += __builtin_amdgcn_s_memtime() - w0_;   \
+  }
+#else
+#define M3S_WAIT(f) wait_flag(f, &fail_s);
+#endif
+  for (int it = wave_ptr[wave]; it < wave_ptr[wave + 1]; it++) {
+    const int item = witems[it];
+    if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
       const int k = -1 - item;
       const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
-      for (int q = q0; q < q1; q++) wait_flag(&sdone[dtr_slot[q]], &fail_s);
+      for (int q = q0; q < q1; q++) M3S_WAIT(&sdone[dtr_slot[q]]);
+#if M3S_LLT_CYC
+      const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+#endif
       double v = Lb[(size_t)k * 49 + lane49];
-      double bb = y[k * 7 + lane7];
-      int q = q0;
-      for (; q + 1 < q1; q += 2) {  // two updates in flight
-        const double *A0 = Lb + (size_t)dtr_slot[q] * 49, *A1 = Lb + (size_t)dtr_slot[q + 1] * 49;
-        const double *y0 = y + dtr_p[q] * 7, *y1 = y + dtr_p[q + 1] * 7;
-        double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) {
-          s0 += A0[r7 + mm] * A0[c7 + mm];
-          s1 += A1[r7 + mm] * A1[c7 + mm];
-          t0 += A0[l7 + mm] * y0[mm];
-          t1 += A1[l7 + mm] * y1[mm];
-        }
-        v -= s0;
-        v -= s1;
-        bb -= t0;
-        bb -= t1;
-      }
-      if (q < q1) {
-        const double *A0 = Lb + (size_t)dtr_slot[q] * 49;
-        const double *y0 = y + dtr_p[q] * 7;
-        double s0 = 0.0, t0 = 0.0;
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) {
-          s0 += A0[r7 + mm] * A0[c7 + mm];
-          t0 += A0[l7 + mm] * y0[mm];
-        }
-        v -= s0;
-        bb -= t0;
-      }
+      v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+#if M3S_LLT_CYC
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      cyc_trip += __builtin_amdgcn_s_memtime() - t0_;
+#endif
       // entry layout -> row layout through the wave's scratch
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double a[7];
 #pragma unroll
-      for (int qq = 0; qq < 7; qq++) a[qq] = (lane < 7) ? scr[lane * 7 + qq] : 0.0;
+      for (int qq = 0; qq < 7; qq++) a[qq] = scr[l7 + qq];
       wave_lds_fence();
       // Cholesky: lane r holds row r; column j of L broadcast by readlane
       bool bad = false;
@@ -1060,22 +1167,19 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
           if (lane >= cc) a[cc] -= a[j] * lcj;
         }
       }
-      // forward substitution L y_k = bb (uniform values)
-      double yk[7];
+      // strictly-lower entries of L_kk as wave-uniform values
+      double Lr[7][7];
 #pragma unroll
-      for (int rr = 0; rr < 7; rr++) {
-        double acc = readlane_d(bb, rr);
+      for (int rr = 1; rr < 7; rr++)
 #pragma unroll
-        for (int mm = 0; mm < rr; mm++) acc -= readlane_d(a[mm], rr) * yk[mm];
-        yk[rr] = acc * dinv[rr];
-      }
+        for (int mm = 0; mm < rr; mm++) Lr[rr][mm] = readlane_d(a[mm], rr);
       // W = L^-1: lane c computes column c
       double w[7];
 #pragma unroll
       for (int rr = 0; rr < 7; rr++) {
         double acc = (rr == lane) ? 1.0 : 0.0;
 #pragma unroll
-        for (int mm = 0; mm < rr; mm++) acc -= readlane_d(a[mm], rr) * w[mm];
+        for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * w[mm];
         w[rr] = (rr >= lane) ? acc * dinv[rr] : 0.0;
       }
       if (lane < 7) {
@@ -1084,44 +1188,50 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
           Lb[(size_t)k * 49 + lane * 7 + qq] = (qq <= lane) ? a[qq] : 0.0;  // row `lane` of L_kk
           Di[(size_t)k * 49 + qq * 7 + lane] = w[qq];                       // column `lane` of W
         }
+      }
+      if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if M3S_LLT_CYC
+      if (lane == 0) D.dbg[64 + k] = (int64_t)(__builtin_amdgcn_s_memtime() - t0_) | ((int64_t)(q1 - q0) << 40);
+#endif
+      // forward step, off the factorisation's critical path:
+      // y_k = L_kk^-1 (b_k - sum_p L_kp y_p)
+      for (int q = q0; q < q1; q++) M3S_WAIT(&ydone[dtr_p[q]]);
+      double bb = y[k * 7 + lane7];
+      bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+      double yk[7];
+#pragma unroll
+      for (int rr = 0; rr < 7; rr++) {
+        double acc = readlane_d(bb, rr);
+#pragma unroll
+        for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * yk[mm];
+        yk[rr] = acc * dinv[rr];
+      }
+      if (lane < 7) {
         double yo = 0.0;
 #pragma unroll
         for (int qq = 0; qq < 7; qq++) yo = (qq == lane) ? yk[qq] : yo;
         y[k * 7 + lane] = yo;
       }
-      if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
-#if M3S_LLT_TIMING
-      if (lane == 0) D.dbg[k] = wall_clock64();
-#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_store(&ydone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
       const int t2 = item;
       const int dst = task_dst[t2], k = task_col[t2];
       const int q0 = task_tr_ptr[t2], q1 = task_tr_ptr[t2 + 1];
-      wait_flag(&sdone[k], &fail_s);  // W_k and (through DIAG(k)) every L_kp
-      for (int q = q0; q < q1; q++) wait_flag(&sdone[tr_a[q]], &fail_s);
+      M3S_WAIT(&sdone[k]);  // W_k and (through DIAG(k)) every L_kp
+      for (int q = q0; q < q1; q++) M3S_WAIT(&sdone[tr_a[q]]);
+#if M3S_LLT_CYC
+      const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+#endif
       double v = Lb[(size_t)dst * 49 + lane49];
-      int q = q0;
-      for (; q + 1 < q1; q += 2) {
-        const double *A0 = Lb + (size_t)tr_a[q] * 49, *B0 = Lb + (size_t)tr_b[q] * 49;
-        const double *A1 = Lb + (size_t)tr_a[q + 1] * 49, *B1 = Lb + (size_t)tr_b[q + 1] * 49;
-        double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) {
-          s0 += A0[r7 + mm] * B0[c7 + mm];
-          s1 += A1[r7 + mm] * B1[c7 + mm];
-        }
-        v -= s0;
-        v -= s1;
-      }
-      if (q < q1) {
-        const double *A0 = Lb + (size_t)tr_a[q] * 49, *B0 = Lb + (size_t)tr_b[q] * 49;
-        double s0 = 0.0;
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) s0 += A0[r7 + mm] * B0[c7 + mm];
-        v -= s0;
-      }
+      v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+#if M3S_LLT_CYC
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      cyc_trip += __builtin_amdgcn_s_memtime() - t0_;
+#endif
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -1131,8 +1241,18 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       wave_lds_fence();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if M3S_LLT_CYC
+      if (lane == 0) D.dbg[64 + dst] = (int64_t)(__builtin_amdgcn_s_memtime() - t0_) | ((int64_t)(q1 - q0) << 40);
+#endif
     }
   }
+#if M3S_LLT_CYC
+  if (lane == 0) {
+    D.dbg[3 * wave + 0] = (int64_t)(__builtin_amdgcn_s_memtime() - cyc_start);
+    D.dbg[3 * wave + 1] = (int64_t)cyc_wait;
+    D.dbg[3 * wave + 2] = (int64_t)cyc_trip;
+  }
+#endif
   __syncthreads();
 
   if (fail_s) {
@@ -1145,25 +1265,15 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // dataflow: column k waits for x_i of every i in struct(k)
   for (int t = wave; t < m; t += NW) {
     const int k = lev_col[m - 1 - t];
-    for (int q = col_ptr[k]; q < col_ptr[k + 1]; q++) {
-      wait_flag(&done2[col_row[q]], &fail_s);
-    }
-    double rr = (lane < 7) ? y[k * 7 + lane] : 0.0;
-    for (int q = col_ptr[k]; q < col_ptr[k + 1]; q++) {
-      const double *A = Lb + (size_t)col_slot[q] * 49;
-      const int i = col_row[q];
-      if (lane < 7) {
-        double s = 0.0;
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) s += A[mm * 7 + lane] * y[i * 7 + mm];
-        rr -= s;
-      }
-    }
+    const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
+    for (int q = q0; q < q1; q++) wait_flag(&done2[col_row[q]], &fail_s);
+    double rr = y[k * 7 + lane7];
+    rr = sub_matvec<STAGE, true>(rr, Lb, col_slot, col_row, q0, q1, y, lane7, lane49, lane, stg);
     double xk = 0.0;
 #pragma unroll
     for (int mm = 0; mm < 7; mm++) {
       const double rm = readlane_d(rr, mm);
-      if (lane < 7) xk += Di[(size_t)k * 49 + mm * 7 + lane] * rm;
+      xk += Di[(size_t)k * 49 + mm * 7 + lane7] * rm;
     }
     if (lane < 7) y[k * 7 + lane] = xk;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1405,7 +1515,7 @@ int read_K(const float *K, ResidualParams &P, hipStream_t st) {
 // calls prepare and solve separately.
 struct PlanMeta {
   bool sparse = false;
-  bool lds = false;
+  int store = 0;  // sparse_llt_kernel<STORE>
   size_t lds_bytes = 0;
   int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0;
   PlanImage img;  // offsets (data vector cleared after upload)
@@ -1551,7 +1661,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         I.off_lev_col,  I.off_dtr_ptr,      I.off_dtr_slot, I.off_dtr_p,    I.off_task_lev_ptr,
         I.off_task_dst, I.off_task_col,     I.off_task_tr_ptr, I.off_tr_a,  I.off_tr_b,
         I.off_asm_ptr,  I.off_asm_edge,     I.off_g_ptr,    I.off_g_edge,   I.off_ctask_ptr,
-        I.off_items};
+        I.off_items,    I.off_wave_ptr,     I.off_witems};
     for (int q = 0; q < kPlanSections; q++) D.off[q] = (int)offs[q];
     D.n_items = meta.n_items;
     D.dbg = at<int64_t>(ws, Ly.A);
@@ -1567,10 +1677,12 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     D.info = a->info;
     D.flags = flags;
     D.delta_thresh = a->delta_thresh;
-    if (meta.lds)
-      sparse_llt_kernel<true><<<1, 1024, meta.lds_bytes, st>>>(D);
+    if (meta.store == 1)
+      sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
+    else if (meta.store == 2)
+      sparse_llt_kernel<2><<<1, 1024, meta.lds_bytes, st>>>(D);
     else
-      sparse_llt_kernel<false><<<1, 1024, meta.lds_bytes, st>>>(D);
+      sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
     return launch_ok();
   }
   // dense fallback: RHS-augmented system, register or tiled LLT
@@ -1662,11 +1774,24 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       meta.levels = P.levels;
       meta.plan_len = (int)img.data.size();
       meta.n_items = (int)P.items.size();
-      const size_t flags_bytes = sizeof(int32_t) * (size_t)(P.S + P.m);
-      const size_t lds_all = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) +
-                             sizeof(int32_t) * ((img.data.size() + 1) & ~size_t(1)) + flags_bytes;
-      meta.lds = lds_all <= kMaxLdsBytes;
-      meta.lds_bytes = meta.lds ? lds_all : sizeof(double) * (size_t)P.m * 7 + flags_bytes;
+      // LDS plan of sparse_llt_kernel<STORE>: flags always, factor + W + y if
+      // they fit, the plan too if it fits as well; else global factor with
+      // per-wave stage areas
+      const size_t flags_bytes = sizeof(int32_t) * (((size_t)(P.S + 2 * P.m) + 1) & ~size_t(1));
+      const size_t fac_bytes = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7);
+      const size_t plan_bytes = sizeof(int32_t) * ((img.data.size() + 1) & ~size_t(1));
+      const size_t stage_bytes = sizeof(double) * 16 * (size_t)kStageDoubles;
+      if (fac_bytes + plan_bytes + flags_bytes <= kMaxLdsBytes) {
+        meta.store = 1;
+        meta.lds_bytes = fac_bytes + plan_bytes + flags_bytes;
+      } else if (fac_bytes + flags_bytes <= kMaxLdsBytes) {
+        meta.store = 2;
+        meta.lds_bytes = fac_bytes + flags_bytes;
+      } else {
+        meta.store = 0;
+        meta.lds_bytes = sizeof(double) * (size_t)P.m * 7 + flags_bytes + stage_bytes;
+        if (meta.lds_bytes > kMaxLdsBytes) meta.sparse = false;  // dense fallback
+      }
     }
   }
   if (E > 0) {
@@ -1703,9 +1828,11 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   if (meta.sparse && meta.lds_bytes > 64 * 1024) {
     static std::once_flag once;
     std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<0>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<false>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<2>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     });
   }
@@ -1951,7 +2078,7 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
       I.off_lev_col,  I.off_dtr_ptr,  I.off_dtr_slot,    I.off_dtr_p,    I.off_task_lev_ptr,
       I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a,     I.off_tr_b,
       I.off_asm_ptr,  I.off_asm_edge, I.off_g_ptr,       I.off_g_edge,   I.off_ctask_ptr,
-      I.off_items};
+      I.off_items,    I.off_wave_ptr, I.off_witems};
   if (meta) {
     meta[0] = P.m, meta[1] = P.S, meta[2] = P.levels;
     for (int k = 0; k < kPlanSections; k++) meta[3 + k] = (int32_t)offs[k];

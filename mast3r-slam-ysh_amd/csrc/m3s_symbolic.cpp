@@ -3,6 +3,9 @@
 #include "m3s_symbolic.h"
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <queue>
 #include <set>
 #include <unordered_map>
 
@@ -25,31 +28,155 @@ int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int3
 
 namespace {
 
-// minimum-degree elimination order on the variable graph (ties: lowest index)
-std::vector<int32_t> min_degree_order(int m, const std::vector<std::set<int>> &adj0) {
+// Minimum-degree elimination order on the variable graph (ties: lowest
+// index). With `multiple` set, each round eliminates an independent set of
+// minimum-degree (+ slack) variables together (multiple minimum degree): the
+// same kind of fill, but a shallower elimination tree, i.e. fewer dependent
+// steps in the dataflow factorisation.
+std::vector<int32_t> min_degree_order(int m, const std::vector<std::set<int>> &adj0, bool multiple,
+                                      int slack) {
   std::vector<std::set<int>> adj = adj0;
   std::vector<char> alive(m, 1);
   std::vector<int32_t> order;
   order.reserve(m);
-  for (int step = 0; step < m; step++) {
-    int best = -1;
-    size_t bd = 0;
-    for (int v = 0; v < m; v++)
-      if (alive[v] && (best < 0 || adj[v].size() < bd)) best = v, bd = adj[v].size();
-    order.push_back(best);
-    alive[best] = 0;
-    const std::set<int> nb = adj[best];
+  auto eliminate = [&](int v) {
+    order.push_back(v);
+    alive[v] = 0;
+    const std::set<int> nb = adj[v];
     for (int a : nb) {
-      adj[a].erase(best);
+      adj[a].erase(v);
       for (int b : nb)
         if (b != a) adj[a].insert(b);
     }
-    adj[best].clear();
+    adj[v].clear();
+  };
+  while ((int)order.size() < m) {
+    size_t dmin = SIZE_MAX;
+    for (int v = 0; v < m; v++)
+      if (alive[v] && adj[v].size() < dmin) dmin = adj[v].size();
+    if (!multiple) {
+      for (int v = 0; v < m; v++)
+        if (alive[v] && adj[v].size() == dmin) {
+          eliminate(v);
+          break;
+        }
+      continue;
+    }
+    std::vector<char> marked(m, 0);
+    std::vector<int> sel;
+    for (size_t d = dmin; d <= dmin + (size_t)slack; d++)
+      for (int v = 0; v < m; v++)
+        if (alive[v] && !marked[v] && adj[v].size() == d) {
+          sel.push_back(v);
+          marked[v] = 1;
+          for (int u : adj[v]) marked[u] = 1;
+        }
+    for (int v : sel) eliminate(v);
   }
   return order;
 }
 
+// elimination-tree height and number of off-diagonal factor blocks of an order
+std::pair<int, int64_t> etree_shape(int m, const std::vector<std::set<int>> &adj0,
+                                    const std::vector<int32_t> &order) {
+  std::vector<int32_t> pos(m);
+  for (int k = 0; k < m; k++) pos[order[k]] = k;
+  std::vector<std::set<int>> S(m);
+  for (int v = 0; v < m; v++)
+    for (int u : adj0[v])
+      if (pos[u] > pos[v]) S[pos[v]].insert(pos[u]);
+  std::vector<int> h(m, 0);
+  int64_t nnz = 0;
+  int height = m ? 1 : 0;
+  for (int k = 0; k < m; k++) {
+    nnz += (int64_t)S[k].size();
+    if (!S[k].empty()) {
+      const int par = *S[k].begin();
+      h[par] = std::max(h[par], h[k] + 1);
+      height = std::max(height, h[par] + 1);
+      for (int i : S[k])
+        if (i != par) S[par].insert(i);
+    }
+  }
+  return {height, nnz};
+}
+
 }  // namespace
+
+// Static list schedule of the dataflow items onto kLltWaves waves. Item
+// dependencies are the blocks it reads (DIAG(k): L_kp; OFF(i,k): W_k, L_ip,
+// L_kp); priority is the upward rank (longest cost path to the end) with a
+// rough cycle cost per item. Items are handed out in decreasing priority
+// among ready ones to the wave that frees first. Each wave runs its items in
+// assignment order; since every dependency was assigned earlier, the
+// unfinished item with the lowest assignment index can always run (no
+// deadlock), whatever the real timings.
+static void schedule_items(SparsePlan &P) {
+  const int n = (int)P.items.size();
+  const int T = (int)P.task_dst.size();
+  std::vector<int> item_of_slot(P.S, -1);
+  for (int it = 0; it < n; it++) {
+    const int v = P.items[it];
+    item_of_slot[v < 0 ? -1 - v : P.task_dst[v]] = it;
+  }
+  std::vector<std::vector<int>> deps(n), succ(n);
+  std::vector<double> cost(n);
+  for (int it = 0; it < n; it++) {
+    const int v = P.items[it];
+    std::vector<int> &d = deps[it];
+    if (v < 0) {
+      const int k = -1 - v;
+      for (int q = P.dtr_ptr[k]; q < P.dtr_ptr[k + 1]; q++) d.push_back(item_of_slot[P.dtr_slot[q]]);
+      cost[it] = 3000.0 + 300.0 * (P.dtr_ptr[k + 1] - P.dtr_ptr[k]);
+    } else {
+      d.push_back(item_of_slot[P.task_col[v]]);
+      for (int q = P.task_tr_ptr[v]; q < P.task_tr_ptr[v + 1]; q++) d.push_back(item_of_slot[P.tr_a[q]]);
+      cost[it] = 800.0 + 300.0 * (P.task_tr_ptr[v + 1] - P.task_tr_ptr[v]);
+    }
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    for (int x : d) succ[x].push_back(it);
+  }
+  (void)T;
+  // upward rank: items are listed in a topological order (level order)
+  std::vector<double> rank(n, 0.0);
+  for (int it = n - 1; it >= 0; it--) {
+    double best = 0.0;
+    for (int s2 : succ[it]) best = std::max(best, rank[s2]);
+    rank[it] = cost[it] + best;
+  }
+  std::vector<int> missing(n);
+  std::vector<double> ready_at(n, 0.0);
+  using Entry = std::pair<double, int>;  // (priority, -item) max-heap
+  std::priority_queue<Entry> ready;
+  for (int it = 0; it < n; it++) {
+    missing[it] = (int)deps[it].size();
+    if (!missing[it]) ready.push({rank[it], -it});
+  }
+  std::vector<double> free_at(kLltWaves, 0.0);
+  std::vector<std::vector<int32_t>> seq(kLltWaves);
+  while (!ready.empty()) {
+    const int it = -ready.top().second;
+    ready.pop();
+    int w = 0;
+    for (int x = 1; x < kLltWaves; x++)
+      if (free_at[x] < free_at[w]) w = x;
+    const double start = std::max(free_at[w], ready_at[it]);
+    const double finish = start + cost[it];
+    free_at[w] = finish;
+    seq[w].push_back(P.items[it]);
+    for (int s2 : succ[it]) {
+      ready_at[s2] = std::max(ready_at[s2], finish);
+      if (--missing[s2] == 0) ready.push({rank[s2], -s2});
+    }
+  }
+  P.wave_ptr.assign(1, 0);
+  P.witems.clear();
+  for (int w = 0; w < kLltWaves; w++) {
+    P.witems.insert(P.witems.end(), seq[w].begin(), seq[w].end());
+    P.wave_ptr.push_back((int32_t)P.witems.size());
+  }
+}
 
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
                        SparsePlan &P) {
@@ -62,7 +189,16 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     const int a = ri[e] - 1, b = rj[e] - 1;
     if (a >= 0 && b >= 0 && a != b) adj[a].insert(b), adj[b].insert(a);
   }
-  P.perm = min_degree_order(m, adj);
+  {  // the shallowest elimination tree among MD / MMD variants (fill breaks ties)
+    std::vector<int32_t> best = min_degree_order(m, adj, false, 0);
+    std::pair<int, int64_t> bs = etree_shape(m, adj, best);
+    for (int slack = 0; slack <= 1; slack++) {
+      std::vector<int32_t> o = min_degree_order(m, adj, true, slack);
+      const std::pair<int, int64_t> sh = etree_shape(m, adj, o);
+      if (sh.first < bs.first || (sh.first == bs.first && sh.second < bs.second)) best = o, bs = sh;
+    }
+    P.perm = best;
+  }
   P.iperm.assign(m, 0);
   for (int k = 0; k < m; k++) P.iperm[P.perm[k]] = k;
 
@@ -147,6 +283,7 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     }
     P.task_lev_ptr.push_back((int32_t)P.task_dst.size());
   }
+  schedule_items(P);
   // assembly lists (edge order => deterministic sums)
   std::vector<std::vector<int32_t>> asl(P.S), gl(m);
   for (int64_t e = 0; e < E; e++) {
@@ -198,6 +335,8 @@ void flatten_plan(const SparsePlan &P, PlanImage &img) {
   img.off_g_edge = put(P.g_edge);
   img.off_ctask_ptr = put(P.ctask_ptr);
   img.off_items = put(P.items);
+  img.off_wave_ptr = put(P.wave_ptr);
+  img.off_witems = put(P.witems);
 }
 
 }  // namespace m3s

@@ -36,6 +36,9 @@ struct SparsePlan {
   std::vector<int32_t> ctask_ptr;
   // dataflow work items in level order: -1-k = DIAG(k), t >= 0 = off-diagonal task t
   std::vector<int32_t> items;
+  // the items assigned to the kernel's waves by host list scheduling: wave w
+  // runs witems[wave_ptr[w] .. wave_ptr[w+1]) in order
+  std::vector<int32_t> wave_ptr, witems;
 };
 
 // ranks of (ii, jj) in sorted-unique(cat(ii, jj)); returns the unique count
@@ -52,9 +55,10 @@ struct PlanImage {
   int64_t off_perm, off_col_ptr, off_col_row, off_col_slot, off_lev_ptr, off_lev_col, off_dtr_ptr,
       off_dtr_slot, off_dtr_p, off_task_lev_ptr, off_task_dst, off_task_col, off_task_tr_ptr,
       off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge, off_ctask_ptr,
-      off_items;
+      off_items, off_wave_ptr, off_witems;
 };
-constexpr int kPlanSections = 21;
+constexpr int kPlanSections = 23;
+constexpr int kLltWaves = 16;  // waves of sparse_llt_kernel (1024 threads)
 void flatten_plan(const SparsePlan &P, PlanImage &img);
 
 }  // namespace m3s

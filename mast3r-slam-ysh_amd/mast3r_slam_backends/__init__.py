@@ -123,7 +123,7 @@ def version() -> str:
 
 PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col", "dtr_ptr",
                  "dtr_slot", "dtr_p", "task_lev_ptr", "task_dst", "task_col", "task_tr_ptr", "tr_a",
-                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items")
+                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items", "wave_ptr", "witems")
 
 
 LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
@@ -159,7 +159,7 @@ def sparse_plan(N, ri, rj):
     lens = {"perm": m, "col_ptr": m + 1, "lev_ptr": L + 1, "lev_col": m, "dtr_ptr": m + 1,
             "task_lev_ptr": L + 1, "task_dst": T, "task_col": T, "task_tr_ptr": T + 1,
             "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1,
-            "items": m + T}
+            "items": m + T, "wave_ptr": 17, "witems": m + T}
     for name, ln in lens.items():
         plan[name] = plan[name][:ln]
     nnz = int(plan["col_ptr"][m])

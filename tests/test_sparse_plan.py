@@ -1,10 +1,10 @@
 """CPU check of the host symbolic plan of the block-sparse LLT (the part of the
 solver that replaces Eigen's SimplicialLLT analysis, gn_kernels.cu:132-153).
 
-The plan is executed in numpy in the order of sparse_llt_kernel's dataflow
-work items (assembly lists -> DIAG(k) / OFF(i,k) items in list order -> back
-substitution in reverse level order), asserting that every block an item
-reads is already complete on random SPD edge blocks, and the solution is compared with
+The plan is executed in numpy the way sparse_llt_kernel runs it (assembly
+lists -> the 16 waves' list-scheduled DIAG(k) / OFF(i,k) items, each waiting
+for the blocks it reads -> back substitution in reverse level order); a
+schedule that could deadlock fails the test on random SPD edge blocks, and the solution is compared with
 a dense fp64 solve of the same assembled system.
 """
 import numpy as np
@@ -47,16 +47,26 @@ def run_plan(p, Hjj, gj):
             ent = p["g_edge"][t]
             y[v] += gj[ent >> 1] * (1 if ent & 1 else -1)
     W = np.zeros((m, 7, 7))
-    # the kernel's dataflow work items in list order; each asserts that the
-    # blocks it reads are complete (the LDS flags the kernel waits on)
+    # the kernel's dataflow: wave w runs witems[wave_ptr[w]:wave_ptr[w+1]] in
+    # order and waits on the blocks an item reads. Simulated by stepping the
+    # waves round-robin; a full round without progress would be a deadlock.
     sdone = np.zeros(S, bool)
-    for item in p["items"]:
+    pos = [p["wave_ptr"][w] for w in range(16)]
+
+    def ready(item):
+        if item < 0:
+            k = -1 - item
+            return all(sdone[p["dtr_slot"][q]] for q in range(p["dtr_ptr"][k], p["dtr_ptr"][k + 1]))
+        k = p["task_col"][item]
+        return sdone[k] and all(sdone[p["tr_a"][q]] and sdone[p["tr_b"][q]]
+                                for q in range(p["task_tr_ptr"][item], p["task_tr_ptr"][item + 1]))
+
+    def run(item):
         if item < 0:
             k = -1 - item
             D = L[k].copy()
             b = y[k].copy()
             for q in range(p["dtr_ptr"][k], p["dtr_ptr"][k + 1]):
-                assert sdone[p["dtr_slot"][q]], "DIAG reads an unfinished block"
                 A = L[p["dtr_slot"][q]]
                 D -= A @ A.T
                 b -= A @ y[p["dtr_p"][q]]
@@ -67,13 +77,21 @@ def run_plan(p, Hjj, gj):
             sdone[k] = True
         else:
             dst, k = p["task_dst"][item], p["task_col"][item]
-            assert sdone[k], "OFF before its DIAG"
             A = L[dst].copy()
             for q in range(p["task_tr_ptr"][item], p["task_tr_ptr"][item + 1]):
-                assert sdone[p["tr_a"][q]] and sdone[p["tr_b"][q]], "OFF reads an unfinished block"
                 A -= L[p["tr_a"][q]] @ L[p["tr_b"][q]].T
             L[dst] = A @ W[k].T
             sdone[dst] = True
+
+    while any(pos[w] < p["wave_ptr"][w + 1] for w in range(16)):
+        progressed = False
+        for w in range(16):
+            if pos[w] < p["wave_ptr"][w + 1] and ready(p["witems"][pos[w]]):
+                run(p["witems"][pos[w]])
+                pos[w] += 1
+                progressed = True
+        assert progressed, "wave schedule deadlocks"
+    assert sorted(p["witems"].tolist()) == sorted(p["items"].tolist())
     assert sdone.all()
     done = np.zeros(m, bool)
     done[:] = False

@@ -28,13 +28,19 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
     plan = be.sparse_plan(N, *[torch.searchsorted(torch.unique(torch.cat([g.ii, g.jj])), t).cpu().numpy() for t in (g.ii, g.jj)])
     import numpy as np
     m = N - 1
-    stamps = wst[lay["A"]: lay["A"] + 8 * m].clone().view(torch.int64).cpu().numpy()
-    ts0 = wst[lay["flags"] + 64: lay["flags"] + 72].clone().view(torch.int64).cpu().item()
-    lev = np.zeros(m, int)
-    lp, lc = plan["lev_ptr"], plan["lev_col"]
-    for l in range(plan["levels"]):
-        lev[lc[lp[l]:lp[l + 1]]] = l
-    fin_by_level = [max((stamps[k] - ts0) / 100.0 for k in lc[lp[l]:lp[l + 1]]) for l in range(plan["levels"])]
-    print("  DIAG completion (us since kernel start) by level:", " ".join(f"{x:.0f}" for x in fin_by_level))
+    if os.environ.get("CYC") == "1":
+        d = wst[lay["A"]: lay["A"] + 8 * 48].clone().view(torch.int64).cpu().numpy().reshape(16, 3)
+        print("  per-wave factor cycles: total %.0f, waiting %.0f (%.0f%%), update products %.0f (%.0f%%)"
+              % (d[:, 0].mean(), d[:, 1].mean(), 100 * d[:, 1].mean() / d[:, 0].mean(),
+                 d[:, 2].mean(), 100 * d[:, 2].mean() / d[:, 0].mean()))
+        S_ = plan["S"]
+        it_ = wst[lay["A"] + 8 * 64: lay["A"] + 8 * (64 + S_)].clone().view(torch.int64).cpu().numpy()
+        dur, nt = it_ & ((1 << 40) - 1), it_ >> 40
+        for name, sel in (("DIAG", slice(0, m)), ("OFF", slice(m, S_))):
+            dd, nn = dur[sel], nt[sel]
+            for lo, hi in ((0, 1), (1, 3), (3, 8), (8, 100)):
+                mk = (nn >= lo) & (nn < hi)
+                if mk.any():
+                    print(f"    {name} items with {lo}-{hi - 1} updates: n={mk.sum()} mean {dd[mk].mean():.0f} cycles")
     print(f"N={N} levels={plan['levels']} S={plan['S']}: assembly {r[0]:.1f} us, factor {r[1]:.1f} us, "
           f"backsub {r[2]:.1f} us, retract {r[3]:.1f} us")

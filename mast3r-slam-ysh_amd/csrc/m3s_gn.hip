@@ -83,8 +83,8 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 }
 
 struct Layout {
-  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, tasks, planes,
-      total;
+  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, tasks,
+      planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -124,6 +124,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 49 * (size_t)L.slot_cap, 256);
   L.Dinv = off;
   off = align_up(off + sizeof(double) * 49 * (size_t)(m + 1), 256);
+  L.rhs = off;
+  off = align_up(off + sizeof(double) * 7 * (size_t)(m + 1), 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
   // target-side planes of every edge (5 planes = rays, the widest mode)
@@ -856,6 +858,38 @@ __global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__rest
   }
 }
 
+// Block-sparse assembly, one 64-thread block per factor slot (then one per
+// free pose for the RHS): slot s = sum over its assembly edges, in edge order,
+// of +H_jj (diagonal slots) or -H_jj (off-diagonal slots); rhs_v = sum of
+// +-g_j. Written to the global factor array the LLT kernel starts from.
+__global__ void __launch_bounds__(64) assemble_slots_kernel(const double *__restrict__ fin,
+                                                            const int32_t *__restrict__ plan, int off_asm_ptr,
+                                                            int off_asm_edge, int off_g_ptr, int off_g_edge,
+                                                            int m, int S, double *__restrict__ L,
+                                                            double *__restrict__ rhs,
+                                                            const int32_t *__restrict__ stop) {
+  if (*stop) return;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (b < S) {
+    if (t >= 49) return;
+    const int32_t *asm_ptr = plan + off_asm_ptr, *asm_edge = plan + off_asm_edge;
+    double v = 0.0;
+    for (int q = asm_ptr[b]; q < asm_ptr[b + 1]; q++) v += fin[(size_t)asm_edge[q] * kFin + t];
+    L[(size_t)b * 49 + t] = (b < m) ? v : -v;
+  } else {
+    const int vv = b - S;
+    if (t >= 7 || vv >= m) return;
+    const int32_t *g_ptr = plan + off_g_ptr, *g_edge = plan + off_g_edge;
+    double v = 0.0;
+    for (int q = g_ptr[vv]; q < g_ptr[vv + 1]; q++) {
+      const int ent = g_edge[q];
+      const double gj = fin[(size_t)(ent >> 1) * kFin + 49 + t];
+      v += (ent & 1) ? gj : -gj;
+    }
+    rhs[(size_t)vv * 7 + t] = v;
+  }
+}
+
 struct SparseDev {
   const int32_t *plan;  // flattened plan (global); copied to LDS by the IN_LDS variant
   int plan_len;
@@ -865,6 +899,7 @@ struct SparseDev {
   double *L;     // [S][49] (global variant)
   double *Dinv;  // [m][49] (global variant)
   const double *fin;
+  const double *rhs;  // assembled RHS [m][7] (assemble_slots_kernel)
   float *Twc;
   int64_t N;
   float *dx_out;
@@ -1087,25 +1122,12 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #endif
   double *scr = scratch[wave];
 
-  // 0. assembly (edge order within each slot: deterministic)
-  for (int idx = tid; idx < S * 49; idx += 1024) {
-    const int s = idx / 49, q = idx - s * 49;
-    double v = 0.0;
-    for (int t = asm_ptr[s]; t < asm_ptr[s + 1]; t++) v += D.fin[(size_t)asm_edge[t] * kFin + q];
-    Lb[idx] = (s < m) ? v : -v;
+  // 0. the assembled factor (assemble_slots_kernel) into LDS, RHS into LDS
+  if (IN_LDS) {
+    for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
   }
-  for (int idx = tid; idx < m * 7; idx += 1024) {
-    const int vv = idx / 7, q = idx - vv * 7;
-    double v = 0.0;
-    for (int t = g_ptr[vv]; t < g_ptr[vv + 1]; t++) {
-      const int ent = g_edge[t];
-      const double gj = D.fin[(size_t)(ent >> 1) * kFin + 49 + q];
-      v += (ent & 1) ? gj : -gj;
-    }
-    y[idx] = v;
-  }
+  for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
   if (tid == 0) fail_s = 0;
-  if (!IN_LDS) __threadfence_block();
   __syncthreads();
   M3S_TS(1)
 
@@ -1669,6 +1691,11 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     D.S = meta.S;
     D.levels = meta.levels;
     D.L = at<double>(ws, Ly.Lblk);
+    D.rhs = at<double>(ws, Ly.rhs);
+    assemble_slots_kernel<<<dim3((unsigned)(meta.S + meta.m)), dim3(64), 0, st>>>(
+        fin, D.plan, (int)I.off_asm_ptr, (int)I.off_asm_edge, (int)I.off_g_ptr, (int)I.off_g_edge, meta.m,
+        meta.S, D.L, at<double>(ws, Ly.rhs), stop);
+    if ((rc = launch_ok())) return rc;
     D.Dinv = at<double>(ws, Ly.Dinv);
     D.fin = fin;
     D.Twc = a->Twc;

@@ -209,6 +209,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_tracker:
         out["tracker_c2"] = tracker_leg(be, synthetic, dev, H, W)
+        out["matching_512"] = matching_leg(be, synthetic, dev, H, W)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E)
     if rank == 0:
@@ -236,6 +237,35 @@ def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
     return {"workload": "C2: 1 frame->keyframe pair, rays+dist Sim3 GN, %dx%d, %d fixed iterations"
                         % (H, W, iters),
             "gn_iters_per_s": round(reps * iters / dt, 1), "ms_per_solve": round(dt / reps * 1e3, 4)}
+
+
+def matching_leg(be, synthetic, dev, H, W, reps=20):
+    """iter_proj + refine_matches on one 512x512 view pair
+    (matching.py:52-90 with base.yaml's matching config)."""
+    from mast3r_slam_amd import matching
+
+    m = synthetic.make_match_inputs(H, W, device=dev)
+    img, pts, p0 = matching.prep_for_iter_proj(m.X11, m.X21)
+    cfg = matching.MATCHING_CFG
+    p1 = be.iter_proj(img, pts, p0, cfg["max_iter"], cfg["lambda_init"], cfg["convergence_thresh"])[0].long()
+    times = {}
+    for name, fn in (
+        ("iter_proj", lambda: be.iter_proj(img, pts, p0, cfg["max_iter"], cfg["lambda_init"],
+                                           cfg["convergence_thresh"])),
+        ("refine_matches", lambda: be.refine_matches(m.D11, m.D21, p1, cfg["radius"], cfg["dilation_max"])),
+    ):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        times[name] = round(e0.elapsed_time(e1) / reps, 4)
+    return {"workload": "one %dx%d view pair, F=%d float16 descriptors, matching config of base.yaml"
+                        % (H, W, m.D11.shape[-1]),
+            "ms_iter_proj": times["iter_proj"], "ms_refine_matches": times["refine_matches"]}
 
 
 def cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E):

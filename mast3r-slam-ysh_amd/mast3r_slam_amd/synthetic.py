@@ -275,3 +275,49 @@ def make_pair(H: int, W: int, seed: int = 1001, device=None, identity_idx=False)
     xi[:, 6] = torch.randn(1, generator=gen) * 0.01
     T_WCf_init = Sim3.exp(xi.to(device)) * T_WCf_gt
     return Pair(H, W, K, T_WCk, T_WCf_gt, T_WCf_init, Xf, Xk, Qk, valid, Cf, Ck)
+
+
+@dataclass
+class MatchInputs:
+    """Inputs of matching.match (matching.py:8-10) for one view pair: X11 is view
+    1's pointmap in camera 1, X21 view 2's pointmap expressed in camera 1 (what
+    MASt3R's pairwise head returns), D11 / D21 per-pixel descriptors. p_true is
+    the pixel of view 1 each view-2 pixel projects to (vis marks visible ones)."""
+    H: int
+    W: int
+    X11: torch.Tensor  # [1, H, W, 3] f32
+    X21: torch.Tensor  # [1, H, W, 3] f32
+    D11: torch.Tensor  # [1, H, W, F] f16
+    D21: torch.Tensor  # [1, H*W, F] f16
+    p_true: torch.Tensor  # [1, H*W, 2] int64
+    vis: torch.Tensor  # [1, H*W] bool
+
+
+def make_match_inputs(H: int, W: int, seed: int = 1005, device=None, F: int = 24) -> MatchInputs:
+    gen = torch.Generator().manual_seed(seed)
+    K = intrinsics(H, W, device)
+    T = loop_trajectory(16, gen, device=device)[0:2]
+    rays = pixel_rays(H, W, K)
+    depth = raycast_depth(T, rays)
+    X = depth[..., None] * rays[None]
+    Xw2 = T[1:2].act(X[1])
+    idx, vis = correspondences(Xw2, T[0:1], depth[0], K, H, W)
+    X21 = T[0:1].inv().act(Xw2)
+    p_true = torch.stack((idx % W, idx // W), -1)
+    # descriptors: a spatially smooth unit feature field for view 1 (blurred
+    # noise plus a fine-scale part), view 2 = the matched view-1 feature plus
+    # noise where visible (random elsewhere)
+    raw = torch.randn(1, F, H, W, generator=gen)
+    g = torch.exp(-0.5 * (torch.arange(-6, 7, dtype=torch.float32) / 3.0) ** 2)
+    g = g / g.sum()
+    sm = torch.nn.functional.conv2d(torch.nn.functional.pad(raw, (6, 6, 0, 0), mode="replicate"),
+                                    g.view(1, 1, 1, 13).repeat(F, 1, 1, 1), groups=F)
+    sm = torch.nn.functional.conv2d(torch.nn.functional.pad(sm, (0, 0, 6, 6), mode="replicate"),
+                                    g.view(1, 1, 13, 1).repeat(F, 1, 1, 1), groups=F)
+    field = sm / sm.std() + 0.15 * torch.randn(1, F, H, W, generator=gen)
+    D11 = torch.nn.functional.normalize(field[0].permute(1, 2, 0).reshape(H * W, F), dim=-1).to(device)
+    noise = torch.nn.functional.normalize(torch.randn(H * W, F, generator=gen), dim=-1).to(device)
+    D21 = torch.where(vis[:, None], torch.nn.functional.normalize(D11[idx] + 0.3 * noise, dim=-1), noise)
+    return MatchInputs(H, W, X[0].reshape(1, H, W, 3).contiguous(), X21.reshape(1, H, W, 3).contiguous(),
+                       D11.reshape(1, H, W, F).half().contiguous(), D21[None].half().contiguous(),
+                       p_true[None].contiguous(), vis[None].contiguous())

@@ -1,6 +1,6 @@
 """``mast3r_slam_backends`` — drop-in for the reference's CUDA extension module,
 backed by the MI355X HIP library ``libm3s_gn.so`` through its C ABI
-(``include/m3s_gn.h``).
+(``include/m3s_gn.h``, ``include/m3s_match.h``).
 
 Reference interface (``/root/reference/mast3r_slam/backend/src/gn.cpp:116-122``):
 same module name, same function names, same positional arguments, same
@@ -17,8 +17,8 @@ module fails at import.
 New entry points (the reference tracker has no backend call, tracker.py:173-266):
 ``track_rays_sim3`` and ``track_calib_sim3``.
 
-``iter_proj`` / ``refine_matches`` (matching kernels, SURVEY.md §8f "next" #1)
-are exported for interface completeness and raise ``NotImplementedError``.
+``iter_proj`` / ``refine_matches`` (gn.cpp:84-114, matching_kernels.cu) run
+the HIP matching kernels with the reference's signatures and return values.
 """
 from __future__ import annotations
 
@@ -57,6 +57,28 @@ class GnArgs(ctypes.Structure):
     ]
 
 
+class IterProjArgs(ctypes.Structure):
+    """Mirror of ``m3s_iter_proj_args`` (include/m3s_match.h)."""
+
+    _fields_ = [
+        ("rays_img", _VP), ("pts_3d_norm", _VP), ("p_init", _VP),
+        ("B", ctypes.c_int64), ("H", ctypes.c_int64), ("W", ctypes.c_int64), ("N", ctypes.c_int64),
+        ("max_iter", ctypes.c_int), ("lambda_init", ctypes.c_float), ("cost_thresh", ctypes.c_float),
+        ("p_new", _VP), ("converged", _VP),
+    ]
+
+
+class RefineArgs(ctypes.Structure):
+    """Mirror of ``m3s_refine_args`` (include/m3s_match.h)."""
+
+    _fields_ = [
+        ("D11", _VP), ("D21", _VP), ("p1", _VP),
+        ("B", ctypes.c_int64), ("H", ctypes.c_int64), ("W", ctypes.c_int64), ("N", ctypes.c_int64),
+        ("F", ctypes.c_int64), ("dtype", ctypes.c_int), ("radius", ctypes.c_int),
+        ("dilation_max", ctypes.c_int), ("p1_new", _VP),
+    ]
+
+
 class TrackArgs(ctypes.Structure):
     """Mirror of ``m3s_track_args`` (include/m3s_gn.h)."""
 
@@ -78,7 +100,7 @@ EXPORTS = (
     "m3s_gn_workspace_size", "m3s_gauss_newton_points", "m3s_gauss_newton_rays",
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
-    "m3s_sparse_plan_debug", "m3s_gn_layout_debug",
+    "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
 )
 
 
@@ -109,6 +131,10 @@ def _load():
     lib.m3s_version.argtypes = []
     lib.m3s_sparse_plan_debug.restype = ctypes.c_int64
     lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, _VP, ctypes.c_int64, _VP]
+    lib.m3s_iter_proj.restype = ctypes.c_int
+    lib.m3s_iter_proj.argtypes = [P(IterProjArgs), _VP]
+    lib.m3s_refine_matches.restype = ctypes.c_int
+    lib.m3s_refine_matches.argtypes = [P(RefineArgs), _VP]
     lib.m3s_gn_layout_debug.restype = ctypes.c_size_t
     lib.m3s_gn_layout_debug.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP]
     return lib
@@ -293,13 +319,52 @@ def gauss_newton_calib(Twc, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q, height
 
 
 def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh):
-    """matching_kernels.cu:119-315 — not part of this build's scope yet (SURVEY §8f #1)."""
-    raise NotImplementedError("iter_proj: matching kernels are not built yet (SURVEY.md §8f #1)")
+    """gn.cpp:84-99 / matching_kernels.cu:119-296: per-pixel LM projection.
+
+    rays_img_with_grad [B,H,W,9] f32, pts_3d_norm [B,N,3] f32, p_init [B,N,2]
+    f32 -> [p_new [B,N,2] f32, converged [B,N] bool] (new tensors)."""
+    for name, t in (("rays_img_with_grad", rays_img_with_grad), ("pts_3d_norm", pts_3d_norm),
+                    ("p_init", p_init)):
+        _check(t, name, torch.float32)
+    B, H, W, C = rays_img_with_grad.shape
+    Bn, N = int(p_init.shape[0]), int(p_init.shape[1])
+    if C != 9 or Bn != B or tuple(pts_3d_norm.shape) != (B, N, 3) or tuple(p_init.shape) != (B, N, 2):
+        raise RuntimeError("iter_proj: expected rays [B,H,W,9], pts_3d_norm [B,N,3], p_init [B,N,2]")
+    dev = p_init.device
+    p_new = torch.zeros(B, N, 2, dtype=torch.float32, device=dev)
+    converged = torch.zeros(B, N, dtype=torch.bool, device=dev)
+    a = IterProjArgs()
+    a.rays_img, a.pts_3d_norm, a.p_init = _p(rays_img_with_grad), _p(pts_3d_norm), _p(p_init)
+    a.B, a.H, a.W, a.N = B, H, W, N
+    a.max_iter, a.lambda_init, a.cost_thresh = int(max_iter), float(lambda_init), float(cost_thresh)
+    a.p_new, a.converged = _p(p_new), _p(converged)
+    _raise(_lib.m3s_iter_proj(ctypes.byref(a), _stream(dev)), "m3s_iter_proj")
+    return [p_new, converged]
 
 
 def refine_matches(D11, D21, p1, radius, dilation_max):
-    """matching_kernels.cu:25-116 — not part of this build's scope yet (SURVEY §8f #1)."""
-    raise NotImplementedError("refine_matches: matching kernels are not built yet (SURVEY.md §8f #1)")
+    """gn.cpp:101-114 / matching_kernels.cu:25-116: dilated local search.
+
+    D11 [B,H,W,F] f16 (or f32), D21 [B,N,F] same dtype, p1 [B,N,2] int64 (u, v)
+    -> [p1_new [B,N,2] int64] (new tensor)."""
+    _check(D11, "D11")
+    _check(D21, "D21", D11.dtype)
+    _check(p1, "p1", torch.int64)
+    dt = {torch.float16: 0, torch.float32: 1}.get(D11.dtype)
+    if dt is None:
+        raise RuntimeError(f"refine_matches: descriptors must be float16 or float32 (got {D11.dtype})")
+    B, H, W, F = D11.shape
+    N = int(p1.shape[1])
+    if tuple(D21.shape) != (B, N, F) or tuple(p1.shape) != (B, N, 2):
+        raise RuntimeError("refine_matches: expected D11 [B,H,W,F], D21 [B,N,F], p1 [B,N,2]")
+    p1_new = torch.zeros(B, N, 2, dtype=torch.int64, device=p1.device)
+    a = RefineArgs()
+    a.D11, a.D21, a.p1 = _p(D11), _p(D21), _p(p1)
+    a.B, a.H, a.W, a.N, a.F = B, H, W, N, F
+    a.dtype, a.radius, a.dilation_max = dt, int(radius), int(dilation_max)
+    a.p1_new = _p(p1_new)
+    _raise(_lib.m3s_refine_matches(ctypes.byref(a), _stream(p1.device)), "m3s_refine_matches")
+    return [p1_new]
 
 
 # ------------------------------------------------------------ tracker ---

@@ -16,6 +16,7 @@ import torch
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 HEADER = os.path.join(ROOT, "include", "m3s_gn.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "m3s_match.h")]
 
 
 @pytest.fixture(scope="module")
@@ -26,7 +27,7 @@ def be():
 
 
 def test_library_exports_every_header_symbol(be):
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     declared = set(re.findall(r"\b(m3s_[a-z0-9_]+)\s*\(", src))
     assert declared == set(be.EXPORTS)
     for sym in declared:
@@ -38,14 +39,20 @@ def test_reference_entry_points_present(be):
     for f in ("gauss_newton_points", "gauss_newton_rays", "gauss_newton_calib", "iter_proj",
               "refine_matches"):
         assert callable(getattr(be, f))
-    with pytest.raises(NotImplementedError):
-        be.iter_proj(None, None, None, 10, 1e-8, 1e-6)
+    with pytest.raises(RuntimeError):  # CPU tensors: no CPU path
+        be.iter_proj(torch.zeros(1, 4, 4, 9), torch.zeros(1, 16, 3), torch.zeros(1, 16, 2), 10, 1e-8,
+                     1e-6)
+    with pytest.raises(RuntimeError):
+        be.refine_matches(torch.zeros(1, 4, 4, 8, dtype=torch.float16),
+                          torch.zeros(1, 16, 8, dtype=torch.float16),
+                          torch.zeros(1, 16, 2, dtype=torch.int64), 3, 5)
 
 
 PROBE = r"""
 #include <stdio.h>
 #include <stddef.h>
 #include "m3s_gn.h"
+#include "m3s_match.h"
 #define F(T, m) printf(#T "." #m " %zu\n", offsetof(T, m))
 int main(void) {
   printf("m3s_gn_args.size %zu\n", sizeof(m3s_gn_args));
@@ -57,6 +64,13 @@ int main(void) {
   F(m3s_track_args, K); F(m3s_track_args, HW); F(m3s_track_args, height); F(m3s_track_args, z_eps);
   F(m3s_track_args, huber_k); F(m3s_track_args, max_iters); F(m3s_track_args, sync_every);
   F(m3s_track_args, T_WCf_out); F(m3s_track_args, workspace_bytes);
+  printf("m3s_iter_proj_args.size %zu\n", sizeof(m3s_iter_proj_args));
+  F(m3s_iter_proj_args, B); F(m3s_iter_proj_args, N); F(m3s_iter_proj_args, max_iter);
+  F(m3s_iter_proj_args, lambda_init); F(m3s_iter_proj_args, cost_thresh);
+  F(m3s_iter_proj_args, p_new); F(m3s_iter_proj_args, converged);
+  printf("m3s_refine_args.size %zu\n", sizeof(m3s_refine_args));
+  F(m3s_refine_args, p1); F(m3s_refine_args, F); F(m3s_refine_args, dtype);
+  F(m3s_refine_args, radius); F(m3s_refine_args, dilation_max); F(m3s_refine_args, p1_new);
   return 0;
 }
 """
@@ -69,7 +83,8 @@ def test_ctypes_struct_layout_matches_header(be, tmp_path):
     subprocess.check_call(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)])
     out = subprocess.check_output([str(exe)]).decode().split("\n")
     got = dict(l.split() for l in out if l.strip())
-    mirror = {"m3s_gn_args": be.GnArgs, "m3s_track_args": be.TrackArgs}
+    mirror = {"m3s_gn_args": be.GnArgs, "m3s_track_args": be.TrackArgs,
+              "m3s_iter_proj_args": be.IterProjArgs, "m3s_refine_args": be.RefineArgs}
     for key, val in got.items():
         t, m = key.split(".")
         cls = mirror[t]

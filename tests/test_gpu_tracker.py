@@ -95,3 +95,36 @@ def test_tracker_c1_shape_matches_oracle(be, calib):
     assert info[0] == it
     tol = pose_tol([r["tau"][0] for r in rec])
     np.testing.assert_allclose(T_WCf[0], T_f[0], atol=tol)
+
+
+@pytest.mark.parametrize("name", ["tracker_rays_64x48", "tracker_calib_64x48"])
+def test_host_tracker_mirror(golden_dir, name):
+    """mast3r_slam_amd.tracker.opt_pose_* (tracker.py:173-266 signatures) vs the
+    reference's own outputs, Sim3 in / Sim3 out."""
+    from mast3r_slam_amd import tracker
+    from mast3r_slam_amd.sim3 import Sim3
+
+    d = dict(np.load(os.path.join(golden_dir, name + ".npz")))
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k])).to(DEV)  # noqa: E731
+    cfg = dict(tracker.TRACKING_CFG, max_iters=int(d["max_iters"]))
+    if int(d["calib"]):
+        T_WCf, T_CkCf = tracker.opt_pose_calib_sim3(
+            t("Xf"), t("Xk"), Sim3(t("T_WCf_init")), Sim3(t("T_WCk")), t("Qk"), t("valid"), None, None,
+            t("K"), (int(d["H"]), int(d["W"])), cfg=cfg)
+    else:
+        T_WCf, T_CkCf = tracker.opt_pose_ray_dist_sim3(
+            t("Xf"), t("Xk"), Sim3(t("T_WCf_init")), Sim3(t("T_WCk")), t("Qk"), t("valid"), cfg=cfg)
+    tol = pose_tol(d["tau_iter"])
+    np.testing.assert_allclose(T_WCf.data.cpu().numpy()[0], d["T_WCf"][0], atol=tol)
+    np.testing.assert_allclose(T_CkCf.data.cpu().numpy()[0], d["T_CkCf"][0], atol=tol)
+
+
+def test_host_tracker_mirror_raises_on_cholesky_failure(golden_dir):
+    from mast3r_slam_amd import tracker
+    from mast3r_slam_amd.sim3 import Sim3
+
+    d = dict(np.load(os.path.join(golden_dir, "tracker_rays_allinvalid_32x24.npz")))
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k])).to(DEV)  # noqa: E731
+    with pytest.raises(torch.linalg.LinAlgError):
+        tracker.opt_pose_ray_dist_sim3(t("Xf"), t("Xk"), Sim3(t("T_WCf_init")), Sim3(t("T_WCk")),
+                                       t("Qk"), t("valid"))

@@ -1544,7 +1544,13 @@ struct PlanMeta {
   // linearize state of this solve call: edge ranks, the task table of the
   // edge range last linearized (host copy stays alive for the async upload)
   // and whether that range's planes are stored
-  std::vector<int32_t> rj;
+  std::vector<int32_t> rj, h_ri;   // edge ranks (host copies of the uploaded arrays)
+  std::vector<int32_t> h_plan;     // flattened plan (host copy of the upload)
+  int32_t h_info[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int32_t h_flags[64] = {0};
+  int64_t n_blocks_full = 0;       // task-table length of the full edge range
+  std::vector<int32_t> tasks_r;    // task table of a sharded rank's edge range
+  std::vector<std::vector<int32_t>> tasks_old;  // earlier tables (uploads may be queued)
   bool has_K = false;
   float K4[4] = {0.f, 0.f, 0.f, 0.f};  // fx, fy, cx, cy (calib; read once per call)
   int64_t range_b = -1, range_e = -1, n_blocks = 0;
@@ -1620,15 +1626,18 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
     auto it = g_reg.find(ws);
     if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
     PlanMeta &M = it->second;
-    if (M.range_b != eb || M.range_e != ee) {
+    if (M.range_b != eb || M.range_e != ee) {  // a sharded rank's own edge range
       M.range_b = eb, M.range_e = ee, M.planes_ok = false;
       M.n_blocks = 0;
       if (M3S_TASKS && !(no_tasks && no_tasks[0] == '1') && (int64_t)M.rj.size() >= ee) {
-        build_tasks(M.rj, eb, E_loc, L.chunks, M.tasks);
-        if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), M.tasks.data(), sizeof(int32_t) * M.tasks.size(),
+        // fresh host buffer: an earlier upload from tasks_r may still be queued
+        if (!M.tasks_r.empty()) M.tasks_old.push_back(std::move(M.tasks_r));  // freed at the next prepare
+        M.tasks_r.clear();
+        build_tasks(M.rj, eb, E_loc, L.chunks, M.tasks_r);
+        if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), M.tasks_r.data(), sizeof(int32_t) * M.tasks_r.size(),
                            hipMemcpyHostToDevice, st) != hipSuccess)
           return M3S_ELAUNCH;
-        M.n_blocks = (int64_t)M.tasks.size();
+        M.n_blocks = (int64_t)M.tasks_r.size();
       }
     }
     if (M.n_blocks > 0) {
@@ -1763,38 +1772,43 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
 
 // Per call: zero state, bring ii/jj to the host (the reference's _unique /
 // searchsorted also synchronise), rank them, build and upload the sparse plan.
-int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
-  const Layout Ly = gn_layout(a->N, a->HW, a->E);
-  void *ws = a->workspace;
-  float hK[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // calib intrinsics, read with ii/jj
-  if (a->mode == M3S_MODE_CALIB &&
-      hipMemcpyAsync(hK, a->K, sizeof hK, hipMemcpyDeviceToHost, st) != hipSuccess)
-    return M3S_ELAUNCH;
-  if (hipMemsetAsync(at<int32_t>(ws, Ly.flags), 0, 64 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
-  if (hipMemsetAsync(a->info, 0, 8 * sizeof(int32_t), st) != hipSuccess) return M3S_ELAUNCH;
-  if (a->N > 1 && a->dx_out && hipMemsetAsync(a->dx_out, 0, sizeof(float) * 7 * (a->N - 1), st) != hipSuccess)
-    return M3S_ELAUNCH;
-  const int64_t E = a->E;
-  std::vector<int64_t> hii(E), hjj(E);
-  if (E > 0 && (hipMemcpyAsync(hii.data(), a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(hjj.data(), a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess))
-    return M3S_ELAUNCH;
-  if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
+// Host symbolic plans of recent edge sets (the same factor graph is usually
+// solved many times: every keyframe's local/global optimisation, every bench
+// step). Keyed by (N, HW, E, dense override, remapped ranks).
+struct PlanCacheEntry {
+  int64_t N = 0, HW = 0, E = 0;
+  bool dense = false;
   std::vector<int32_t> ri, rj;
-  const int nu = host_remap(hii.data(), hjj.data(), E, ri, rj);
-  int32_t hinfo[8] = {0, 0, 0, 0, nu, 0, 0, 0};
-  int32_t hflags[2] = {0, 0};
-  const bool bad = nu > a->N;
-  if (bad) hinfo[M3S_INFO_BAD_EDGE] = 1, hflags[kFlagStop] = 1;
   PlanMeta meta;
-  PlanImage img;
-  if (!bad && a->N > 1) {
-    const char *force_dense = std::getenv("M3S_DENSE");
+};
+std::mutex g_cache_mu;
+std::vector<PlanCacheEntry> g_cache;  // most recent first
+constexpr size_t kPlanCacheSize = 4;
+
+void set_lds_attributes_once() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+  });
+}
+
+// Symbolic plan + LDS budget + full-range task table for remapped ranks.
+PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vector<int32_t> &ri,
+                         const std::vector<int32_t> &rj, bool force_dense) {
+  PlanMeta meta;
+  const int64_t E = a->E;
+  if (a->N > 1) {
     SparsePlan P;
     build_sparse_plan((int)a->N, ri, rj, P);
+    PlanImage img;
     flatten_plan(P, img);
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
-    if (fits && !(force_dense && force_dense[0] == '1')) {
+    if (fits && !force_dense) {
       meta.sparse = true;
       meta.m = P.m;
       meta.S = P.S;
@@ -1819,53 +1833,107 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
         meta.lds_bytes = sizeof(double) * (size_t)P.m * 7 + flags_bytes + stage_bytes;
         if (meta.lds_bytes > kMaxLdsBytes) meta.sparse = false;  // dense fallback
       }
+      meta.h_plan = std::move(img.data);
+      img.data.clear();
+      meta.img = img;
     }
   }
-  if (E > 0) {
-    if (hipMemcpyAsync(at<int32_t>(ws, Ly.rank_i), ri.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(at<int32_t>(ws, Ly.rank_j), rj.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice, st) != hipSuccess)
-      return M3S_ELAUNCH;
+  meta.rj = rj;
+  meta.h_ri = ri;
+  // task table of the full edge range (the single-GPU call and world size 1);
+  // a sharded rank's first m3s_gn_linearize builds its own
+  if (M3S_TASKS && E > 0) {
+    build_tasks(meta.rj, 0, E, chunks_for(a->HW, E), meta.tasks);
+    meta.n_blocks_full = (int64_t)meta.tasks.size();
   }
-  if (meta.sparse && !img.data.empty() &&
-      hipMemcpyAsync(at<int32_t>(ws, Ly.plan), img.data.data(), sizeof(int32_t) * img.data.size(),
-                     hipMemcpyHostToDevice, st) != hipSuccess)
+  return meta;
+}
+
+// Per solve call: read ii/jj (+ K) once — the call's only host sync — rank
+// the ids, fetch or build the plan, and enqueue its upload. The host buffers
+// of every upload live in the workspace's registry entry until the next
+// prepare on that workspace (which syncs first), so nothing waits here.
+int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
+  const Layout Ly = gn_layout(a->N, a->HW, a->E);
+  void *ws = a->workspace;
+  float hK[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // calib intrinsics, read with ii/jj
+  if (a->mode == M3S_MODE_CALIB &&
+      hipMemcpyAsync(hK, a->K, sizeof hK, hipMemcpyDeviceToHost, st) != hipSuccess)
     return M3S_ELAUNCH;
-  if (hipMemcpyAsync(a->info, hinfo, sizeof hinfo, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(at<int32_t>(ws, Ly.flags), hflags, sizeof hflags, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)  // host buffers are released below
+  if (a->N > 1 && a->dx_out && hipMemsetAsync(a->dx_out, 0, sizeof(float) * 7 * (a->N - 1), st) != hipSuccess)
     return M3S_ELAUNCH;
-  img.data.clear();
-  meta.img = img;
-  meta.rj = std::move(rj);
+  const int64_t E = a->E;
+  std::vector<int64_t> hii(E), hjj(E);
+  if (E > 0 && (hipMemcpyAsync(hii.data(), a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(hjj.data(), a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess))
+    return M3S_ELAUNCH;
+  if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
+  std::vector<int32_t> ri, rj;
+  const int nu = host_remap(hii.data(), hjj.data(), E, ri, rj);
+  const bool bad = nu > a->N;
+  const char *fd = std::getenv("M3S_DENSE");
+  const bool force_dense = fd && fd[0] == '1';
+  PlanMeta meta;
+  if (!bad) {
+    bool hit = false;
+    {
+      std::lock_guard<std::mutex> g(g_cache_mu);
+      for (size_t q = 0; q < g_cache.size(); q++) {
+        const PlanCacheEntry &C = g_cache[q];
+        if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense && C.ri == ri && C.rj == rj) {
+          meta = C.meta;
+          std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
+          hit = true;
+          break;
+        }
+      }
+    }
+    if (!hit) {
+      meta = build_plan_meta(a, Ly, ri, rj, force_dense);
+      PlanCacheEntry C;
+      C.N = a->N, C.HW = a->HW, C.E = E, C.dense = force_dense, C.ri = ri, C.rj = rj, C.meta = meta;
+      std::lock_guard<std::mutex> g(g_cache_mu);
+      g_cache.insert(g_cache.begin(), std::move(C));
+      if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
+    }
+  } else {
+    meta.h_ri = ri;
+    meta.rj = rj;
+  }
+  for (int q = 0; q < 8; q++) meta.h_info[q] = 0;
+  for (int q = 0; q < 64; q++) meta.h_flags[q] = 0;
+  meta.h_info[M3S_INFO_N_UNIQUE] = nu;
+  if (bad) meta.h_info[M3S_INFO_BAD_EDGE] = 1, meta.h_flags[kFlagStop] = 1;
   if (a->mode == M3S_MODE_CALIB) {  // K row-major: fx = K[0][0], fy = K[1][1], cx = K[0][2], cy = K[1][2]
     meta.has_K = true;
     meta.K4[0] = hK[0], meta.K4[1] = hK[4], meta.K4[2] = hK[2], meta.K4[3] = hK[5];
   }
-  // task table of the full edge range (the single-GPU call and world size 1);
-  // a sharded rank's first m3s_gn_linearize builds its own
-  if (M3S_TASKS && E > 0 && !bad) {
-    const int64_t chunks = chunks_for(a->HW, E);
-    build_tasks(meta.rj, 0, E, chunks, meta.tasks);
-    if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), meta.tasks.data(), sizeof(int32_t) * meta.tasks.size(),
-                       hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return M3S_ELAUNCH;
-    meta.range_b = 0, meta.range_e = E, meta.n_blocks = (int64_t)meta.tasks.size();
+  meta.planes_ok = false;
+  if (meta.n_blocks_full > 0) {
+    meta.range_b = 0, meta.range_e = E, meta.n_blocks = meta.n_blocks_full;
+  } else {
+    meta.range_b = meta.range_e = -1, meta.n_blocks = 0;
   }
-  if (meta.sparse && meta.lds_bytes > 64 * 1024) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<0>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<1>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<2>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-    });
-  }
+  if (meta.sparse && meta.lds_bytes > 64 * 1024) set_lds_attributes_once();
   std::lock_guard<std::mutex> g(g_reg_mu);
-  g_reg[ws] = meta;
-  return M3S_OK;
+  PlanMeta &M = g_reg[ws];
+  M = std::move(meta);
+  bool ok = true;
+  ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.flags), M.h_flags, sizeof M.h_flags, hipMemcpyHostToDevice, st) == hipSuccess;
+  ok &= hipMemcpyAsync(a->info, M.h_info, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (E > 0) {
+    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_i), M.h_ri.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
+                         st) == hipSuccess;
+    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_j), M.rj.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
+                         st) == hipSuccess;
+  }
+  if (M.sparse && !M.h_plan.empty())
+    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.plan), M.h_plan.data(), sizeof(int32_t) * M.h_plan.size(),
+                         hipMemcpyHostToDevice, st) == hipSuccess;
+  if (M.n_blocks > 0)
+    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), M.tasks.data(), sizeof(int32_t) * M.tasks.size(),
+                         hipMemcpyHostToDevice, st) == hipSuccess;
+  return ok ? M3S_OK : M3S_ELAUNCH;
 }
 
 int gn_full(const m3s_gn_args *a, int mode, void *stream) {

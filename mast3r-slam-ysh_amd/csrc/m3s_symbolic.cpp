@@ -6,8 +6,6 @@
 #include <climits>
 #include <cstdint>
 #include <queue>
-#include <set>
-#include <unordered_map>
 
 namespace m3s {
 
@@ -28,35 +26,65 @@ int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int3
 
 namespace {
 
+// Fixed-width bit rows: the variable graphs here have at most a few hundred
+// vertices, so elimination updates are word-wide ORs and degrees popcounts.
+struct BitRows {
+  int n = 0, words = 0;
+  std::vector<uint64_t> w;
+  BitRows(int n_ = 0) : n(n_), words((n_ + 63) / 64), w((size_t)n_ * ((n_ + 63) / 64), 0) {}
+  uint64_t *row(int r) { return w.data() + (size_t)r * words; }
+  const uint64_t *row(int r) const { return w.data() + (size_t)r * words; }
+  void set(int r, int c) { row(r)[c >> 6] |= uint64_t(1) << (c & 63); }
+  void reset(int r, int c) { row(r)[c >> 6] &= ~(uint64_t(1) << (c & 63)); }
+  bool test(int r, int c) const { return (row(r)[c >> 6] >> (c & 63)) & 1; }
+  int count(int r) const {
+    int k = 0;
+    for (int q = 0; q < words; q++) k += __builtin_popcountll(row(r)[q]);
+    return k;
+  }
+  template <typename F>
+  void for_each(int r, F f) const {  // ascending column order
+    const uint64_t *x = row(r);
+    for (int q = 0; q < words; q++)
+      for (uint64_t v = x[q]; v; v &= v - 1) f(q * 64 + __builtin_ctzll(v));
+  }
+};
+
 // Minimum-degree elimination order on the variable graph (ties: lowest
 // index). With `multiple` set, each round eliminates an independent set of
 // minimum-degree (+ slack) variables together (multiple minimum degree): the
 // same kind of fill, but a shallower elimination tree, i.e. fewer dependent
 // steps in the dataflow factorisation.
-std::vector<int32_t> min_degree_order(int m, const std::vector<std::set<int>> &adj0, bool multiple,
-                                      int slack) {
-  std::vector<std::set<int>> adj = adj0;
+std::vector<int32_t> min_degree_order(int m, const BitRows &adj0, bool multiple, int slack) {
+  BitRows adj = adj0;
   std::vector<char> alive(m, 1);
+  std::vector<int> deg(m);
+  for (int v = 0; v < m; v++) deg[v] = adj.count(v);
   std::vector<int32_t> order;
   order.reserve(m);
+  std::vector<int> nb;
   auto eliminate = [&](int v) {
     order.push_back(v);
     alive[v] = 0;
-    const std::set<int> nb = adj[v];
-    for (int a : nb) {
-      adj[a].erase(v);
-      for (int b : nb)
-        if (b != a) adj[a].insert(b);
+    nb.clear();
+    adj.for_each(v, [&](int u) { nb.push_back(u); });
+    const uint64_t *rv = adj.row(v);
+    for (int u : nb) {
+      uint64_t *ru = adj.row(u);
+      for (int q = 0; q < adj.words; q++) ru[q] |= rv[q];
+      adj.reset(u, u);
+      adj.reset(u, v);
+      deg[u] = adj.count(u);
     }
-    adj[v].clear();
+    std::fill(adj.row(v), adj.row(v) + adj.words, 0);
   };
   while ((int)order.size() < m) {
-    size_t dmin = SIZE_MAX;
+    int dmin = INT_MAX;
     for (int v = 0; v < m; v++)
-      if (alive[v] && adj[v].size() < dmin) dmin = adj[v].size();
+      if (alive[v] && deg[v] < dmin) dmin = deg[v];
     if (!multiple) {
       for (int v = 0; v < m; v++)
-        if (alive[v] && adj[v].size() == dmin) {
+        if (alive[v] && deg[v] == dmin) {
           eliminate(v);
           break;
         }
@@ -64,38 +92,58 @@ std::vector<int32_t> min_degree_order(int m, const std::vector<std::set<int>> &a
     }
     std::vector<char> marked(m, 0);
     std::vector<int> sel;
-    for (size_t d = dmin; d <= dmin + (size_t)slack; d++)
+    for (int d = dmin; d <= dmin + slack; d++)
       for (int v = 0; v < m; v++)
-        if (alive[v] && !marked[v] && adj[v].size() == d) {
+        if (alive[v] && !marked[v] && deg[v] == d) {
           sel.push_back(v);
           marked[v] = 1;
-          for (int u : adj[v]) marked[u] = 1;
+          adj.for_each(v, [&](int u) { marked[u] = 1; });
         }
     for (int v : sel) eliminate(v);
   }
   return order;
 }
 
-// elimination-tree height and number of off-diagonal factor blocks of an order
-std::pair<int, int64_t> etree_shape(int m, const std::vector<std::set<int>> &adj0,
-                                    const std::vector<int32_t> &order) {
+// Symbolic factorisation in elimination order: S row k = rows i > k with
+// L_ik != 0 (new numbering), parent = first of them.
+BitRows symbolic_fill(int m, const BitRows &adj, const std::vector<int32_t> &order,
+                      std::vector<int> &parent) {
   std::vector<int32_t> pos(m);
   for (int k = 0; k < m; k++) pos[order[k]] = k;
-  std::vector<std::set<int>> S(m);
+  BitRows S(m);
   for (int v = 0; v < m; v++)
-    for (int u : adj0[v])
-      if (pos[u] > pos[v]) S[pos[v]].insert(pos[u]);
+    adj.for_each(v, [&](int u) {
+      if (pos[u] > pos[v]) S.set(pos[v], pos[u]);
+    });
+  parent.assign(m, -1);
+  for (int k = 0; k < m; k++) {
+    int par = -1;
+    S.for_each(k, [&](int i) {
+      if (par < 0) par = i;
+    });
+    if (par >= 0) {
+      parent[k] = par;
+      uint64_t *rp = S.row(par);
+      const uint64_t *rk = S.row(k);
+      for (int q = 0; q < S.words; q++) rp[q] |= rk[q];
+      S.reset(par, par);
+    }
+  }
+  return S;
+}
+
+// elimination-tree height and number of off-diagonal factor blocks of an order
+std::pair<int, int64_t> etree_shape(int m, const BitRows &adj, const std::vector<int32_t> &order) {
+  std::vector<int> parent;
+  const BitRows S = symbolic_fill(m, adj, order, parent);
   std::vector<int> h(m, 0);
   int64_t nnz = 0;
   int height = m ? 1 : 0;
   for (int k = 0; k < m; k++) {
-    nnz += (int64_t)S[k].size();
-    if (!S[k].empty()) {
-      const int par = *S[k].begin();
-      h[par] = std::max(h[par], h[k] + 1);
-      height = std::max(height, h[par] + 1);
-      for (int i : S[k])
-        if (i != par) S[par].insert(i);
+    nnz += S.count(k);
+    if (parent[k] >= 0) {
+      h[parent[k]] = std::max(h[parent[k]], h[k] + 1);
+      height = std::max(height, h[parent[k]] + 1);
     }
   }
   return {height, nnz};
@@ -184,10 +232,10 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   const int64_t E = (int64_t)ri.size();
   P = SparsePlan();
   P.m = m;
-  std::vector<std::set<int>> adj(m);
+  BitRows adj(m);
   for (int64_t e = 0; e < E; e++) {
     const int a = ri[e] - 1, b = rj[e] - 1;
-    if (a >= 0 && b >= 0 && a != b) adj[a].insert(b), adj[b].insert(a);
+    if (a >= 0 && b >= 0 && a != b) adj.set(a, b), adj.set(b, a);
   }
   {  // the shallowest elimination tree among MD / MMD variants (fill breaks ties)
     std::vector<int32_t> best = min_degree_order(m, adj, false, 0);
@@ -203,35 +251,24 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   for (int k = 0; k < m; k++) P.iperm[P.perm[k]] = k;
 
   // symbolic factorisation in the new order
-  std::vector<std::set<int>> S(m);
-  for (int v = 0; v < m; v++)
-    for (int u : adj[v]) {
-      const int i = P.iperm[v], j = P.iperm[u];
-      if (i > j) S[j].insert(i);
-    }
+  std::vector<int> parent;
+  const BitRows Sb = symbolic_fill(m, adj, P.perm, parent);
   std::vector<std::vector<int>> st(m);
-  std::vector<int> parent(m, -1);
-  for (int k = 0; k < m; k++) {
-    st[k].assign(S[k].begin(), S[k].end());
-    if (!st[k].empty()) {
-      parent[k] = st[k][0];
-      for (size_t q = 1; q < st[k].size(); q++) S[parent[k]].insert(st[k][q]);
-    }
-  }
+  for (int k = 0; k < m; k++) Sb.for_each(k, [&](int i) { st[k].push_back(i); });
   // slots: diagonals 0..m-1, then off-diagonals column by column
-  std::unordered_map<int64_t, int> slot;
+  std::vector<int> slot((size_t)m * m, -1);  // slot of (i, k), i > k
   int next = m;
   P.col_ptr.assign(1, 0);
   for (int k = 0; k < m; k++) {
     for (int i : st[k]) {
       P.col_row.push_back(i);
       P.col_slot.push_back(next);
-      slot[(int64_t)i * m + k] = next++;
+      slot[(size_t)i * m + k] = next++;
     }
     P.col_ptr.push_back((int32_t)P.col_row.size());
   }
   P.S = next;
-  auto sl = [&](int i, int k) { return slot.at((int64_t)i * m + k); };
+  auto sl = [&](int i, int k) { return slot[(size_t)i * m + k]; };
 
   // elimination-tree levels (children before parents)
   std::vector<int> lev(m, 0);
@@ -273,7 +310,7 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
         P.task_col.push_back(k);
         for (int p : rowst[k]) {
           // i in struct(p)?  (struct lists are sorted)
-          if (std::binary_search(st[p].begin(), st[p].end(), i)) {
+          if (Sb.test(p, i)) {
             P.tr_a.push_back(sl(i, p));
             P.tr_b.push_back(sl(k, p));
           }

@@ -246,6 +246,7 @@ def matching_leg(be, synthetic, dev, H, W, reps=20):
 
     m = synthetic.make_match_inputs(H, W, device=dev)
     img, pts, p0 = matching.prep_for_iter_proj(m.X11, m.X21)
+    X11, X21 = m.X11.contiguous(), m.X21.contiguous()
     cfg = matching.MATCHING_CFG
     p1 = be.iter_proj(img, pts, p0, cfg["max_iter"], cfg["lambda_init"], cfg["convergence_thresh"])[0].long()
     times = {}
@@ -253,6 +254,7 @@ def matching_leg(be, synthetic, dev, H, W, reps=20):
         ("iter_proj", lambda: be.iter_proj(img, pts, p0, cfg["max_iter"], cfg["lambda_init"],
                                            cfg["convergence_thresh"])),
         ("refine_matches", lambda: be.refine_matches(m.D11, m.D21, p1, cfg["radius"], cfg["dilation_max"])),
+        ("prep_rays", lambda: be.prep_rays(X11, X21)),
     ):
         fn()
         torch.cuda.synchronize()
@@ -265,7 +267,8 @@ def matching_leg(be, synthetic, dev, H, W, reps=20):
         times[name] = round(e0.elapsed_time(e1) / reps, 4)
     return {"workload": "one %dx%d view pair, F=%d float16 descriptors, matching config of base.yaml"
                         % (H, W, m.D11.shape[-1]),
-            "ms_iter_proj": times["iter_proj"], "ms_refine_matches": times["refine_matches"]}
+            "ms_iter_proj": times["iter_proj"], "ms_refine_matches": times["refine_matches"],
+            "ms_prep_rays": times["prep_rays"]}
 
 
 def cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E):

@@ -3,33 +3,22 @@ kernels), on top of the HIP entry points ``mast3r_slam_backends.iter_proj`` /
 ``refine_matches``.
 
 Same functions, arguments and semantics as
-/root/reference/mast3r_slam/matching.py:1-90 and the ray-image gradient of
-image.py:5-38; the matching configuration is passed explicitly (the
-reference reads ``config["matching"]``; MATCHING_CFG holds its base.yaml:8-14
-values). Torch here is only the glue the reference also uses (normalise,
-3x3 Scharr convolution, gathers); the per-pixel searches run in HIP.
+/root/reference/mast3r_slam/matching.py:1-90; the matching configuration is
+passed explicitly (the reference reads ``config["matching"]``; MATCHING_CFG
+holds its base.yaml:8-14 values). The ray-image prep (normalise + Scharr
+gradient of image.py:5-38 + pack) and both per-pixel searches run in HIP;
+torch is only the glue the reference also uses (index math, the occlusion
+gather).
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 import mast3r_slam_backends as be
 
 # config/base.yaml:8-14
 MATCHING_CFG = dict(max_iter=10, lambda_init=1e-8, convergence_thresh=1e-6, dist_thresh=1e-1,
                     radius=3, dilation_max=5)
-
-
-def img_gradient(img: torch.Tensor):
-    """image.py:5-38: Scharr x/y derivatives (/32) with reflect padding; img [b,c,h,w]."""
-    b, c, h, w = img.shape
-    k = torch.tensor([[-3.0, 0.0, 3.0], [-10.0, 0.0, 10.0], [-3.0, 0.0, 3.0]], device=img.device,
-                     dtype=img.dtype) * (1.0 / 32.0)
-    gx_k = k.repeat(c, 1, 1, 1)
-    gy_k = k.t().contiguous().repeat(c, 1, 1, 1)
-    padded = F.pad(img, (1, 1, 1, 1), mode="reflect")
-    return F.conv2d(padded, gx_k, groups=c), F.conv2d(padded, gy_k, groups=c)
 
 
 def pixel_to_lin(p1, w):
@@ -41,12 +30,11 @@ def lin_to_pixel(idx_1_to_2, w):
 
 
 def prep_for_iter_proj(X11, X21, idx_1_to_2_init=None):
-    """matching.py:25-49: ray image + gradients [b,h,w,9], unit rays [b,hw,3], p_init [b,hw,2]."""
+    """matching.py:25-49: ray image + gradients [b,h,w,9], unit rays [b,hw,3],
+    p_init [b,hw,2]. The normalise + Scharr + pack chain is one HIP pass
+    (mast3r_slam_backends.prep_rays; device tensors only)."""
     b, h, w, _ = X11.shape
-    rays_img = F.normalize(X11, dim=-1).permute(0, 3, 1, 2)
-    gx_img, gy_img = img_gradient(rays_img)
-    rays_with_grad_img = torch.cat((rays_img, gx_img, gy_img), dim=1).permute(0, 2, 3, 1).contiguous()
-    pts3d_norm = F.normalize(X21.reshape(b, -1, 3), dim=-1).contiguous()
+    rays_with_grad_img, pts3d_norm = be.prep_rays(X11.contiguous(), X21.contiguous())
     if idx_1_to_2_init is None:
         idx_1_to_2_init = torch.arange(h * w, device=X11.device)[None, :].repeat(b, 1)
     p_init = lin_to_pixel(idx_1_to_2_init, w).float().contiguous()

@@ -79,6 +79,24 @@ class RefineArgs(ctypes.Structure):
     ]
 
 
+class FuseArgs(ctypes.Structure):
+    """Mirror of ``m3s_fuse_args`` (include/m3s_fuse.h)."""
+
+    _fields_ = [
+        ("X_canon", _VP), ("C", _VP), ("X_new", _VP), ("C_new", _VP), ("T", _VP),
+        ("HW", ctypes.c_int64), ("mode", ctypes.c_int),
+    ]
+
+
+class PrepRaysArgs(ctypes.Structure):
+    """Mirror of ``m3s_prep_rays_args`` (include/m3s_fuse.h)."""
+
+    _fields_ = [
+        ("X11", _VP), ("X21", _VP), ("B", ctypes.c_int64), ("H", ctypes.c_int64),
+        ("W", ctypes.c_int64), ("rays_img", _VP), ("pts_norm", _VP),
+    ]
+
+
 class TrackArgs(ctypes.Structure):
     """Mirror of ``m3s_track_args`` (include/m3s_gn.h)."""
 
@@ -101,7 +119,9 @@ EXPORTS = (
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
+    "m3s_fuse_pointmap", "m3s_prep_rays",
 )
+FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2}
 
 
 def _load():
@@ -131,6 +151,10 @@ def _load():
     lib.m3s_version.argtypes = []
     lib.m3s_sparse_plan_debug.restype = ctypes.c_int64
     lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, _VP, ctypes.c_int64, _VP]
+    lib.m3s_fuse_pointmap.restype = ctypes.c_int
+    lib.m3s_fuse_pointmap.argtypes = [P(FuseArgs), _VP]
+    lib.m3s_prep_rays.restype = ctypes.c_int
+    lib.m3s_prep_rays.argtypes = [P(PrepRaysArgs), _VP]
     lib.m3s_iter_proj.restype = ctypes.c_int
     lib.m3s_iter_proj.argtypes = [P(IterProjArgs), _VP]
     lib.m3s_refine_matches.restype = ctypes.c_int
@@ -365,6 +389,47 @@ def refine_matches(D11, D21, p1, radius, dilation_max):
     a.p1_new = _p(p1_new)
     _raise(_lib.m3s_refine_matches(ctypes.byref(a), _stream(p1.device)), "m3s_refine_matches")
     return [p1_new]
+
+
+def fuse_pointmap(X_canon, C, X_new, C_new, T=None, mode="weighted_pointmap"):
+    """Keyframe pointmap fusion after tracking, in place (new entry point):
+    X_canon/C <- filter(X_canon, C, T.act(X_new), C_new) — tracker.py:98-99 +
+    Frame.update_pointmap (frame.py:41-100) for an initialised keyframe.
+    X_canon, X_new [HW,3] f32; C, C_new [HW,1] (or [HW]) f32; T [8] or [1,8]."""
+    _check(X_canon, "X_canon", torch.float32)
+    _check(C, "C", torch.float32)
+    _check(X_new, "X_new", torch.float32)
+    _check(C_new, "C_new", torch.float32)
+    if mode not in FILTER_MODES:
+        raise RuntimeError(f"fuse_pointmap: unsupported filtering mode {mode!r}")
+    HW = int(X_canon.shape[0])
+    if X_canon.numel() != 3 * HW or X_new.numel() != 3 * HW or C.numel() != HW or C_new.numel() != HW:
+        raise RuntimeError("fuse_pointmap: expected X [HW,3] and C [HW,1]")
+    if T is not None:
+        T = T.contiguous()
+        _check(T, "T", torch.float32)
+    a = FuseArgs()
+    a.X_canon, a.C, a.X_new, a.C_new, a.T = _p(X_canon), _p(C), _p(X_new), _p(C_new), _p(T)
+    a.HW, a.mode = HW, FILTER_MODES[mode]
+    _raise(_lib.m3s_fuse_pointmap(ctypes.byref(a), _stream(X_canon.device)), "m3s_fuse_pointmap")
+
+
+def prep_rays(X11, X21):
+    """iter_proj inputs in one pass (new entry point; prep_for_iter_proj,
+    matching.py:25-49): X11 [B,H,W,3], X21 [B,H,W,3] (or [B,HW,3]) f32 ->
+    (rays_with_grad [B,H,W,9], pts3d_norm [B,HW,3])."""
+    _check(X11, "X11", torch.float32)
+    _check(X21, "X21", torch.float32)
+    B, H, W, _ = X11.shape
+    if X21.numel() != B * H * W * 3:
+        raise RuntimeError("prep_rays: X21 must hold B*H*W points")
+    dev = X11.device
+    rays = torch.empty(B, H, W, 9, dtype=torch.float32, device=dev)
+    pts = torch.empty(B, H * W, 3, dtype=torch.float32, device=dev)
+    a = PrepRaysArgs()
+    a.X11, a.X21, a.B, a.H, a.W, a.rays_img, a.pts_norm = _p(X11), _p(X21), B, H, W, _p(rays), _p(pts)
+    _raise(_lib.m3s_prep_rays(ctypes.byref(a), _stream(dev)), "m3s_prep_rays")
+    return rays, pts
 
 
 # ------------------------------------------------------------ tracker ---

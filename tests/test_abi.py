@@ -16,7 +16,7 @@ import torch
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 HEADER = os.path.join(ROOT, "include", "m3s_gn.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "m3s_match.h")]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "m3s_match.h"), os.path.join(ROOT, "include", "m3s_fuse.h")]
 
 
 @pytest.fixture(scope="module")
@@ -53,6 +53,7 @@ PROBE = r"""
 #include <stddef.h>
 #include "m3s_gn.h"
 #include "m3s_match.h"
+#include "m3s_fuse.h"
 #define F(T, m) printf(#T "." #m " %zu\n", offsetof(T, m))
 int main(void) {
   printf("m3s_gn_args.size %zu\n", sizeof(m3s_gn_args));
@@ -71,6 +72,10 @@ int main(void) {
   printf("m3s_refine_args.size %zu\n", sizeof(m3s_refine_args));
   F(m3s_refine_args, p1); F(m3s_refine_args, F); F(m3s_refine_args, dtype);
   F(m3s_refine_args, radius); F(m3s_refine_args, dilation_max); F(m3s_refine_args, p1_new);
+  printf("m3s_fuse_args.size %zu\n", sizeof(m3s_fuse_args));
+  F(m3s_fuse_args, T); F(m3s_fuse_args, HW); F(m3s_fuse_args, mode);
+  printf("m3s_prep_rays_args.size %zu\n", sizeof(m3s_prep_rays_args));
+  F(m3s_prep_rays_args, B); F(m3s_prep_rays_args, W); F(m3s_prep_rays_args, pts_norm);
   return 0;
 }
 """
@@ -84,7 +89,8 @@ def test_ctypes_struct_layout_matches_header(be, tmp_path):
     out = subprocess.check_output([str(exe)]).decode().split("\n")
     got = dict(l.split() for l in out if l.strip())
     mirror = {"m3s_gn_args": be.GnArgs, "m3s_track_args": be.TrackArgs,
-              "m3s_iter_proj_args": be.IterProjArgs, "m3s_refine_args": be.RefineArgs}
+              "m3s_iter_proj_args": be.IterProjArgs, "m3s_refine_args": be.RefineArgs,
+              "m3s_fuse_args": be.FuseArgs, "m3s_prep_rays_args": be.PrepRaysArgs}
     for key, val in got.items():
         t, m = key.split(".")
         cls = mirror[t]

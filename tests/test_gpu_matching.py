@@ -13,6 +13,7 @@ import torch
 
 import mast3r_slam_backends as be
 from mast3r_slam_amd import matching, synthetic
+from oracle import fusion_oracle as fo
 from oracle import matching_oracle as mo
 
 pytestmark = pytest.mark.gpu
@@ -20,9 +21,12 @@ DEV = torch.device("cuda:0")
 
 
 def _inputs(H=48, W=64, seed=1005):
+    """CPU inputs built with the reference's torch expressions (oracle)."""
     m = synthetic.make_match_inputs(H, W, seed=seed)
-    img, pts, p0 = matching.prep_for_iter_proj(m.X11, m.X21)
-    return m, img, pts, p0
+    img, pts = fo.prep_rays(m.X11.numpy(), m.X21.numpy())
+    ar = torch.arange(H * W)
+    p0 = torch.stack((ar % W, ar // W), -1)[None].float().contiguous()
+    return m, torch.from_numpy(img), torch.from_numpy(pts), p0
 
 
 @pytest.mark.parametrize("H,W,max_iter", [(48, 64, 10), (37, 53, 3), (3, 3, 10)])

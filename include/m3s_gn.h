@@ -149,11 +149,14 @@ int m3s_track_calib_sim3(const m3s_track_args *a, void *stream);
 const char *m3s_version(void);
 
 /* Diagnostic: the host symbolic plan of the block-sparse LLT for N poses and
- * edge ranks (ri, rj) (pose rank 0 fixed). Writes the flattened int32 plan to
- * out (if cap suffices) and meta[0..25] = {m, S, levels, 23 section offsets in
- * the order of m3s_symbolic.h}. Returns the plan length in int32 words. */
-int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj,
-                              int32_t *out, int64_t cap, int32_t *meta);
+ * edge ranks (ri, rj) (pose rank 0 fixed); split > 0 cuts update lists longer
+ * than split into PART items (at most max_parts, widening split to fit), as
+ * the solver does for factors that live in global memory. Writes the
+ * flattened int32 plan to out (if cap suffices) and meta[0..31] = {m, S,
+ * levels, 28 section offsets in the order of m3s_symbolic.h, n_parts}.
+ * Returns the plan length in int32 words. */
+int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t split,
+                              int32_t max_parts, int32_t *out, int64_t cap, int32_t *meta);
 
 /* Diagnostic: byte offsets of the workspace sections for (N, HW, E), in the
  * order flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk,

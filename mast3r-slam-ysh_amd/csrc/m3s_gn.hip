@@ -83,7 +83,7 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 }
 
 struct Layout {
-  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, tasks,
+  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts, tasks,
       planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
@@ -126,6 +126,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 49 * (size_t)(m + 1), 256);
   L.rhs = off;
   off = align_up(off + sizeof(double) * 7 * (size_t)(m + 1), 256);
+  L.parts = off;  // split update partials, at most slot_cap of them
+  off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
   // target-side planes of every edge (5 planes = rays, the widest mode)
@@ -895,6 +897,8 @@ struct SparseDev {
   int plan_len;
   int off[kPlanSections];  // section offsets, order of m3s_symbolic.h
   int m, S, levels, n_items;
+  int n_tasks, n_parts;  // OFF tasks; PART items (0: no split updates)
+  double *parts;         // [n_parts][56] partial update blocks (+ partial RHS)
   int64_t *dbg;  // M3S_LLT_TIMING: per-column DIAG completion stamps
   double *L;     // [S][49] (global variant)
   double *Dinv;  // [m][49] (global variant)
@@ -963,6 +967,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 // entry of up to kStage blocks at once (one memory latency per batch), the
 // wave parks them in its LDS stage area and the products run from LDS.
 constexpr int kStage = 8;                  // updates per staged batch
+constexpr int kSplitUpdates = 8;           // updates per PART item (global factors)
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 
 // v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
@@ -1099,14 +1104,19 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
                 *task_col = pl + D.off[11], *task_tr_ptr = pl + D.off[12], *tr_a = pl + D.off[13],
                 *tr_b = pl + D.off[14], *asm_ptr = pl + D.off[15], *asm_edge = pl + D.off[16],
                 *g_ptr = pl + D.off[17], *g_edge = pl + D.off[18], *wave_ptr = pl + D.off[21],
-                *witems = pl + D.off[22];
+                *witems = pl + D.off[22], *part_q0 = pl + D.off[23], *part_q1 = pl + D.off[24],
+                *part_tgt = pl + D.off[25], *dpart_ptr = pl + D.off[26], *opart_ptr = pl + D.off[27];
+  const int n_tasks = D.n_tasks;
+  const bool split = D.n_parts > 0;
   // completion flags: sdone[slot] (factor block final; diagonal slot k also
   // means W_k final), ydone[k] (forward value y_k final), done2[k] (x_k final)
   int32_t *sdone = after_y + (STORE == 1 ? ((D.plan_len + 1) & ~1) : 0);
   int32_t *ydone = sdone + S;
   int32_t *done2 = ydone + m;
-  double *stg = reinterpret_cast<double *>(sdone + ((S + 2 * m + 1) & ~1)) + (size_t)wave * kStageDoubles;
-  for (int q = tid; q < S + 2 * m; q += 1024) sdone[q] = 0;
+  int32_t *pdone = done2 + m;  // PART items
+  const int n_flags = S + 2 * m + D.n_parts;
+  double *stg = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1)) + (size_t)wave * kStageDoubles;
+  for (int q = tid; q < n_flags; q += 1024) sdone[q] = 0;
   __syncthreads();  // plan copy complete
   const int r = lane / 7, c = lane % 7;
   const bool act49 = lane < 49;
@@ -1132,40 +1142,47 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   M3S_TS(1)
 
   // 1. factorisation + forward substitution as a dataflow over work items:
-  // DIAG(k) (diagonal block and W_k = L_kk^-1, then the forward step of y_k)
-  // and OFF(i,k) (one off-diagonal block). The host list-schedules the items
-  // onto the 16 waves (m3s_symbolic.cpp, schedule_items); each item waits on
-  // LDS completion flags of exactly the blocks it reads and publishes its
-  // own. No workgroup barriers inside the factorisation; the schedule's
-  // assignment order guarantees progress.
-#if M3S_LLT_CYC
-  uint64_t cyc_wait = 0, cyc_trip = 0;
-  const uint64_t cyc_start = __builtin_amdgcn_s_memtime();
-#define M3S_WAIT(f)                                   \
-  {                                                   \
-    const uint64_t w0_ = __builtin_amdgcn_s_memtime(); \
-    wait_flag(f, &fail_s);                            \
-    cyc_wait += __builtin_amdgcn_s_memtime() - w0_;   \
-  }
-#else
-#define M3S_WAIT(f) wait_flag(f, &fail_s);
-#endif
+  // DIAG(k) (diagonal block and W_k = L_kk^-1, then the forward step of y_k),
+  // OFF(i,k) (one off-diagonal block) and, for global factors, PART items
+  // (the head of a long update list, summed early into a partial block). The
+  // host list-schedules the items onto the 16 waves (m3s_symbolic.cpp,
+  // schedule_items); each item waits on LDS completion flags of exactly the
+  // blocks it reads and publishes its own. No workgroup barriers inside the
+  // factorisation; the schedule's assignment order guarantees progress.
   for (int it = wave_ptr[wave]; it < wave_ptr[wave + 1]; it++) {
     const int item = witems[it];
-    if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
+    if (item >= n_tasks) {  // PART: partial sum of the head of a long update list
+      const int pi = item - n_tasks, tg = part_tgt[pi];
+      const int q0 = part_q0[pi], q1 = part_q1[pi];
+      double v, bp = 0.0;
+      if (tg < 0) {  // of DIAG(k): sum L_kp L_kp^T and sum L_kp y_p
+        for (int q = q0; q < q1; q++) {
+          wait_flag(&sdone[dtr_slot[q]], &fail_s);
+          wait_flag(&ydone[dtr_p[q]], &fail_s);
+        }
+        v = sub_products<STAGE, true>(0.0, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+        bp = sub_matvec<STAGE, false>(0.0, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+      } else {  // of OFF(t): sum L_ip L_kp^T
+        for (int q = q0; q < q1; q++) {
+          wait_flag(&sdone[tr_a[q]], &fail_s);
+          wait_flag(&sdone[tr_b[q]], &fail_s);
+        }
+        v = sub_products<STAGE, false>(0.0, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+      }
+      double *pb = D.parts + (size_t)pi * 56;
+      if (act49) pb[lane] = v;
+      if (lane < 7) pb[49 + lane] = bp;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&pdone[pi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
       const int k = -1 - item;
-      const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
-      for (int q = q0; q < q1; q++) M3S_WAIT(&sdone[dtr_slot[q]]);
-#if M3S_LLT_CYC
-      const uint64_t t0_ = __builtin_amdgcn_s_memtime();
-#endif
+      const int p0 = split ? dpart_ptr[k] : 0, p1 = split ? dpart_ptr[k + 1] : 0;
+      const int q0 = (p1 > p0) ? part_q1[p1 - 1] : dtr_ptr[k], q1 = dtr_ptr[k + 1];
+      for (int pi = p0; pi < p1; pi++) wait_flag(&pdone[pi], &fail_s);
+      for (int q = q0; q < q1; q++) wait_flag(&sdone[dtr_slot[q]], &fail_s);
       double v = Lb[(size_t)k * 49 + lane49];
+      for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
-#if M3S_LLT_CYC
-      if (act49) scr[lane] = v;
-      wave_lds_fence();
-      cyc_trip += __builtin_amdgcn_s_memtime() - t0_;
-#endif
       // entry layout -> row layout through the wave's scratch
       if (act49) scr[lane] = v;
       wave_lds_fence();
@@ -1214,13 +1231,11 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if M3S_LLT_CYC
-      if (lane == 0) D.dbg[64 + k] = (int64_t)(__builtin_amdgcn_s_memtime() - t0_) | ((int64_t)(q1 - q0) << 40);
-#endif
       // forward step, off the factorisation's critical path:
       // y_k = L_kk^-1 (b_k - sum_p L_kp y_p)
-      for (int q = q0; q < q1; q++) M3S_WAIT(&ydone[dtr_p[q]]);
+      for (int q = q0; q < q1; q++) wait_flag(&ydone[dtr_p[q]], &fail_s);
       double bb = y[k * 7 + lane7];
+      for (int pi = p0; pi < p1; pi++) bb += D.parts[(size_t)pi * 56 + 49 + lane7];
       bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
       double yk[7];
 #pragma unroll
@@ -1241,19 +1256,14 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
       const int t2 = item;
       const int dst = task_dst[t2], k = task_col[t2];
-      const int q0 = task_tr_ptr[t2], q1 = task_tr_ptr[t2 + 1];
-      M3S_WAIT(&sdone[k]);  // W_k and (through DIAG(k)) every L_kp
-      for (int q = q0; q < q1; q++) M3S_WAIT(&sdone[tr_a[q]]);
-#if M3S_LLT_CYC
-      const uint64_t t0_ = __builtin_amdgcn_s_memtime();
-#endif
+      const int p0 = split ? opart_ptr[t2] : 0, p1 = split ? opart_ptr[t2 + 1] : 0;
+      const int q0 = (p1 > p0) ? part_q1[p1 - 1] : task_tr_ptr[t2], q1 = task_tr_ptr[t2 + 1];
+      wait_flag(&sdone[k], &fail_s);  // W_k and (through DIAG(k)) every L_kp
+      for (int pi = p0; pi < p1; pi++) wait_flag(&pdone[pi], &fail_s);
+      for (int q = q0; q < q1; q++) wait_flag(&sdone[tr_a[q]], &fail_s);
       double v = Lb[(size_t)dst * 49 + lane49];
+      for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
-#if M3S_LLT_CYC
-      if (act49) scr[lane] = v;
-      wave_lds_fence();
-      cyc_trip += __builtin_amdgcn_s_memtime() - t0_;
-#endif
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -1263,18 +1273,8 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       wave_lds_fence();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if M3S_LLT_CYC
-      if (lane == 0) D.dbg[64 + dst] = (int64_t)(__builtin_amdgcn_s_memtime() - t0_) | ((int64_t)(q1 - q0) << 40);
-#endif
     }
   }
-#if M3S_LLT_CYC
-  if (lane == 0) {
-    D.dbg[3 * wave + 0] = (int64_t)(__builtin_amdgcn_s_memtime() - cyc_start);
-    D.dbg[3 * wave + 1] = (int64_t)cyc_wait;
-    D.dbg[3 * wave + 2] = (int64_t)cyc_trip;
-  }
-#endif
   __syncthreads();
 
   if (fail_s) {
@@ -1539,7 +1539,7 @@ struct PlanMeta {
   bool sparse = false;
   int store = 0;  // sparse_llt_kernel<STORE>
   size_t lds_bytes = 0;
-  int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0;
+  int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0;
   PlanImage img;  // offsets (data vector cleared after upload)
   // linearize state of this solve call: edge ranks, the task table of the
   // edge range last linearized (host copy stays alive for the async upload)
@@ -1692,9 +1692,13 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         I.off_lev_col,  I.off_dtr_ptr,      I.off_dtr_slot, I.off_dtr_p,    I.off_task_lev_ptr,
         I.off_task_dst, I.off_task_col,     I.off_task_tr_ptr, I.off_tr_a,  I.off_tr_b,
         I.off_asm_ptr,  I.off_asm_edge,     I.off_g_ptr,    I.off_g_edge,   I.off_ctask_ptr,
-        I.off_items,    I.off_wave_ptr,     I.off_witems};
+        I.off_items,    I.off_wave_ptr,     I.off_witems,
+        I.off_part_q0,  I.off_part_q1,      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr};
     for (int q = 0; q < kPlanSections; q++) D.off[q] = (int)offs[q];
     D.n_items = meta.n_items;
+    D.n_tasks = meta.n_tasks;
+    D.n_parts = meta.n_parts;
+    D.parts = at<double>(ws, Ly.parts);
     D.dbg = at<int64_t>(ws, Ly.A);
     D.m = meta.m;
     D.S = meta.S;
@@ -1804,7 +1808,11 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
   const int64_t E = a->E;
   if (a->N > 1) {
     SparsePlan P;
+    // split long update lists only when the factor lives in global memory
+    // (its products are the slow, staged ones there)
     build_sparse_plan((int)a->N, ri, rj, P);
+    if (sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) > kMaxLdsBytes)
+      build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1);
     PlanImage img;
     flatten_plan(P, img);
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
@@ -1815,10 +1823,13 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       meta.levels = P.levels;
       meta.plan_len = (int)img.data.size();
       meta.n_items = (int)P.items.size();
+      meta.n_tasks = (int)P.task_dst.size();
+      meta.n_parts = (int)P.part_q0.size();
       // LDS plan of sparse_llt_kernel<STORE>: flags always, factor + W + y if
       // they fit, the plan too if it fits as well; else global factor with
       // per-wave stage areas
-      const size_t flags_bytes = sizeof(int32_t) * (((size_t)(P.S + 2 * P.m) + 1) & ~size_t(1));
+      const size_t flags_bytes =
+          sizeof(int32_t) * (((size_t)(P.S + 2 * P.m + P.part_q0.size()) + 1) & ~size_t(1));
       const size_t fac_bytes = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7);
       const size_t plan_bytes = sizeof(int32_t) * ((img.data.size() + 1) & ~size_t(1));
       const size_t stage_bytes = sizeof(double) * 16 * (size_t)kStageDoubles;
@@ -2161,11 +2172,11 @@ int m3s_track_calib_sim3(const m3s_track_args *a, void *stream) { return track_i
 
 const char *m3s_version(void) { return "m3s-gn 0.2 gfx950"; }
 
-int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj,
-                              int32_t *out, int64_t cap, int32_t *meta) {
+int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t split,
+                              int32_t max_parts, int32_t *out, int64_t cap, int32_t *meta) {
   std::vector<int32_t> a(ri, ri + E), b(rj, rj + E);
   SparsePlan P;
-  build_sparse_plan(N, a, b, P);
+  build_sparse_plan(N, a, b, P, split, max_parts);
   PlanImage I;
   flatten_plan(P, I);
   const int64_t offs[kPlanSections] = {
@@ -2173,10 +2184,12 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
       I.off_lev_col,  I.off_dtr_ptr,  I.off_dtr_slot,    I.off_dtr_p,    I.off_task_lev_ptr,
       I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a,     I.off_tr_b,
       I.off_asm_ptr,  I.off_asm_edge, I.off_g_ptr,       I.off_g_edge,   I.off_ctask_ptr,
-      I.off_items,    I.off_wave_ptr, I.off_witems};
+      I.off_items,    I.off_wave_ptr, I.off_witems,    I.off_part_q0,  I.off_part_q1,
+      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr};
   if (meta) {
     meta[0] = P.m, meta[1] = P.S, meta[2] = P.levels;
     for (int k = 0; k < kPlanSections; k++) meta[3 + k] = (int32_t)offs[k];
+    meta[3 + kPlanSections] = (int32_t)P.part_q0.size();
   }
   const int64_t n = (int64_t)I.data.size();
   if (out && cap >= n) std::copy(I.data.begin(), I.data.end(), out);

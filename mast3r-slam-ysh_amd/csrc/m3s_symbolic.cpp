@@ -162,24 +162,48 @@ std::pair<int, int64_t> etree_shape(int m, const BitRows &adj, const std::vector
 static void schedule_items(SparsePlan &P) {
   const int n = (int)P.items.size();
   const int T = (int)P.task_dst.size();
-  std::vector<int> item_of_slot(P.S, -1);
+  std::vector<int> item_of_slot(P.S, -1), item_of_part(P.part_q0.size(), -1);
   for (int it = 0; it < n; it++) {
     const int v = P.items[it];
-    item_of_slot[v < 0 ? -1 - v : P.task_dst[v]] = it;
+    if (v >= T) item_of_part[v - T] = it;
+    else item_of_slot[v < 0 ? -1 - v : P.task_dst[v]] = it;
   }
   std::vector<std::vector<int>> deps(n), succ(n);
   std::vector<double> cost(n);
+  const bool split = !P.dpart_ptr.empty();
   for (int it = 0; it < n; it++) {
     const int v = P.items[it];
     std::vector<int> &d = deps[it];
-    if (v < 0) {
+    if (v >= T) {  // PART: the blocks of its update range (+ y_p for DIAG targets)
+      const int pi = v - T, tg = P.part_tgt[pi];
+      for (int q = P.part_q0[pi]; q < P.part_q1[pi]; q++) {
+        if (tg < 0) {
+          d.push_back(item_of_slot[P.dtr_slot[q]]);
+          d.push_back(item_of_slot[P.dtr_p[q]]);
+        } else {
+          d.push_back(item_of_slot[P.tr_a[q]]);
+          d.push_back(item_of_slot[P.tr_b[q]]);
+        }
+      }
+      cost[it] = 300.0 * (P.part_q1[pi] - P.part_q0[pi]);
+    } else if (v < 0) {
       const int k = -1 - v;
-      for (int q = P.dtr_ptr[k]; q < P.dtr_ptr[k + 1]; q++) d.push_back(item_of_slot[P.dtr_slot[q]]);
-      cost[it] = 3000.0 + 300.0 * (P.dtr_ptr[k + 1] - P.dtr_ptr[k]);
+      int q0 = P.dtr_ptr[k];
+      if (split) {
+        for (int pi = P.dpart_ptr[k]; pi < P.dpart_ptr[k + 1]; pi++) d.push_back(item_of_part[pi]), q0 = P.part_q1[pi];
+      }
+      for (int q = q0; q < P.dtr_ptr[k + 1]; q++) d.push_back(item_of_slot[P.dtr_slot[q]]);
+      cost[it] = 3000.0 + 300.0 * (P.dtr_ptr[k + 1] - q0) +
+                 (split ? 150.0 * (P.dpart_ptr[k + 1] - P.dpart_ptr[k]) : 0.0);
     } else {
       d.push_back(item_of_slot[P.task_col[v]]);
-      for (int q = P.task_tr_ptr[v]; q < P.task_tr_ptr[v + 1]; q++) d.push_back(item_of_slot[P.tr_a[q]]);
-      cost[it] = 800.0 + 300.0 * (P.task_tr_ptr[v + 1] - P.task_tr_ptr[v]);
+      int q0 = P.task_tr_ptr[v];
+      if (split) {
+        for (int pi = P.opart_ptr[v]; pi < P.opart_ptr[v + 1]; pi++) d.push_back(item_of_part[pi]), q0 = P.part_q1[pi];
+      }
+      for (int q = q0; q < P.task_tr_ptr[v + 1]; q++) d.push_back(item_of_slot[P.tr_a[q]]);
+      cost[it] = 800.0 + 300.0 * (P.task_tr_ptr[v + 1] - q0) +
+                 (split ? 150.0 * (P.opart_ptr[v + 1] - P.opart_ptr[v]) : 0.0);
     }
     std::sort(d.begin(), d.end());
     d.erase(std::unique(d.begin(), d.end()), d.end());
@@ -227,7 +251,7 @@ static void schedule_items(SparsePlan &P) {
 }
 
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
-                       SparsePlan &P) {
+                       SparsePlan &P, int split, int64_t max_parts) {
   const int m = N > 1 ? N - 1 : 0;
   const int64_t E = (int64_t)ri.size();
   P = SparsePlan();
@@ -320,6 +344,52 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     }
     P.task_lev_ptr.push_back((int32_t)P.task_dst.size());
   }
+  if (split > 0) {
+    // count parts first; widen the split until they fit the buffer
+    auto n_parts = [&](int sp) {
+      int64_t c = 0;
+      for (int k = 0; k < m; k++) c += std::max(0, (P.dtr_ptr[k + 1] - P.dtr_ptr[k] - 1) / sp);
+      for (size_t t = 0; t < P.task_dst.size(); t++)
+        c += std::max(0, (P.task_tr_ptr[t + 1] - P.task_tr_ptr[t] - 1) / sp);
+      return c;
+    };
+    while (n_parts(split) > max_parts) split *= 2;
+    // items again, column by column: the parts of DIAG(k) and of OFF(., k)
+    // (inputs from earlier columns only) precede DIAG(k)
+    const int T = (int)P.task_dst.size();
+    std::vector<int32_t> items;
+    P.dpart_ptr.assign(m + 1, 0);
+    P.opart_ptr.assign(T + 1, 0);
+    std::vector<std::vector<int32_t>> dparts(m), oparts(T);
+    auto add_parts = [&](int tgt, int q0, int q1, std::vector<int32_t> &out) {
+      const int np = std::max(0, (q1 - q0 - 1) / split);
+      for (int j = 0; j < np; j++) {
+        out.push_back((int32_t)P.part_q0.size());
+        P.part_q0.push_back(q0 + j * split);
+        P.part_q1.push_back(q0 + (j + 1) * split);
+        P.part_tgt.push_back(tgt);
+      }
+    };
+    // part indices are assigned target by target (DIAG targets in column
+    // order, then OFF tasks in task order) so each target's parts are contiguous
+    for (int k = 0; k < m; k++) add_parts(-1 - k, P.dtr_ptr[k], P.dtr_ptr[k + 1], dparts[k]);
+    for (int t = 0; t < T; t++) add_parts(t, P.task_tr_ptr[t], P.task_tr_ptr[t + 1], oparts[t]);
+    for (int k = 0; k < m; k++) P.dpart_ptr[k + 1] = P.dpart_ptr[k] + (int32_t)dparts[k].size();
+    P.opart_ptr[0] = P.dpart_ptr[m];  // OFF parts follow the DIAG parts
+    for (int t = 0; t < T; t++) P.opart_ptr[t + 1] = P.opart_ptr[t] + (int32_t)oparts[t].size();
+    int t = 0;
+    for (int l = 0; l < P.levels; l++)
+      for (int pos = P.lev_ptr[l]; pos < P.lev_ptr[l + 1]; pos++) {
+        const int k = P.lev_col[pos];
+        for (int32_t pi : dparts[k]) items.push_back(T + pi);
+        for (int q = 0; q < (int)st[k].size(); q++)
+          for (int32_t pi : oparts[t + q]) items.push_back(T + pi);
+        items.push_back(-1 - k);
+        for (int q = 0; q < (int)st[k].size(); q++) items.push_back(t + q);
+        t += (int)st[k].size();
+      }
+    P.items.swap(items);
+  }
   schedule_items(P);
   // assembly lists (edge order => deterministic sums)
   std::vector<std::vector<int32_t>> asl(P.S), gl(m);
@@ -374,6 +444,11 @@ void flatten_plan(const SparsePlan &P, PlanImage &img) {
   img.off_items = put(P.items);
   img.off_wave_ptr = put(P.wave_ptr);
   img.off_witems = put(P.witems);
+  img.off_part_q0 = put(P.part_q0);
+  img.off_part_q1 = put(P.part_q1);
+  img.off_part_tgt = put(P.part_tgt);
+  img.off_dpart_ptr = put(P.dpart_ptr);
+  img.off_opart_ptr = put(P.opart_ptr);
 }
 
 }  // namespace m3s

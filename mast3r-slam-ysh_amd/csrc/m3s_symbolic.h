@@ -36,6 +36,14 @@ struct SparsePlan {
   std::vector<int32_t> ctask_ptr;
   // dataflow work items in level order: -1-k = DIAG(k), t >= 0 = off-diagonal task t
   std::vector<int32_t> items;
+  // Split updates (large factors): the head of a long update list runs as
+  // PART items (item code T + part index) that sum up to `split` products into
+  // a partial block as soon as their inputs exist; the DIAG / OFF item then
+  // adds the partials in part order and does only its tail. Part p covers
+  // update entries [part_q0[p], part_q1[p]) of its target (dtr list for
+  // DIAG(k) targets, tr list for OFF(t)); target code -1-k or t.
+  std::vector<int32_t> part_q0, part_q1, part_tgt;
+  std::vector<int32_t> dpart_ptr, opart_ptr;  // parts of DIAG(k) / OFF(t), contiguous
   // the items assigned to the kernel's waves by host list scheduling: wave w
   // runs witems[wave_ptr[w] .. wave_ptr[w+1]) in order
   std::vector<int32_t> wave_ptr, witems;
@@ -46,8 +54,9 @@ int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int3
                std::vector<int32_t> &rj);
 
 // Build the plan for N poses (rank 0 fixed) and edges with ranks (ri, rj).
+// split > 0 enables PART items of `split` updates each (at most max_parts).
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
-                       SparsePlan &P);
+                       SparsePlan &P, int split = 0, int64_t max_parts = 0);
 
 // Flattened int32 image of the plan (offsets of each array into it).
 struct PlanImage {
@@ -55,9 +64,10 @@ struct PlanImage {
   int64_t off_perm, off_col_ptr, off_col_row, off_col_slot, off_lev_ptr, off_lev_col, off_dtr_ptr,
       off_dtr_slot, off_dtr_p, off_task_lev_ptr, off_task_dst, off_task_col, off_task_tr_ptr,
       off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge, off_ctask_ptr,
-      off_items, off_wave_ptr, off_witems;
+      off_items, off_wave_ptr, off_witems, off_part_q0, off_part_q1, off_part_tgt, off_dpart_ptr,
+      off_opart_ptr;
 };
-constexpr int kPlanSections = 23;
+constexpr int kPlanSections = 28;
 constexpr int kLltWaves = 16;  // waves of sparse_llt_kernel (1024 threads)
 void flatten_plan(const SparsePlan &P, PlanImage &img);
 

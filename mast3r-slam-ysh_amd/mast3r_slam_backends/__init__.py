@@ -150,7 +150,8 @@ def _load():
     lib.m3s_version.restype = ctypes.c_char_p
     lib.m3s_version.argtypes = []
     lib.m3s_sparse_plan_debug.restype = ctypes.c_int64
-    lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, _VP, ctypes.c_int64, _VP]
+    lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, ctypes.c_int32, ctypes.c_int32, _VP,
+                                          ctypes.c_int64, _VP]
     lib.m3s_fuse_pointmap.restype = ctypes.c_int
     lib.m3s_fuse_pointmap.argtypes = [P(FuseArgs), _VP]
     lib.m3s_prep_rays.restype = ctypes.c_int
@@ -173,7 +174,8 @@ def version() -> str:
 
 PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col", "dtr_ptr",
                  "dtr_slot", "dtr_p", "task_lev_ptr", "task_dst", "task_col", "task_tr_ptr", "tr_a",
-                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items", "wave_ptr", "witems")
+                 "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items", "wave_ptr", "witems",
+                 "part_q0", "part_q1", "part_tgt", "dpart_ptr", "opart_ptr")
 
 
 LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
@@ -187,29 +189,33 @@ def workspace_layout(N, HW, E):
     return dict(zip(LAYOUT_SECTIONS, list(offs)))
 
 
-def sparse_plan(N, ri, rj):
-    """Host symbolic plan of the block-sparse LLT (diagnostics/tests; CPU only)."""
+def sparse_plan(N, ri, rj, split=0, max_parts=0):
+    """Host symbolic plan of the block-sparse LLT (diagnostics/tests; CPU only).
+    split > 0: long update lists cut into PART items (global-factor solves)."""
     import numpy as np
 
     ri = np.ascontiguousarray(ri, dtype=np.int32)
     rj = np.ascontiguousarray(rj, dtype=np.int32)
-    meta = np.zeros(3 + len(PLAN_SECTIONS), np.int32)
+    meta = np.zeros(4 + len(PLAN_SECTIONS), np.int32)
     P = ctypes.c_void_p
-    n = _lib.m3s_sparse_plan_debug(int(N), ri.size, P(ri.ctypes.data), P(rj.ctypes.data), None, 0,
-                                   P(meta.ctypes.data))
+    args = (int(N), ri.size, P(ri.ctypes.data), P(rj.ctypes.data), int(split), int(max_parts))
+    n = _lib.m3s_sparse_plan_debug(*args, None, 0, P(meta.ctypes.data))
     out = np.zeros(max(n, 1), np.int32)
-    _lib.m3s_sparse_plan_debug(int(N), ri.size, P(ri.ctypes.data), P(rj.ctypes.data),
-                               P(out.ctypes.data), n, P(meta.ctypes.data))
-    offs = list(meta[3:]) + [n]
-    plan = {"m": int(meta[0]), "S": int(meta[1]), "levels": int(meta[2])}
+    _lib.m3s_sparse_plan_debug(*args, P(out.ctypes.data), n, P(meta.ctypes.data))
+    offs = list(meta[3:3 + len(PLAN_SECTIONS)]) + [n]
+    plan = {"m": int(meta[0]), "S": int(meta[1]), "levels": int(meta[2]),
+            "n_parts": int(meta[3 + len(PLAN_SECTIONS)])}
     for k, name in enumerate(PLAN_SECTIONS):
         plan[name] = out[offs[k]:]
-    m, S, L = plan["m"], plan["S"], plan["levels"]
+    m, S, L, NP = plan["m"], plan["S"], plan["levels"], plan["n_parts"]
     T = int(plan["task_lev_ptr"][L])
+    sp = NP > 0 or split > 0
     lens = {"perm": m, "col_ptr": m + 1, "lev_ptr": L + 1, "lev_col": m, "dtr_ptr": m + 1,
             "task_lev_ptr": L + 1, "task_dst": T, "task_col": T, "task_tr_ptr": T + 1,
             "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1,
-            "items": m + T, "wave_ptr": 17, "witems": m + T}
+            "items": m + T + NP, "wave_ptr": 17, "witems": m + T + NP,
+            "part_q0": NP, "part_q1": NP, "part_tgt": NP,
+            "dpart_ptr": m + 1 if sp else 0, "opart_ptr": T + 1 if sp else 0}
     for name, ln in lens.items():
         plan[name] = plan[name][:ln]
     nnz = int(plan["col_ptr"][m])

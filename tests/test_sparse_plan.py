@@ -2,7 +2,7 @@
 solver that replaces Eigen's SimplicialLLT analysis, gn_kernels.cu:132-153).
 
 The plan is executed in numpy the way sparse_llt_kernel runs it (assembly
-lists -> the 16 waves' list-scheduled DIAG(k) / OFF(i,k) items, each waiting
+lists -> the 16 waves' list-scheduled DIAG(k) / OFF(i,k) / PART items, each waiting
 for the blocks it reads -> back substitution in reverse level order); a
 schedule that could deadlock fails the test on random SPD edge blocks, and the solution is compared with
 a dense fp64 solve of the same assembled system.
@@ -53,20 +53,57 @@ def run_plan(p, Hjj, gj):
     sdone = np.zeros(S, bool)
     pos = [p["wave_ptr"][w] for w in range(16)]
 
+    T = len(p["task_dst"])
+    NP = p["n_parts"]
+    split = len(p["dpart_ptr"]) > 0
+    pdone = np.zeros(NP, bool)
+    parts = np.zeros((NP, 7, 7))
+    pb = np.zeros((NP, 7))
+
+    def dparts(k):
+        return range(p["dpart_ptr"][k], p["dpart_ptr"][k + 1]) if split else range(0)
+
+    def oparts(t):
+        return range(p["opart_ptr"][t], p["opart_ptr"][t + 1]) if split else range(0)
+
+    def tail(ps, q0):  # the updates a final item still applies itself
+        return p["part_q1"][ps[-1]] if len(ps) else q0
+
     def ready(item):
+        if item >= T:  # PART
+            pi = item - T
+            q = range(p["part_q0"][pi], p["part_q1"][pi])
+            if p["part_tgt"][pi] < 0:
+                return all(sdone[p["dtr_slot"][j]] for j in q)
+            return all(sdone[p["tr_a"][j]] and sdone[p["tr_b"][j]] for j in q)
         if item < 0:
             k = -1 - item
-            return all(sdone[p["dtr_slot"][q]] for q in range(p["dtr_ptr"][k], p["dtr_ptr"][k + 1]))
+            ps = dparts(k)
+            return all(pdone[i] for i in ps) and all(
+                sdone[p["dtr_slot"][q]] for q in range(tail(ps, p["dtr_ptr"][k]), p["dtr_ptr"][k + 1]))
         k = p["task_col"][item]
-        return sdone[k] and all(sdone[p["tr_a"][q]] and sdone[p["tr_b"][q]]
-                                for q in range(p["task_tr_ptr"][item], p["task_tr_ptr"][item + 1]))
+        ps = oparts(item)
+        return sdone[k] and all(pdone[i] for i in ps) and all(
+            sdone[p["tr_a"][q]] and sdone[p["tr_b"][q]]
+            for q in range(tail(ps, p["task_tr_ptr"][item]), p["task_tr_ptr"][item + 1]))
 
     def run(item):
-        if item < 0:
+        if item >= T:
+            pi = item - T
+            for j in range(p["part_q0"][pi], p["part_q1"][pi]):
+                if p["part_tgt"][pi] < 0:
+                    A = L[p["dtr_slot"][j]]
+                    parts[pi] -= A @ A.T
+                    pb[pi] -= A @ y[p["dtr_p"][j]]
+                else:
+                    parts[pi] -= L[p["tr_a"][j]] @ L[p["tr_b"][j]].T
+            pdone[pi] = True
+        elif item < 0:
             k = -1 - item
-            D = L[k].copy()
-            b = y[k].copy()
-            for q in range(p["dtr_ptr"][k], p["dtr_ptr"][k + 1]):
+            ps = dparts(k)
+            D = L[k] + sum((parts[i] for i in ps), np.zeros((7, 7)))
+            b = y[k] + sum((pb[i] for i in ps), np.zeros(7))
+            for q in range(tail(ps, p["dtr_ptr"][k]), p["dtr_ptr"][k + 1]):
                 A = L[p["dtr_slot"][q]]
                 D -= A @ A.T
                 b -= A @ y[p["dtr_p"][q]]
@@ -77,8 +114,9 @@ def run_plan(p, Hjj, gj):
             sdone[k] = True
         else:
             dst, k = p["task_dst"][item], p["task_col"][item]
-            A = L[dst].copy()
-            for q in range(p["task_tr_ptr"][item], p["task_tr_ptr"][item + 1]):
+            ps = oparts(item)
+            A = L[dst] + sum((parts[i] for i in ps), np.zeros((7, 7)))
+            for q in range(tail(ps, p["task_tr_ptr"][item]), p["task_tr_ptr"][item + 1]):
                 A -= L[p["tr_a"][q]] @ L[p["tr_b"][q]].T
             L[dst] = A @ W[k].T
             sdone[dst] = True
@@ -92,7 +130,7 @@ def run_plan(p, Hjj, gj):
                 progressed = True
         assert progressed, "wave schedule deadlocks"
     assert sorted(p["witems"].tolist()) == sorted(p["items"].tolist())
-    assert sdone.all()
+    assert sdone.all() and pdone.all()
     done = np.zeros(m, bool)
     done[:] = False
     for t in range(m - 1, -1, -1):
@@ -109,8 +147,9 @@ def run_plan(p, Hjj, gj):
     return x.reshape(-1)
 
 
-@pytest.mark.parametrize("N,seed", [(2, 0), (5, 1), (32, 2), (70, 3)])
-def test_plan_executes_to_dense_solution(be, N, seed):
+@pytest.mark.parametrize("N,seed,split", [(2, 0, 0), (5, 1, 0), (32, 2, 0), (70, 3, 0), (32, 4, 2), (70, 5, 3),
+                                          (128, 6, 8)])
+def test_plan_executes_to_dense_solution(be, N, seed, split):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 2, 2, seed=seed, edge_range=(0, 0), kf_ids=np.arange(N) * 3 + 5)
@@ -126,7 +165,9 @@ def test_plan_executes_to_dense_solution(be, N, seed):
         A = rng.standard_normal((7, 7))
         Hjj[e] = A @ A.T + 7 * np.eye(7)
     gj = rng.standard_normal((E, 7))
-    p = be.sparse_plan(N, ri, rj)
+    p = be.sparse_plan(N, ri, rj, split, 4096 if split else 0)
+    if split:
+        assert p["n_parts"] > 0  # the split path is exercised
     assert p["m"] == N - 1
     assert sorted(p["perm"].tolist()) == list(range(N - 1))
     assert p["lev_ptr"][-1] == N - 1

@@ -949,6 +949,43 @@ __device__ __forceinline__ void wait_flag(int32_t *flag, int *fail) {
   }
 }
 
+// Dataflow over an update list [Q0, Q1): lane l polls the completion flag(s)
+// of update q = q_ + l (READY, an expression in q, with acquire loads), the
+// wave takes the ready prefix [qa, qb) and runs BODY on it, then polls the
+// rest. The updates are applied as their inputs arrive, in list order (the
+// sums are the same as waiting for all of them first), and one LDS round trip
+// checks up to 64 flags. Bounded like wait_flag. (A macro: lambdas here leave
+// a private segment behind.)
+__device__ __forceinline__ int ready_prefix(bool ok, int q_, int q1) {
+  const uint64_t nb = ~(uint64_t)__ballot(ok);
+  const int n = nb ? __builtin_ctzll(nb) : 64;
+  return n < q1 - q_ ? n : q1 - q_;
+}
+#define M3S_POLL(Q0, Q1, READY, BODY)                              \
+  {                                                                \
+    int q_ = (Q0), spins_ = 0;                                     \
+    const int q1_ = (Q1);                                          \
+    while (q_ < q1_) {                                             \
+      const int q = q_ + lane;                                     \
+      const int n_ = ready_prefix(q >= q1_ || (READY), q_, q1_);   \
+      if (n_ == 0) {                                               \
+        __builtin_amdgcn_s_sleep(1);                               \
+        if (++spins_ >= (1 << 21)) {                               \
+          fail_s = 1;                                              \
+          break;                                                   \
+        }                                                          \
+        continue;                                                  \
+      }                                                            \
+      const int qa = q_, qb = q_ + n_;                             \
+      BODY;                                                        \
+      q_ = qb;                                                     \
+    }                                                              \
+  }
+
+__device__ __forceinline__ bool flag_set(int32_t *flag) {
+  return __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1130,6 +1167,11 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #else
 #define M3S_TS(i)
 #endif
+#if M3S_LLT_ITEMS  // experiment: per-item (start, inputs ready, published) clock stamps into D.dbg
+#define M3S_IT(j) if (lane == 0) D.dbg[4 * it + (j)] = (int64_t)clock64();
+#else
+#define M3S_IT(j)
+#endif
   double *scr = scratch[wave];
 
   // 0. the assembled factor (assemble_slots_kernel) into LDS, RHS into LDS
@@ -1151,38 +1193,34 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // factorisation; the schedule's assignment order guarantees progress.
   for (int it = wave_ptr[wave]; it < wave_ptr[wave + 1]; it++) {
     const int item = witems[it];
+    M3S_IT(0)
     if (item >= n_tasks) {  // PART: partial sum of the head of a long update list
       const int pi = item - n_tasks, tg = part_tgt[pi];
       const int q0 = part_q0[pi], q1 = part_q1[pi];
       double v, bp = 0.0;
+      v = 0.0;
       if (tg < 0) {  // of DIAG(k): sum L_kp L_kp^T and sum L_kp y_p
-        for (int q = q0; q < q1; q++) {
-          wait_flag(&sdone[dtr_slot[q]], &fail_s);
-          wait_flag(&ydone[dtr_p[q]], &fail_s);
-        }
-        v = sub_products<STAGE, true>(0.0, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
-        bp = sub_matvec<STAGE, false>(0.0, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+        M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
+        M3S_POLL(q0, q1, flag_set(&ydone[dtr_p[q]]), (bp = sub_matvec<STAGE, false>(bp, Lb, dtr_slot, dtr_p, qa, qb, y, lane7, lane49, lane, stg)));
       } else {  // of OFF(t): sum L_ip L_kp^T
-        for (int q = q0; q < q1; q++) {
-          wait_flag(&sdone[tr_a[q]], &fail_s);
-          wait_flag(&sdone[tr_b[q]], &fail_s);
-        }
-        v = sub_products<STAGE, false>(0.0, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+        M3S_POLL(q0, q1, flag_set(&sdone[tr_a[q]]) && flag_set(&sdone[tr_b[q]]), (v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, qa, qb, r7, c7, lane49, lane, stg)));
       }
+      M3S_IT(1)
       double *pb = D.parts + (size_t)pi * 56;
       if (act49) pb[lane] = v;
       if (lane < 7) pb[49 + lane] = bp;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&pdone[pi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_IT(2)
     } else if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
       const int k = -1 - item;
       const int p0 = split ? dpart_ptr[k] : 0, p1 = split ? dpart_ptr[k + 1] : 0;
       const int q0 = (p1 > p0) ? part_q1[p1 - 1] : dtr_ptr[k], q1 = dtr_ptr[k + 1];
       for (int pi = p0; pi < p1; pi++) wait_flag(&pdone[pi], &fail_s);
-      for (int q = q0; q < q1; q++) wait_flag(&sdone[dtr_slot[q]], &fail_s);
       double v = Lb[(size_t)k * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
-      v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+      M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
+      M3S_IT(1)
       // entry layout -> row layout through the wave's scratch
       if (act49) scr[lane] = v;
       wave_lds_fence();
@@ -1231,12 +1269,12 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_IT(3)
       // forward step, off the factorisation's critical path:
       // y_k = L_kk^-1 (b_k - sum_p L_kp y_p)
-      for (int q = q0; q < q1; q++) wait_flag(&ydone[dtr_p[q]], &fail_s);
       double bb = y[k * 7 + lane7];
       for (int pi = p0; pi < p1; pi++) bb += D.parts[(size_t)pi * 56 + 49 + lane7];
-      bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+      M3S_POLL(q0, q1, flag_set(&ydone[dtr_p[q]]), (bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, qa, qb, y, lane7, lane49, lane, stg)));
       double yk[7];
 #pragma unroll
       for (int rr = 0; rr < 7; rr++) {
@@ -1253,17 +1291,20 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&ydone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_IT(2)
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
       const int t2 = item;
       const int dst = task_dst[t2], k = task_col[t2];
       const int p0 = split ? opart_ptr[t2] : 0, p1 = split ? opart_ptr[t2 + 1] : 0;
       const int q0 = (p1 > p0) ? part_q1[p1 - 1] : task_tr_ptr[t2], q1 = task_tr_ptr[t2 + 1];
-      wait_flag(&sdone[k], &fail_s);  // W_k and (through DIAG(k)) every L_kp
+      // the updates first (their inputs L_ip, L_kp are older than DIAG(k)),
+      // so only the W_k product waits for DIAG(k)
       for (int pi = p0; pi < p1; pi++) wait_flag(&pdone[pi], &fail_s);
-      for (int q = q0; q < q1; q++) wait_flag(&sdone[tr_a[q]], &fail_s);
       double v = Lb[(size_t)dst * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
-      v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+      M3S_POLL(q0, q1, flag_set(&sdone[tr_a[q]]) && flag_set(&sdone[tr_b[q]]), (v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, qa, qb, r7, c7, lane49, lane, stg)));
+      wait_flag(&sdone[k], &fail_s);  // W_k
+      M3S_IT(1)
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -1273,6 +1314,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       wave_lds_fence();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_IT(2)
     }
   }
   __syncthreads();

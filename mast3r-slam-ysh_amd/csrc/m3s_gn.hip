@@ -83,14 +83,16 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 }
 
 struct Layout {
-  size_t flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts, tasks,
-      planes, total;
+  size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
+      tasks, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
 
 constexpr int kTile = 64;  // tiled Cholesky tile (large systems)
 inline int64_t aug_ld(int64_t n) { return (n + 1 + kTile - 1) / kTile * kTile; }
+
+inline size_t edge_cnt_bytes(int64_t E) { return (sizeof(uint32_t) * (size_t)(E + 1) + 15) & ~size_t(15); }
 
 inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   Layout L;
@@ -105,6 +107,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
   L.first = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(2 * E + 1), 256);
+  L.edge_cnt = off;  // per-edge chunk arrival counters (fused finalize), zeroed per call
+  off = align_up(off + edge_cnt_bytes(E), 256);
   L.partials = off;
   off = align_up(off + sizeof(float) * kNP * (size_t)max_partials, 256);
   L.edge_sums = off;
@@ -158,6 +162,8 @@ struct LinArgs {
   const int32_t *tasks;    // block -> task (e_loc * chunks + c), -1 = idle; null = identity
   float *planes;           // per-edge target-side planes (PixIn), [E_loc][kPlanes][HW]
   float *partials;         // [task][36]
+  uint32_t *edge_cnt;      // non-null: the last chunk of an edge to finish also finalizes it into fin
+  double *fin;             // [E][kFin] per-edge blocks M L M^T, M g (fused finalize)
   int64_t HW, edge_begin, chunks, chunk_pix;
   ResidualParams P;
 };
@@ -190,6 +196,13 @@ __device__ __forceinline__ PixIn<MODE> gather_pixel(const LinArgs &A, const floa
 // block -> (edge, chunk) through the XCD-grouped task table
 __device__ __forceinline__ int64_t block_task(const LinArgs &A) {
   return A.tasks ? (int64_t)A.tasks[blockIdx.x] : (int64_t)blockIdx.x;
+}
+
+// The block partial is stored write-through (sc1), so the edge's last chunk
+// can read it from another XCD without a release fence (guide §6 G16 R1).
+__device__ __forceinline__ void store_sc1(float *p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Block reduction of the 36 per-thread sums through LDS: every thread stores
@@ -226,7 +239,7 @@ __device__ __forceinline__ void block_reduce_store(const float *acc, float *out)
       float x = 0.0f;
 #pragma unroll
       for (int s = 0; s < S; s++) x += part[t][s];
-      out[pass * kRedW + t] = x;
+      store_sc1(out + pass * kRedW + t, x);
     }
   }
 }
@@ -255,6 +268,41 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 #define M3S_LDS_REDUCE 0
 #endif
 
+// Per edge: H_jj = M L M^T and g_j = M l in fp64 (M = Adj(T_i)^-T), written
+// as fin[0:49] (row-major) and fin[49:56], from the edge's 36 local sums `es`
+// (LDS). Threads 0..63 of the block work; every thread of the block must call
+// it (block barriers).
+constexpr int kFin = 56;
+__device__ __forceinline__ void finalize_edge(const double *es, const float *Ti, double *fin) {
+  __shared__ double M[7][7], Lm[7][7], T1[7][7], l[7];
+  const int t = threadIdx.x;
+  if (t == 0) adjT_inv_matrix(Ti, M);
+  if (t < 49) {
+    const int a = t / 7, c = t % 7;
+    Lm[a][c] = es[kL + tri(a < c ? a : c, a < c ? c : a)];
+  }
+  if (t < 7) l[t] = es[kG + t];
+  __syncthreads();
+  if (t < 49) {
+    const int a = t / 7, c = t % 7;
+    double sm = 0.0;
+    for (int k = 0; k < 7; k++) sm += M[a][k] * Lm[k][c];
+    T1[a][c] = sm;
+  } else if (t < 56) {
+    const int a = t - 49;
+    double sm = 0.0;
+    for (int k = 0; k < 7; k++) sm += M[a][k] * l[k];
+    fin[49 + a] = sm;
+  }
+  __syncthreads();
+  if (t < 49) {
+    const int a = t / 7, c = t % 7;
+    double sm = 0.0;
+    for (int k = 0; k < 7; k++) sm += T1[a][k] * M[c][k];
+    fin[t] = sm;
+  }
+}
+
 // Each lane owns 4 consecutive pixels (one 16-B vector per stream); a wave
 // sweeps 256 pixels per trip, a block 1024.
 // 36 per-thread sums -> one block partial
@@ -275,9 +323,49 @@ __device__ __forceinline__ void store_partial(const float *acc, float *out) {
     float s = 0.0f;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; w++) s += red[w][threadIdx.x];
-    out[threadIdx.x] = s;
+    store_sc1(out + threadIdx.x, s);
   }
 #endif
+}
+
+// Fused finalize (single-GPU solve): after its chunk partial is stored, a
+// block draws a ticket from its edge's counter; the edge's last chunk
+// (ticket = chunks - 1 mod chunks: the counter runs on over a call's GN
+// iterations and is zeroed per call) sums the edge's chunk partials in fp64
+// in chunk order with sc1 loads (the same sums as edge_reduce_kernel /
+// finalize_edges_kernel) and writes fin[e] - the finalize launch disappears.
+__device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64_t e) {
+  __shared__ double esl[kNP];
+  __shared__ int last_s;
+  const int t = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t ch = (uint32_t)A.chunks;
+    const uint32_t old = __hip_atomic_fetch_add(A.edge_cnt + e_loc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = (old % ch) == ch - 1;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no loads above the ticket
+  if (t < kNP) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(A.partials + (size_t)e_loc * A.chunks * kNP + t);
+    double acc = 0.0;
+    int64_t c = 0;
+    for (; c + 8 <= A.chunks; c += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        v[k] = __hip_atomic_load(p + (size_t)(c + k) * kNP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc += (double)__uint_as_float(v[k]);
+    }
+    for (; c < A.chunks; c++)
+      acc += (double)__uint_as_float(__hip_atomic_load(p + (size_t)c * kNP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    esl[t] = acc;
+  }
+  __syncthreads();
+  finalize_edge(esl, A.Twc + 8 * (size_t)A.rank_i[e], A.fin + (size_t)e * kFin);
 }
 
 // WPACK: also store the target-side planes for the packed kernel (first GN
@@ -382,6 +470,7 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
     }
   }
   store_partial(acc, A.partials + (size_t)b * kNP);
+  if (A.edge_cnt) edge_tail(A, e_loc, e);
 }
 
 // Later GN iterations of a solve call: target-side inputs from the planes the
@@ -473,6 +562,7 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
   }
 #endif
   store_partial(acc, A.partials + (size_t)b * kNP);
+  if (A.edge_cnt) edge_tail(A, e_loc, e);
 }
 
 // fp64 sum of each edge's chunk partials (fixed order)
@@ -810,7 +900,6 @@ __global__ void __launch_bounds__(1024) backsolve_kernel(const double *__restric
 // The edge's local sums come from edge_sums, or (single-GPU path) straight
 // from the linearize chunk partials, summed in fp64 in chunk order exactly as
 // edge_reduce_kernel does.
-constexpr int kFin = 56;
 __global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__restrict__ edge_sums,
                                                             const float *__restrict__ partials,
                                                             int64_t chunks,
@@ -821,43 +910,19 @@ __global__ void __launch_bounds__(64) finalize_edges_kernel(const double *__rest
   if (*stop) return;
   const int64_t e = blockIdx.x;
   const int t = threadIdx.x;
-  __shared__ double M[7][7], Lm[7][7], T1[7][7], l[7], esl[kNP];
-  const double *es = edge_sums + (size_t)e * kNP;
-  if (partials) {
-    if (t < kNP) {
-      double acc = 0.0;
+  __shared__ double esl[kNP];
+  if (t < kNP) {
+    double acc = 0.0;
+    if (partials) {
       const float *p = partials + (size_t)e * chunks * kNP + t;
       for (int64_t c = 0; c < chunks; c++) acc += (double)p[(size_t)c * kNP];
-      esl[t] = acc;
+    } else {
+      acc = edge_sums[(size_t)e * kNP + t];
     }
-    __syncthreads();
-    es = esl;
-  }
-  if (t == 0) adjT_inv_matrix(Twc + 8 * (size_t)rank_i[e], M);
-  if (t < 49) {
-    const int a = t / 7, c = t % 7;
-    Lm[a][c] = es[kL + tri(a < c ? a : c, a < c ? c : a)];
-  }
-  if (t < 7) l[t] = es[kG + t];
-  __syncthreads();
-  if (t < 49) {
-    const int a = t / 7, c = t % 7;
-    double s = 0.0;
-    for (int k = 0; k < 7; k++) s += M[a][k] * Lm[k][c];
-    T1[a][c] = s;
-  } else if (t < 56) {
-    const int a = t - 49;
-    double s = 0.0;
-    for (int k = 0; k < 7; k++) s += M[a][k] * l[k];
-    fin[(size_t)e * kFin + 49 + a] = s;
+    esl[t] = acc;
   }
   __syncthreads();
-  if (t < 49) {
-    const int a = t / 7, c = t % 7;
-    double s = 0.0;
-    for (int k = 0; k < 7; k++) s += T1[a][k] * M[c][k];
-    fin[(size_t)e * kFin + t] = s;
-  }
+  finalize_edge(esl, Twc + 8 * (size_t)rank_i[e], fin + (size_t)e * kFin);
 }
 
 // Block-sparse assembly, one 64-thread block per factor slot (then one per
@@ -898,6 +963,7 @@ struct SparseDev {
   int off[kPlanSections];  // section offsets, order of m3s_symbolic.h
   int m, S, levels, n_items;
   int n_tasks, n_parts;  // OFF tasks; PART items (0: no split updates)
+  int E, asm_lds;        // asm_lds: assemble in-kernel from fin staged in LDS (else assemble_slots_kernel)
   double *parts;         // [n_parts][56] partial update blocks (+ partial RHS)
   int64_t *dbg;  // M3S_LLT_TIMING: per-column DIAG completion stamps
   double *L;     // [S][49] (global variant)
@@ -1174,11 +1240,35 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #endif
   double *scr = scratch[wave];
 
-  // 0. the assembled factor (assemble_slots_kernel) into LDS, RHS into LDS
-  if (IN_LDS) {
-    for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
+  // 0. assembly. LDS factor with room: the per-edge blocks (fin) are staged
+  // in LDS with coalesced loads, then summed per slot in edge order (the sums
+  // of assemble_slots_kernel); otherwise that kernel assembled into the global
+  // factor array, copied in here.
+  if (IN_LDS && D.asm_lds) {
+    double *fl = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1));
+    for (int idx = tid; idx < D.E * kFin; idx += 1024) fl[idx] = D.fin[idx];
+    __syncthreads();
+    for (int idx = tid; idx < S * 49; idx += 1024) {
+      const int sl = idx / 49, t = idx - sl * 49;
+      double v = 0.0;
+      for (int q = asm_ptr[sl]; q < asm_ptr[sl + 1]; q++) v += fl[asm_edge[q] * kFin + t];
+      Lb[idx] = (sl < m) ? v : -v;
+    }
+    for (int idx = tid; idx < m * 7; idx += 1024) {
+      const int vv = idx / 7, t = idx - vv * 7;
+      double v = 0.0;
+      for (int q = g_ptr[vv]; q < g_ptr[vv + 1]; q++) {
+        const int ent = g_edge[q];
+        const double gj = fl[(ent >> 1) * kFin + 49 + t];
+        v += (ent & 1) ? gj : -gj;
+      }
+      y[idx] = v;
+    }
+  } else {
+    if (IN_LDS)
+      for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
+    for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
   }
-  for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
   if (tid == 0) fail_s = 0;
   __syncthreads();
   M3S_TS(1)
@@ -1580,6 +1670,7 @@ int read_K(const float *K, ResidualParams &P, hipStream_t st) {
 struct PlanMeta {
   bool sparse = false;
   int store = 0;  // sparse_llt_kernel<STORE>
+  bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
   size_t lds_bytes = 0;
   int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0;
   PlanImage img;  // offsets (data vector cleared after upload)
@@ -1631,7 +1722,7 @@ void build_tasks(const std::vector<int32_t> &rj, int64_t eb, int64_t E_loc, int6
 }
 
 int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb, int64_t ee,
-                      double *edge_sums, hipStream_t st) {
+                      double *edge_sums, hipStream_t st, bool fuse_fin = false) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
   const int64_t E_loc = ee - eb;
@@ -1651,6 +1742,9 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.partials = at<float>(ws, Ly.partials);
   L.planes = at<float>(ws, Ly.planes);
   L.tasks = nullptr;
+  // fused finalize only over the whole edge set (single-GPU solve)
+  L.edge_cnt = (fuse_fin && eb == 0 && ee == a->E) ? at<uint32_t>(ws, Ly.edge_cnt) : nullptr;
+  L.fin = at<double>(ws, Ly.fin);
   L.HW = a->HW;
   L.edge_begin = eb;
   L.chunks = chunks_for(a->HW, E_loc);
@@ -1702,7 +1796,7 @@ constexpr size_t kMaxLdsBytes = 150 * 1024;
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
 int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *partials, int64_t chunks,
-                  hipStream_t st) {
+                  hipStream_t st, bool fin_ready = false) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
   int32_t *flags = at<int32_t>(ws, Ly.flags);
@@ -1720,7 +1814,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
   float *dx = a->dx_out;
   if (meta.sparse) {
     double *fin = at<double>(ws, Ly.fin);
-    if (a->E > 0) {
+    if (a->E > 0 && !fin_ready) {
       finalize_edges_kernel<<<dim3((unsigned)a->E), dim3(64), 0, st>>>(
           edge_sums, edge_sums ? nullptr : partials, chunks, at<int32_t>(ws, Ly.rank_i), a->Twc, fin, stop);
       if ((rc = launch_ok())) return rc;
@@ -1740,6 +1834,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     D.n_items = meta.n_items;
     D.n_tasks = meta.n_tasks;
     D.n_parts = meta.n_parts;
+    D.E = (int)a->E;
+    D.asm_lds = meta.asm_lds ? 1 : 0;
     D.parts = at<double>(ws, Ly.parts);
     D.dbg = at<int64_t>(ws, Ly.A);
     D.m = meta.m;
@@ -1747,10 +1843,12 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     D.levels = meta.levels;
     D.L = at<double>(ws, Ly.Lblk);
     D.rhs = at<double>(ws, Ly.rhs);
-    assemble_slots_kernel<<<dim3((unsigned)(meta.S + meta.m)), dim3(64), 0, st>>>(
-        fin, D.plan, (int)I.off_asm_ptr, (int)I.off_asm_edge, (int)I.off_g_ptr, (int)I.off_g_edge, meta.m,
-        meta.S, D.L, at<double>(ws, Ly.rhs), stop);
-    if ((rc = launch_ok())) return rc;
+    if (!meta.asm_lds) {  // multi-workgroup assembly into the global factor array
+      assemble_slots_kernel<<<dim3((unsigned)(meta.S + meta.m)), dim3(64), 0, st>>>(
+          fin, D.plan, (int)I.off_asm_ptr, (int)I.off_asm_edge, (int)I.off_g_ptr, (int)I.off_g_edge, meta.m,
+          meta.S, D.L, at<double>(ws, Ly.rhs), stop);
+      if ((rc = launch_ok())) return rc;
+    }
     D.Dinv = at<double>(ws, Ly.Dinv);
     D.fin = fin;
     D.Twc = a->Twc;
@@ -1875,13 +1973,19 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       const size_t fac_bytes = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7);
       const size_t plan_bytes = sizeof(int32_t) * ((img.data.size() + 1) & ~size_t(1));
       const size_t stage_bytes = sizeof(double) * 16 * (size_t)kStageDoubles;
+      const size_t fin_bytes = sizeof(double) * kFin * (size_t)E;
       if (fac_bytes + plan_bytes + flags_bytes <= kMaxLdsBytes) {
         meta.store = 1;
         meta.lds_bytes = fac_bytes + plan_bytes + flags_bytes;
       } else if (fac_bytes + flags_bytes <= kMaxLdsBytes) {
         meta.store = 2;
         meta.lds_bytes = fac_bytes + flags_bytes;
-      } else {
+      }
+      if (meta.store != 0 && meta.lds_bytes + fin_bytes <= kMaxLdsBytes) {
+        meta.asm_lds = true;
+        meta.lds_bytes += fin_bytes;
+      }
+      if (meta.store == 0) {
         meta.store = 0;
         meta.lds_bytes = sizeof(double) * (size_t)P.m * 7 + flags_bytes + stage_bytes;
         if (meta.lds_bytes > kMaxLdsBytes) meta.sparse = false;  // dense fallback
@@ -1973,6 +2077,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   M = std::move(meta);
   bool ok = true;
   ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.flags), M.h_flags, sizeof M.h_flags, hipMemcpyHostToDevice, st) == hipSuccess;
+  ok &= hipMemsetAsync(at<uint32_t>(ws, Ly.edge_cnt), 0, edge_cnt_bytes(E), st) == hipSuccess;
   ok &= hipMemcpyAsync(a->info, M.h_info, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
   if (E > 0) {
     ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_i), M.h_ri.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
@@ -2005,9 +2110,15 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   const float *partials = at<float>(a->workspace, Ly.partials);
   const int64_t chunks = chunks_for(a->HW, a->E);
+  bool sparse;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    sparse = g_reg.at(a->workspace).sparse;
+  }
+  // sparse solve: the linearize kernels finalize each edge themselves
   for (int it = 0; it < a->max_iter; it++) {
-    if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st))) return rc;
-    if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st))) return rc;
+    if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse))) return rc;
+    if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st, sparse))) return rc;
   }
   return M3S_OK;
 }

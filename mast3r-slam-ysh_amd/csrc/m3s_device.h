@@ -91,7 +91,20 @@ __device__ __forceinline__ Sim3Mat sim3_matrix(const Sim3f &T) {
   M.t[0] = T.t[0], M.t[1] = T.t[1], M.t[2] = T.t[2];
   return M;
 }
+#ifndef M3S_PK_ACT
+#define M3S_PK_ACT 1
+#endif
 __device__ __forceinline__ void act(const Sim3Mat &M, const float *X, float *Y) {
+#if M3S_PK_ACT
+  // rows 0 and 1 as one float2 chain (v_pk_fma_f32), row 2 scalar
+  typedef float v2 __attribute__((ext_vector_type(2)));
+  v2 y = __builtin_elementwise_fma(v2{M.m[2], M.m[5]}, v2{X[2], X[2]}, v2{M.t[0], M.t[1]});
+  y = __builtin_elementwise_fma(v2{M.m[1], M.m[4]}, v2{X[1], X[1]}, y);
+  y = __builtin_elementwise_fma(v2{M.m[0], M.m[3]}, v2{X[0], X[0]}, y);
+  Y[0] = y.x, Y[1] = y.y;
+  Y[2] = __builtin_fmaf(M.m[6], X[0], __builtin_fmaf(M.m[7], X[1], __builtin_fmaf(M.m[8], X[2], M.t[2])));
+  return;
+#endif
   Y[0] = __builtin_fmaf(M.m[0], X[0], __builtin_fmaf(M.m[1], X[1], __builtin_fmaf(M.m[2], X[2], M.t[0])));
   Y[1] = __builtin_fmaf(M.m[3], X[0], __builtin_fmaf(M.m[4], X[1], __builtin_fmaf(M.m[5], X[2], M.t[1])));
   Y[2] = __builtin_fmaf(M.m[6], X[0], __builtin_fmaf(M.m[7], X[1], __builtin_fmaf(M.m[8], X[2], M.t[2])));
@@ -248,39 +261,179 @@ __device__ __forceinline__ float flog(float x) {
 }
 
 // branch-free: both sides are always computed, then selected
+#ifndef M3S_HUBER_MIN
+#define M3S_HUBER_MIN 1
+#endif
 __device__ __forceinline__ float huber_w(float r, float k) {
+#if M3S_HUBER_MIN
+  // min(1, k/|r|): 1 below the threshold (k/|r| > 1 there), k/|r| above; one
+  // v_min_f32 instead of a compare and a select
+  return fminf(1.0f, k * frcp(fabsf(r)));
+#else
   const float a = fabsf(r);
   const float o = k * frcp(a);
   return a < k ? 1.0f : o;
-}
-
-// ------------------------------------------------ normal-eq accumulation --
-// acc[tri(m,n)] += w a_m a_n over the structurally non-zero entries (MASK),
-// acc[kG+m] += (w e) a_m, acc[kCost] += w e^2.
-template <unsigned MASK>
-__device__ __forceinline__ void accum_row(float *acc, const float (&a)[7], float w, float e) {
-  float wa[7];
-#pragma unroll
-  for (int m = 0; m < 7; m++)
-    if (MASK & (1u << m)) wa[m] = w * a[m];
-#pragma unroll
-  for (int m = 0; m < 7; m++) {
-    if (!(MASK & (1u << m))) continue;
-#pragma unroll
-    for (int n = m; n < 7; n++)
-      if (MASK & (1u << n)) acc[kL + tri(m, n)] += wa[m] * a[n];
-  }
-  const float we = w * e;
-#pragma unroll
-  for (int m = 0; m < 7; m++)
-    if (MASK & (1u << m)) acc[kG + m] += we * a[m];
-  acc[kCost] += we * e;
+#endif
 }
 
 // non-zero patterns of the local Jacobian rows (bits: tau0..2 phi0..2 sigma)
 constexpr unsigned kRayX = 0x37, kRayY = 0x2F, kRayZ = 0x1F, kRayD = 0x47;
 constexpr unsigned kCalU = 0x3D, kCalV = 0x3E, kCalZ = 0x5C;
 constexpr unsigned kPtX = 0x71, kPtY = 0x6A, kPtZ = 0x5C;
+
+// ------------------------------------------ packed-fp32 row accumulation --
+// gfx950 issues v_pk_fma_f32 (two fp32 FMAs per lane) at the rate of one
+// v_fma_f32, so two residual rows with the same number of non-zero Jacobian
+// entries are accumulated as one row of float2: lane .x is row A, lane .y is
+// row B, each into its own sums (the shared L entries of the two rows are
+// added once, at the end of the block, in fold()). The per-pixel products are
+// the reference's (w a_m a_n, w e a_m, w e^2); only the order of the fp32 sums
+// differs (per row, then combined).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__host__ __device__ constexpr int popc7(unsigned m) {
+  int n = 0;
+  for (int c = 0; c < 7; c++) n += (m >> c) & 1u;
+  return n;
+}
+// column of the p-th set bit of m, -1 past the last
+__host__ __device__ constexpr int nth_col(unsigned m, int p) {
+  for (int c = 0; c < 7; c++)
+    if (m & (1u << c)) {
+      if (p == 0) return c;
+      p--;
+    }
+  return -1;
+}
+
+// Two rows A (mask MA) and B (mask MB, popc(MB) <= popc(MA)); a[p] holds the
+// p-th non-zero entry of each (B padded with 0 past its last).
+template <unsigned MA, unsigned MB>
+struct PairAcc {
+  static constexpr int K = popc7(MA);
+  static constexpr int NT = K * (K + 1) / 2;
+  f32x2 h[NT], g[K], c;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int t = 0; t < NT; t++) h[t] = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int p = 0; p < K; p++) g[p] = f32x2{0.0f, 0.0f};
+    c = f32x2{0.0f, 0.0f};
+  }
+  __device__ __forceinline__ void add(const f32x2 (&a)[K], f32x2 w, f32x2 e) {
+    f32x2 wa[K];
+#pragma unroll
+    for (int p = 0; p < K; p++) wa[p] = w * a[p];
+    int t = 0;
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++, t++) h[t] = __builtin_elementwise_fma(wa[p], a[q], h[t]);
+    const f32x2 we = w * e;
+#pragma unroll
+    for (int p = 0; p < K; p++) g[p] = __builtin_elementwise_fma(we, a[p], g[p]);
+    c = __builtin_elementwise_fma(we, e, c);
+  }
+  // rows given as a / f (f per row): w a a^T = (w f^2) a' a'^T, w e a = (w f e) a'
+  __device__ __forceinline__ void add_scaled(const f32x2 (&a)[K], f32x2 w, f32x2 e, f32x2 f) {
+    const f32x2 wf = w * f;
+    const f32x2 wff = wf * f;
+    f32x2 wa[K];
+#pragma unroll
+    for (int p = 0; p < K; p++) wa[p] = wff * a[p];
+    int t = 0;
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++, t++) h[t] = __builtin_elementwise_fma(wa[p], a[q], h[t]);
+    const f32x2 wfe = wf * e;
+#pragma unroll
+    for (int p = 0; p < K; p++) g[p] = __builtin_elementwise_fma(wfe, a[p], g[p]);
+    c = __builtin_elementwise_fma(w * e, e, c);
+  }
+  __device__ __forceinline__ void fold(float *acc) const {
+    int t = 0;
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++, t++) {
+        acc[kL + tri(nth_col(MA, p), nth_col(MA, q))] += h[t].x;
+        if (nth_col(MB, q) >= 0) acc[kL + tri(nth_col(MB, p), nth_col(MB, q))] += h[t].y;
+      }
+#pragma unroll
+    for (int p = 0; p < K; p++) {
+      acc[kG + nth_col(MA, p)] += g[p].x;
+      if (nth_col(MB, p) >= 0) acc[kG + nth_col(MB, p)] += g[p].y;
+    }
+    acc[kCost] += c.x + c.y;
+  }
+};
+
+// One row (mask M), a[p] = its p-th non-zero entry.
+template <unsigned M>
+struct RowAcc {
+  static constexpr int K = popc7(M);
+  static constexpr int NT = K * (K + 1) / 2;
+  float h[NT], g[K], c;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int t = 0; t < NT; t++) h[t] = 0.0f;
+#pragma unroll
+    for (int p = 0; p < K; p++) g[p] = 0.0f;
+    c = 0.0f;
+  }
+  __device__ __forceinline__ void add(const float (&a)[K], float w, float e) {
+    float wa[K];
+#pragma unroll
+    for (int p = 0; p < K; p++) wa[p] = w * a[p];
+    int t = 0;
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++, t++) h[t] = __builtin_fmaf(wa[p], a[q], h[t]);
+    const float we = w * e;
+#pragma unroll
+    for (int p = 0; p < K; p++) g[p] = __builtin_fmaf(we, a[p], g[p]);
+    c = __builtin_fmaf(we, e, c);
+  }
+  __device__ __forceinline__ void fold(float *acc) const {
+    int t = 0;
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++, t++) acc[kL + tri(nth_col(M, p), nth_col(M, q))] += h[t];
+#pragma unroll
+    for (int p = 0; p < K; p++) acc[kG + nth_col(M, p)] += g[p];
+    acc[kCost] += c;
+  }
+};
+
+// Per-lane accumulators of one residual model: rays pairs (x, y) and
+// (z, dist); calib pairs (u, v) plus the log-depth row; points pairs (x, y)
+// plus z. fold() adds them into the 36-float layout (kL / kG / kCost).
+template <int MODE>
+struct Accum;
+template <>
+struct Accum<1> {
+  PairAcc<kRayX, kRayY> xy;
+  PairAcc<kRayZ, kRayD> zd;
+  __device__ __forceinline__ void zero() { xy.zero(), zd.zero(); }
+  __device__ __forceinline__ void fold(float *acc) const { xy.fold(acc), zd.fold(acc); }
+};
+template <>
+struct Accum<2> {
+  PairAcc<kCalU, kCalV> uv;
+  RowAcc<kCalZ> z;
+  __device__ __forceinline__ void zero() { uv.zero(), z.zero(); }
+  __device__ __forceinline__ void fold(float *acc) const { uv.fold(acc), z.fold(acc); }
+};
+template <>
+struct Accum<0> {
+  PairAcc<kPtX, kPtY> xy;
+  RowAcc<kPtZ> z;
+  __device__ __forceinline__ void zero() { xy.zero(), z.zero(); }
+  __device__ __forceinline__ void fold(float *acc) const { xy.fold(acc), z.fold(acc); }
+};
 
 struct ResidualParams {
   float inv_sig_a, inv_sig_b;  // 1/sigma
@@ -344,10 +497,13 @@ __device__ __forceinline__ PixIn<MODE> make_pixin(const ResidualParams &P, const
 
 // One (edge, pixel) contribution from the target-side inputs and
 // Y = T_ij Xj (source point in frame i).
+#ifndef M3S_CALIB_V2
+#define M3S_CALIB_V2 1
+#endif
 template <int MODE>
-__device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &P, const PixIn<MODE> &in,
+__device__ __forceinline__ void pixel_contrib(Accum<MODE> &acc, const ResidualParams &P, const PixIn<MODE> &in,
                                               const float *Y) {
-  if (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
+  if constexpr (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
     const float nj2 = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
     const float nj = fsqrt(nj2);
     const float inj = frcp(nj);
@@ -365,15 +521,49 @@ __device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &
     // d r / d P = (I - r r^T) / |P|
     const float dxx = inj - rx * rx * inj, dyy = inj - ry * ry * inj, dzz = inj - rz * rz * inj;
     const float dxy = -rx * ry * inj, dxz = -rx * rz * inj, dyz = -ry * rz * inj;
-    const float a0[7] = {dxx, dxy, dxz, 0.0f, rz, -ry, 0.0f};
-    const float a1[7] = {dxy, dyy, dyz, -rz, 0.0f, rx, 0.0f};
-    const float a2[7] = {dxz, dyz, dzz, ry, -rx, 0.0f, 0.0f};
-    const float a3[7] = {rx, ry, rz, 0.0f, 0.0f, 0.0f, nj};
-    accum_row<kRayX>(acc, a0, w0, e0);
-    accum_row<kRayY>(acc, a1, w1, e1);
-    accum_row<kRayZ>(acc, a2, w2, e2);
-    accum_row<kRayD>(acc, a3, w3, e3);
-  } else if (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
+    // non-zero entries of the rows (kRayX..kRayD order of columns)
+    //   x: {dxx, dxy, dxz, rz, -ry}   y: {dxy, dyy, dyz, -rz, rx}
+    //   z: {dxz, dyz, dzz, ry, -rx}   d: {rx, ry, rz, nj}
+    const f32x2 axy[5] = {{dxx, dxy}, {dxy, dyy}, {dxz, dyz}, {rz, -rz}, {-ry, rx}};
+    const f32x2 azd[5] = {{dxz, rx}, {dyz, ry}, {dzz, rz}, {ry, nj}, {-rx, 0.0f}};
+    acc.xy.add(axy, f32x2{w0, w1}, f32x2{e0, e1});
+    acc.zd.add(azd, f32x2{w2, w3}, f32x2{e2, e3});
+  } else if constexpr (MODE == 2 && M3S_CALIB_V2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
+    // The u / v rows in focal-normalised form: with f = (fx, fy), a' = a / f,
+    // e' = e / f and W = w f^2 the sums are unchanged (W a' a'^T = w a a^T,
+    // W e' a' = w e a, W e'^2 = w e^2), and W needs no extra work:
+    //   w = huber(sw e) sw^2 = min(sw^2, k sw / |e|)  (|sw e| < k -> sw^2)
+    //   W = min((sw f)^2, k (sw f) / |e'|)
+    const bool vz = Y[2] > P.z_eps;  // z_i > z_eps is folded into sq
+    const float zr = frcp(Y[2]), lj_ = flog(Y[2]);
+    const float zinv = vz ? zr : 0.0f;
+    const float e2 = vz ? lj_ - in.v[2] : 0.0f;  // log z_j - log z_i (both 0 when !vz)
+    const int uvt = __float_as_int(in.v[0]);
+    const f32x2 tuv = {(float)(uvt & 0xffff), (float)(uvt >> 16)};
+    const f32x2 fxy = {P.fx, P.fy};
+    const f32x2 xy = f32x2{Y[0], Y[1]} * zinv;
+    const f32x2 uv = __builtin_elementwise_fma(fxy, xy, f32x2{P.cx, P.cy});
+    const bool vu = (uv.x > P.border) && (uv.x < (float)P.width - 1.0f - P.border);
+    const bool vv = (uv.y > P.border) && (uv.y < (float)P.height - 1.0f - P.border);
+    const bool good = vu && vv && vz;
+    const float sq = good ? in.v[1] : 0.0f;
+    const f32x2 et = (uv - tuv) * f32x2{1.0f / P.fx, 1.0f / P.fy};
+    const f32x2 swf = sq * (P.inv_sig_a * fxy);
+    const f32x2 kpf = swf * swf, ksf = swf * P.huber_k;
+    const f32x2 W = {fminf(kpf.x, ksf.x * frcp(fabsf(et.x))), fminf(kpf.y, ksf.y * frcp(fabsf(et.y)))};
+    const float swz = sq * P.inv_sig_b;
+    const float w2 = fminf(swz * swz, (swz * P.huber_k) * frcp(fabsf(e2)));
+    const float x = xy.x, y = xy.y;
+    // u / fx: {1/z, -x/z, -x y, 1 + x^2, -y}   (columns 0 2 3 4 5)
+    // v / fy: {1/z, -y/z, -(1 + y^2), x y, x}  (columns 1 2 3 4 5)
+    // log z:  {1/z, y, -x, 1}                  (columns 2 3 4 6)
+    const float xyp = x * y;
+    const f32x2 auv[5] = {{zinv, zinv}, -(xy * zinv), {-xyp, -__builtin_fmaf(y, y, 1.0f)},
+                          {__builtin_fmaf(x, x, 1.0f), xyp}, {-y, x}};
+    acc.uv.add(auv, W, et);
+    const float az[4] = {zinv, y, -x, 1.0f};
+    acc.z.add(az, w2, e2);
+  } else if constexpr (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
     const bool vz = Y[2] > P.z_eps;  // z_i > z_eps is folded into sq
     // computed unconditionally and selected (no exec-mask branches); the
     // unselected values may be inf/NaN and never reach the sums
@@ -397,12 +587,28 @@ __device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &
     const float w1 = huber_w(swp * e1, P.huber_k) * kp;
     const float w2 = huber_w(swz * e2, P.huber_k) * kz;
     const float fx = P.fx, fy = P.fy;
-    const float a0[7] = {fx * zinv, 0.0f, -fx * x * zinv, -fx * x * y, fx * (1.0f + x * x), -fx * y, 0.0f};
-    const float a1[7] = {0.0f, fy * zinv, -fy * y * zinv, -fy * (1.0f + y * y), fy * x * y, fy * x, 0.0f};
-    const float a2[7] = {0.0f, 0.0f, zinv, y, -x, 0.0f, 1.0f};
-    accum_row<kCalU>(acc, a0, w0, e0);
-    accum_row<kCalV>(acc, a1, w1, e1);
-    accum_row<kCalZ>(acc, a2, w2, e2);
+    // u: {fx/z, -fx x/z, -fx x y, fx (1 + x^2), -fx y}  (columns 0 2 3 4 5)
+    // v: {fy/z, -fy y/z, -fy (1 + y^2), fy x y, fy x}  (columns 1 2 3 4 5)
+    // log z: {1/z, y, -x, 1}                            (columns 2 3 4 6)
+#ifndef M3S_FOLD_F
+#define M3S_FOLD_F 1
+#endif
+#if M3S_FOLD_F
+    // the u / v rows divided by fx / fy, the focal factors moved into the weights
+    const float xz = x * zinv, yz = y * zinv, xy = x * y;
+    const f32x2 auv[5] = {{zinv, zinv}, {-xz, -yz}, {-xy, -__builtin_fmaf(y, y, 1.0f)},
+                          {__builtin_fmaf(x, x, 1.0f), xy}, {-y, x}};
+    acc.uv.add_scaled(auv, f32x2{w0, w1}, f32x2{e0, e1}, f32x2{fx, fy});
+#else
+    const f32x2 auv[5] = {{fx * zinv, fy * zinv},
+                          {-fx * x * zinv, -fy * y * zinv},
+                          {-fx * x * y, -fy * (1.0f + y * y)},
+                          {fx * (1.0f + x * x), fy * x * y},
+                          {-fx * y, fy * x}};
+    acc.uv.add(auv, f32x2{w0, w1}, f32x2{e0, e1});
+#endif
+    const float az[4] = {zinv, y, -x, 1.0f};
+    acc.z.add(az, w2, e2);
   } else {  // 3D point (point_align_kernel :564-674)
     const float e0 = Y[0] - in.v[0], e1 = Y[1] - in.v[1], e2 = Y[2] - in.v[2];
     const float sw = P.inv_sig_a * in.v[3];
@@ -410,12 +616,12 @@ __device__ __forceinline__ void pixel_contrib(float *acc, const ResidualParams &
     const float w0 = huber_w(sw * e0, P.huber_k) * k2;
     const float w1 = huber_w(sw * e1, P.huber_k) * k2;
     const float w2 = huber_w(sw * e2, P.huber_k) * k2;
-    const float a0[7] = {1.0f, 0.0f, 0.0f, 0.0f, Y[2], -Y[1], Y[0]};
-    const float a1[7] = {0.0f, 1.0f, 0.0f, -Y[2], 0.0f, Y[0], Y[1]};
-    const float a2[7] = {0.0f, 0.0f, 1.0f, Y[1], -Y[0], 0.0f, Y[2]};
-    accum_row<kPtX>(acc, a0, w0, e0);
-    accum_row<kPtY>(acc, a1, w1, e1);
-    accum_row<kPtZ>(acc, a2, w2, e2);
+    // x: {1, Y2, -Y1, Y0} (columns 0 4 5 6)  y: {1, -Y2, Y0, Y1} (1 3 5 6)
+    // z: {1, Y1, -Y0, Y2} (columns 2 3 4 6)
+    const f32x2 axy[4] = {{1.0f, 1.0f}, {Y[2], -Y[2]}, {-Y[1], Y[0]}, {Y[0], Y[1]}};
+    const float az[4] = {1.0f, Y[1], -Y[0], Y[2]};
+    acc.xy.add(axy, f32x2{w0, w1}, f32x2{e0, e1});
+    acc.z.add(az, w2, e2);
   }
 }
 

@@ -410,9 +410,8 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
   constexpr int NPL = PixIn<MODE>::kPlanes;
   float *__restrict__ pl = WPACK ? A.planes + (size_t)e_loc * NPL * HW : nullptr;
 
-  float acc[kNP];
-#pragma unroll
-  for (int k = 0; k < kNP; k++) acc[k] = 0.0f;
+  Accum<MODE> acc;
+  acc.zero();
 
   const int64_t p_begin = c * A.chunk_pix;
   const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
@@ -469,15 +468,21 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
       }
     }
   }
-  store_partial(acc, A.partials + (size_t)b * kNP);
+  float sums[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
+  acc.fold(sums);
+  store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
 }
 
 // Later GN iterations of a solve call: target-side inputs from the planes the
 // first iteration stored, Xj streamed (shared through L2 by the edges of one
 // keyframe, which the task table places on one XCD back to back). No gathers.
+// calib / points fit 128 VGPRs (4 waves per SIMD); rays keeps 84 accumulator
+// VGPRs and is left unbounded (164, 3 waves)
 template <int MODE>
-__global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
+__global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_kernel(LinArgs A) {
   if (*A.stop) return;
   const int64_t b = block_task(A);
   if (b < 0) return;
@@ -496,9 +501,8 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
   constexpr int NPL = PixIn<MODE>::kPlanes;
   const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
 
-  float acc[kNP];
-#pragma unroll
-  for (int k = 0; k < kNP; k++) acc[k] = 0.0f;
+  Accum<MODE> acc;
+  acc.zero();
   const int64_t p_begin = c * A.chunk_pix;
   const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
 #ifndef M3S_PK_GROUP
@@ -520,10 +524,11 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
     const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * q);
     xv[0] = xj4[0], xv[1] = xj4[1], xv[2] = xj4[2];
   };
+  float sink = 0.0f;  // M3S_PK_NOCOMPUTE experiment only
   auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
 #if M3S_PK_NOCOMPUTE  // experiment: memory floor
-    for (int k = 0; k < NPL; k++) acc[k] += pv[k].x + pv[k].y + pv[k].z + pv[k].w;
-    acc[8] += xv[0].x + xv[1].y + xv[2].z;
+    for (int k = 0; k < NPL; k++) sink += pv[k].x + pv[k].y + pv[k].z + pv[k].w;
+    sink += xv[0].x + xv[1].y + xv[2].z;
     return;
 #endif
     const float Xj[4][3] = {{xv[0].x, xv[0].y, xv[0].z}, {xv[0].w, xv[1].x, xv[1].y},
@@ -540,7 +545,43 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
       if ((s + 1) % M3S_PK_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
     }
   };
-#if M3S_PK_PREFETCH
+#ifndef M3S_PK_GLDS
+#define M3S_PK_GLDS 1
+#endif
+#if M3S_PK_GLDS && !M3S_PK_NOLOAD
+  // Prefetch one trip ahead through LDS with no VGPR cost: each wave's next
+  // trip (NPL plane vectors + 3 Xj vectors, 16 B per lane each) is loaded by
+  // global_load_lds_dwordx4 into the wave's own LDS slot while the wave
+  // computes the current trip from registers. Lane l's 16 B land at slot +
+  // 16 l (lane-linear), so every lane reads back exactly what it loaded.
+  __shared__ __attribute__((aligned(16))) f32x4 stage[kThreads / 64][NPL + 3][64];
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  auto issue = [&](int64_t q) {
+#pragma unroll
+    for (int k = 0; k < NPL; k++)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(pl + (size_t)k * HW + q),
+                                       (__attribute__((address_space(3))) void *)(&stage[wv][k][0]),
+                                       16, 0, M3S_NT ? 2 : 0);
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(Xs_j + 3 * q + 4 * k),
+                                       (__attribute__((address_space(3))) void *)(&stage[wv][NPL + k][0]),
+                                       16, 0, 0);
+  };
+  int64_t p0 = p_begin + kPixPerThread * threadIdx.x;
+  if (p0 < p_end) issue(p0);
+  for (; p0 < p_end; p0 += kBlockPix) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    f32x4 pv[NPL], xv[3];
+#pragma unroll
+    for (int k = 0; k < NPL; k++) pv[k] = stage[wv][k][ln];
+#pragma unroll
+    for (int k = 0; k < 3; k++) xv[k] = stage[wv][NPL + k][ln];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
+    if (p0 + kBlockPix < p_end) issue(p0 + kBlockPix);
+    do_trip(pv, xv);
+  }
+#elif M3S_PK_PREFETCH
   // software pipeline: the next trip's loads are in flight during this trip's math
   int64_t p0 = p_begin + kPixPerThread * threadIdx.x;
   f32x4 pv[NPL], xv[3];
@@ -561,7 +602,12 @@ __global__ void M3S_LIN_BOUNDS linearize_packed_kernel(LinArgs A) {
     do_trip(pv, xv);
   }
 #endif
-  store_partial(acc, A.partials + (size_t)b * kNP);
+  float sums[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
+  acc.fold(sums);
+  sums[0] += sink;
+  store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
 }
 

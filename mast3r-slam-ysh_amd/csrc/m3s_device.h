@@ -334,23 +334,6 @@ struct PairAcc {
     for (int p = 0; p < K; p++) g[p] = __builtin_elementwise_fma(we, a[p], g[p]);
     c = __builtin_elementwise_fma(we, e, c);
   }
-  // rows given as a / f (f per row): w a a^T = (w f^2) a' a'^T, w e a = (w f e) a'
-  __device__ __forceinline__ void add_scaled(const f32x2 (&a)[K], f32x2 w, f32x2 e, f32x2 f) {
-    const f32x2 wf = w * f;
-    const f32x2 wff = wf * f;
-    f32x2 wa[K];
-#pragma unroll
-    for (int p = 0; p < K; p++) wa[p] = wff * a[p];
-    int t = 0;
-#pragma unroll
-    for (int p = 0; p < K; p++)
-#pragma unroll
-      for (int q = p; q < K; q++, t++) h[t] = __builtin_elementwise_fma(wa[p], a[q], h[t]);
-    const f32x2 wfe = wf * e;
-#pragma unroll
-    for (int p = 0; p < K; p++) g[p] = __builtin_elementwise_fma(wfe, a[p], g[p]);
-    c = __builtin_elementwise_fma(w * e, e, c);
-  }
   __device__ __forceinline__ void fold(float *acc) const {
     int t = 0;
 #pragma unroll
@@ -408,17 +391,82 @@ struct RowAcc {
   }
 };
 
+// Scalar twin of the packed accumulators that adds straight into one
+// 36-float layout (fewer registers: the first, gathering GN iteration keeps 4
+// pixels of raw inputs live and uses it). Same products, the reference's order
+// per entry (rows u/x, then v/y, then the third row).
+struct AccumFlat {
+  float s[kNP];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int k = 0; k < kNP; k++) s[k] = 0.0f;
+  }
+  __device__ __forceinline__ void fold(float *acc) const {
+#pragma unroll
+    for (int k = 0; k < kNP; k++) acc[k] += s[k];
+  }
+  template <unsigned MA, unsigned MB, int K>
+  __device__ __forceinline__ void add2(const f32x2 (&a)[K], f32x2 w, f32x2 e) {
+    f32x2 wa[K];
+#pragma unroll
+    for (int p = 0; p < K; p++) wa[p] = w * a[p];
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++) {
+        const int ta = kL + tri(nth_col(MA, p), nth_col(MA, q));
+        s[ta] = __builtin_fmaf(wa[p].x, a[q].x, s[ta]);
+        if (nth_col(MB, q) >= 0) {
+          const int tb = kL + tri(nth_col(MB, p), nth_col(MB, q));
+          s[tb] = __builtin_fmaf(wa[p].y, a[q].y, s[tb]);
+        }
+      }
+    const f32x2 we = w * e;
+#pragma unroll
+    for (int p = 0; p < K; p++) {
+      s[kG + nth_col(MA, p)] = __builtin_fmaf(we.x, a[p].x, s[kG + nth_col(MA, p)]);
+      if (nth_col(MB, p) >= 0) s[kG + nth_col(MB, p)] = __builtin_fmaf(we.y, a[p].y, s[kG + nth_col(MB, p)]);
+    }
+    s[kCost] = __builtin_fmaf(we.x, e.x, s[kCost]);
+    s[kCost] = __builtin_fmaf(we.y, e.y, s[kCost]);
+  }
+  template <unsigned M, int K>
+  __device__ __forceinline__ void add1(const float (&a)[K], float w, float e) {
+    float wa[K];
+#pragma unroll
+    for (int p = 0; p < K; p++) wa[p] = w * a[p];
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++) {
+        const int t = kL + tri(nth_col(M, p), nth_col(M, q));
+        s[t] = __builtin_fmaf(wa[p], a[q], s[t]);
+      }
+    const float we = w * e;
+#pragma unroll
+    for (int p = 0; p < K; p++) s[kG + nth_col(M, p)] = __builtin_fmaf(we, a[p], s[kG + nth_col(M, p)]);
+    s[kCost] = __builtin_fmaf(we, e, s[kCost]);
+  }
+};
+
 // Per-lane accumulators of one residual model: rays pairs (x, y) and
 // (z, dist); calib pairs (u, v) plus the log-depth row; points pairs (x, y)
 // plus z. fold() adds them into the 36-float layout (kL / kG / kCost).
 template <int MODE>
 struct Accum;
+// add2<MA, MB>(a, w, e) / add1<M>(a, w, e) route a row pair / a row to its
+// accumulator (the same calls drive AccumFlat).
 template <>
 struct Accum<1> {
   PairAcc<kRayX, kRayY> xy;
   PairAcc<kRayZ, kRayD> zd;
   __device__ __forceinline__ void zero() { xy.zero(), zd.zero(); }
   __device__ __forceinline__ void fold(float *acc) const { xy.fold(acc), zd.fold(acc); }
+  template <unsigned MA, unsigned MB, int K>
+  __device__ __forceinline__ void add2(const f32x2 (&a)[K], f32x2 w, f32x2 e) {
+    if constexpr (MA == kRayX) xy.add(a, w, e);
+    else zd.add(a, w, e);
+  }
 };
 template <>
 struct Accum<2> {
@@ -426,6 +474,10 @@ struct Accum<2> {
   RowAcc<kCalZ> z;
   __device__ __forceinline__ void zero() { uv.zero(), z.zero(); }
   __device__ __forceinline__ void fold(float *acc) const { uv.fold(acc), z.fold(acc); }
+  template <unsigned MA, unsigned MB, int K>
+  __device__ __forceinline__ void add2(const f32x2 (&a)[K], f32x2 w, f32x2 e) { uv.add(a, w, e); }
+  template <unsigned M, int K>
+  __device__ __forceinline__ void add1(const float (&a)[K], float w, float e) { z.add(a, w, e); }
 };
 template <>
 struct Accum<0> {
@@ -433,6 +485,10 @@ struct Accum<0> {
   RowAcc<kPtZ> z;
   __device__ __forceinline__ void zero() { xy.zero(), z.zero(); }
   __device__ __forceinline__ void fold(float *acc) const { xy.fold(acc), z.fold(acc); }
+  template <unsigned MA, unsigned MB, int K>
+  __device__ __forceinline__ void add2(const f32x2 (&a)[K], f32x2 w, f32x2 e) { xy.add(a, w, e); }
+  template <unsigned M, int K>
+  __device__ __forceinline__ void add1(const float (&a)[K], float w, float e) { z.add(a, w, e); }
 };
 
 struct ResidualParams {
@@ -497,11 +553,8 @@ __device__ __forceinline__ PixIn<MODE> make_pixin(const ResidualParams &P, const
 
 // One (edge, pixel) contribution from the target-side inputs and
 // Y = T_ij Xj (source point in frame i).
-#ifndef M3S_CALIB_V2
-#define M3S_CALIB_V2 1
-#endif
-template <int MODE>
-__device__ __forceinline__ void pixel_contrib(Accum<MODE> &acc, const ResidualParams &P, const PixIn<MODE> &in,
+template <int MODE, typename ACC>
+__device__ __forceinline__ void pixel_contrib(ACC &acc, const ResidualParams &P, const PixIn<MODE> &in,
                                               const float *Y) {
   if constexpr (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
     const float nj2 = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
@@ -526,9 +579,9 @@ __device__ __forceinline__ void pixel_contrib(Accum<MODE> &acc, const ResidualPa
     //   z: {dxz, dyz, dzz, ry, -rx}   d: {rx, ry, rz, nj}
     const f32x2 axy[5] = {{dxx, dxy}, {dxy, dyy}, {dxz, dyz}, {rz, -rz}, {-ry, rx}};
     const f32x2 azd[5] = {{dxz, rx}, {dyz, ry}, {dzz, rz}, {ry, nj}, {-rx, 0.0f}};
-    acc.xy.add(axy, f32x2{w0, w1}, f32x2{e0, e1});
-    acc.zd.add(azd, f32x2{w2, w3}, f32x2{e2, e3});
-  } else if constexpr (MODE == 2 && M3S_CALIB_V2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
+    acc.template add2<kRayX, kRayY>(axy, f32x2{w0, w1}, f32x2{e0, e1});
+    acc.template add2<kRayZ, kRayD>(azd, f32x2{w2, w3}, f32x2{e2, e3});
+  } else if constexpr (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
     // The u / v rows in focal-normalised form: with f = (fx, fy), a' = a / f,
     // e' = e / f and W = w f^2 the sums are unchanged (W a' a'^T = w a a^T,
     // W e' a' = w e a, W e'^2 = w e^2), and W needs no extra work:
@@ -560,55 +613,9 @@ __device__ __forceinline__ void pixel_contrib(Accum<MODE> &acc, const ResidualPa
     const float xyp = x * y;
     const f32x2 auv[5] = {{zinv, zinv}, -(xy * zinv), {-xyp, -__builtin_fmaf(y, y, 1.0f)},
                           {__builtin_fmaf(x, x, 1.0f), xyp}, {-y, x}};
-    acc.uv.add(auv, W, et);
+    acc.template add2<kCalU, kCalV>(auv, W, et);
     const float az[4] = {zinv, y, -x, 1.0f};
-    acc.z.add(az, w2, e2);
-  } else if constexpr (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
-    const bool vz = Y[2] > P.z_eps;  // z_i > z_eps is folded into sq
-    // computed unconditionally and selected (no exec-mask branches); the
-    // unselected values may be inf/NaN and never reach the sums
-    const float zr = frcp(Y[2]), lj_ = flog(Y[2]);
-    const float zinv = vz ? zr : 0.0f;
-    const float lzj = vz ? lj_ : 0.0f;
-    const float lzi = vz ? in.v[2] : 0.0f;
-    const int uv = __float_as_int(in.v[0]);
-    const float u_t = (float)(uv & 0xffff), v_t = (float)(uv >> 16);
-    const float x = Y[0] * zinv, y = Y[1] * zinv;
-    const float u = P.fx * x + P.cx, v = P.fy * y + P.cy;
-    const bool vu = (u > P.border) && (u < (float)P.width - 1.0f - P.border);
-    const bool vv = (v > P.border) && (v < (float)P.height - 1.0f - P.border);
-    const float e0 = u - u_t, e1 = v - v_t, e2 = lzj - lzi;
-    const bool good = vu && vv && vz;
-    const float sq = in.v[1];
-    const float swp = good ? P.inv_sig_a * sq : 0.0f;
-    const float swz = good ? P.inv_sig_b * sq : 0.0f;
-    const float kp = swp * swp, kz = swz * swz;
-    const float w0 = huber_w(swp * e0, P.huber_k) * kp;
-    const float w1 = huber_w(swp * e1, P.huber_k) * kp;
-    const float w2 = huber_w(swz * e2, P.huber_k) * kz;
-    const float fx = P.fx, fy = P.fy;
-    // u: {fx/z, -fx x/z, -fx x y, fx (1 + x^2), -fx y}  (columns 0 2 3 4 5)
-    // v: {fy/z, -fy y/z, -fy (1 + y^2), fy x y, fy x}  (columns 1 2 3 4 5)
-    // log z: {1/z, y, -x, 1}                            (columns 2 3 4 6)
-#ifndef M3S_FOLD_F
-#define M3S_FOLD_F 1
-#endif
-#if M3S_FOLD_F
-    // the u / v rows divided by fx / fy, the focal factors moved into the weights
-    const float xz = x * zinv, yz = y * zinv, xy = x * y;
-    const f32x2 auv[5] = {{zinv, zinv}, {-xz, -yz}, {-xy, -__builtin_fmaf(y, y, 1.0f)},
-                          {__builtin_fmaf(x, x, 1.0f), xy}, {-y, x}};
-    acc.uv.add_scaled(auv, f32x2{w0, w1}, f32x2{e0, e1}, f32x2{fx, fy});
-#else
-    const f32x2 auv[5] = {{fx * zinv, fy * zinv},
-                          {-fx * x * zinv, -fy * y * zinv},
-                          {-fx * x * y, -fy * (1.0f + y * y)},
-                          {fx * (1.0f + x * x), fy * x * y},
-                          {-fx * y, fy * x}};
-    acc.uv.add(auv, f32x2{w0, w1}, f32x2{e0, e1});
-#endif
-    const float az[4] = {zinv, y, -x, 1.0f};
-    acc.z.add(az, w2, e2);
+    acc.template add1<kCalZ>(az, w2, e2);
   } else {  // 3D point (point_align_kernel :564-674)
     const float e0 = Y[0] - in.v[0], e1 = Y[1] - in.v[1], e2 = Y[2] - in.v[2];
     const float sw = P.inv_sig_a * in.v[3];
@@ -620,8 +627,8 @@ __device__ __forceinline__ void pixel_contrib(Accum<MODE> &acc, const ResidualPa
     // z: {1, Y1, -Y0, Y2} (columns 2 3 4 6)
     const f32x2 axy[4] = {{1.0f, 1.0f}, {Y[2], -Y[2]}, {-Y[1], Y[0]}, {Y[0], Y[1]}};
     const float az[4] = {1.0f, Y[1], -Y[0], Y[2]};
-    acc.xy.add(axy, f32x2{w0, w1}, f32x2{e0, e1});
-    acc.z.add(az, w2, e2);
+    acc.template add2<kPtX, kPtY>(axy, f32x2{w0, w1}, f32x2{e0, e1});
+    acc.template add1<kPtZ>(az, w2, e2);
   }
 }
 

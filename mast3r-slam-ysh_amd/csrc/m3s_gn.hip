@@ -410,7 +410,8 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
   constexpr int NPL = PixIn<MODE>::kPlanes;
   float *__restrict__ pl = WPACK ? A.planes + (size_t)e_loc * NPL * HW : nullptr;
 
-  Accum<MODE> acc;
+  // scalar accumulators here: 4 pixels of raw inputs stay live in this kernel
+  AccumFlat acc;
   acc.zero();
 
   const int64_t p_begin = c * A.chunk_pix;
@@ -1094,6 +1095,16 @@ __device__ __forceinline__ int ready_prefix(bool ok, int q_, int q1) {
     }                                                              \
   }
 
+// Wave-uniform ticket from an LDS counter: every lane adds 1 (the atomic
+// optimizer folds this into one ds_add of the active-lane count) and lane 0's
+// old value / 64 is the ticket (whole waves only). A lane-0-only atomic
+// followed by a broadcast (readfirstlane or an LDS slot) hung the dataflow
+// waits behind it on gfx950 / ROCm 7.2; this form does not.
+__device__ __forceinline__ int wave_ticket(int *ctr) {
+  const int o = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(o) >> 6;
+}
+
 __device__ __forceinline__ bool flag_set(int32_t *flag) {
   return __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
 }
@@ -1231,7 +1242,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   constexpr bool IN_LDS = STORE != 0;
   constexpr bool STAGE = STORE == 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int fail_s;
+  __shared__ int fail_s, next_item, next_col;
   __shared__ float nrm[16];
   __shared__ double scratch[16][64];
   const int m = D.m, S = D.S;
@@ -1280,7 +1291,8 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #define M3S_TS(i)
 #endif
 #if M3S_LLT_ITEMS  // experiment: per-item (start, inputs ready, published) clock stamps into D.dbg
-#define M3S_IT(j) if (lane == 0) D.dbg[4 * it + (j)] = (int64_t)clock64();
+// stamp 0 carries the wave id in bits 58.. (dynamic dispatch)
+#define M3S_IT(j) if (lane == 0) D.dbg[4 * it + (j)] = (int64_t)clock64() | ((j) == 0 ? (int64_t)wave << 58 : 0);
 #else
 #define M3S_IT(j)
 #endif
@@ -1315,7 +1327,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
     for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
   }
-  if (tid == 0) fail_s = 0;
+  if (tid == 0) fail_s = 0, next_item = 0, next_col = 0;
   __syncthreads();
   M3S_TS(1)
 
@@ -1327,8 +1339,15 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // schedule_items); each item waits on LDS completion flags of exactly the
   // blocks it reads and publishes its own. No workgroup barriers inside the
   // factorisation; the schedule's assignment order guarantees progress.
-  for (int it = wave_ptr[wave]; it < wave_ptr[wave + 1]; it++) {
+  const int n_disp = wave_ptr[1];
+  for (;;) {
+    // dynamic dispatch: the next item of the (topological) dispatch list
+    const int it = wave_ticket(&next_item);
+    if (it >= n_disp) break;
     const int item = witems[it];
+#if M3S_LLT_DEBUG
+    if (lane == 0) printf("wave %d takes %d/%d item %d\n", wave, it, n_disp, item);
+#endif
     M3S_IT(0)
     if (item >= n_tasks) {  // PART: partial sum of the head of a long update list
       const int pi = item - n_tasks, tg = part_tgt[pi];
@@ -1452,8 +1471,17 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       M3S_IT(2)
     }
+#if M3S_LLT_DEBUG
+    if (lane == 0) printf("wave %d done %d\n", wave, it);
+#endif
   }
+#if M3S_LLT_DEBUG
+  if (lane == 0) printf("wave %d at barrier\n", wave);
+#endif
   __syncthreads();
+#if M3S_LLT_DEBUG
+  if (tid == 0) printf("factor done fail %d\n", fail_s);
+#endif
 
   if (fail_s) {
     fail_step(7 * m, D.dx_out, D.info, D.flags + kFlagStop, D.delta_thresh);
@@ -1463,12 +1491,18 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 
   // 2. back-substitution L^T x = y in reverse level order (x overwrites y),
   // dataflow: column k waits for x_i of every i in struct(k)
-  for (int t = wave; t < m; t += NW) {
+  // columns are taken dynamically in reverse level order; the x_i terms are
+  // applied as they arrive (lane-parallel flag polling, list order)
+  for (;;) {
+    const int t = wave_ticket(&next_col);
+    if (t >= m) break;
     const int k = lev_col[m - 1 - t];
+#if M3S_LLT_DEBUG
+    if (lane == 0) printf("wave %d backsub t %d k %d\n", wave, t, k);
+#endif
     const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
-    for (int q = q0; q < q1; q++) wait_flag(&done2[col_row[q]], &fail_s);
     double rr = y[k * 7 + lane7];
-    rr = sub_matvec<STAGE, true>(rr, Lb, col_slot, col_row, q0, q1, y, lane7, lane49, lane, stg);
+    M3S_POLL(q0, q1, flag_set(&done2[col_row[q]]), (rr = sub_matvec<STAGE, true>(rr, Lb, col_slot, col_row, qa, qb, y, lane7, lane49, lane, stg)));
     double xk = 0.0;
 #pragma unroll
     for (int mm = 0; mm < 7; mm++) {

@@ -159,6 +159,14 @@ std::pair<int, int64_t> etree_shape(int m, const BitRows &adj, const std::vector
 // assignment order; since every dependency was assigned earlier, the
 // unfinished item with the lowest assignment index can always run (no
 // deadlock), whatever the real timings.
+// Item costs in shader cycles, calibrated on MI355X with tools/llt_items.py
+// (N = 32 and 256): DIAG publishes L_kk / W_k after ~3.5k cycles plus its
+// updates, then spends the forward step y_k on the same wave; a dependency
+// hop (LDS flag, poll, s_sleep) costs a few hundred cycles.
+constexpr double kCostDiag0 = 3500.0, kCostOff0 = 900.0, kCostUpd = 250.0;
+constexpr double kCostPart0 = 150.0, kCostPartUpd = 60.0, kCostPartIn = 120.0;
+constexpr double kCostFwd0 = 1000.0, kCostFwdUpd = 200.0, kHop = 400.0;
+
 static void schedule_items(SparsePlan &P) {
   const int n = (int)P.items.size();
   const int T = (int)P.task_dst.size();
@@ -169,7 +177,7 @@ static void schedule_items(SparsePlan &P) {
     else item_of_slot[v < 0 ? -1 - v : P.task_dst[v]] = it;
   }
   std::vector<std::vector<int>> deps(n), succ(n);
-  std::vector<double> cost(n);
+  std::vector<double> cost(n), pub(n);  // wave busy time; time to publishing its block
   const bool split = !P.dpart_ptr.empty();
   for (int it = 0; it < n; it++) {
     const int v = P.items[it];
@@ -185,7 +193,7 @@ static void schedule_items(SparsePlan &P) {
           d.push_back(item_of_slot[P.tr_b[q]]);
         }
       }
-      cost[it] = 300.0 * (P.part_q1[pi] - P.part_q0[pi]);
+      cost[it] = pub[it] = kCostPart0 + kCostPartUpd * (P.part_q1[pi] - P.part_q0[pi]);
     } else if (v < 0) {
       const int k = -1 - v;
       int q0 = P.dtr_ptr[k];
@@ -193,8 +201,10 @@ static void schedule_items(SparsePlan &P) {
         for (int pi = P.dpart_ptr[k]; pi < P.dpart_ptr[k + 1]; pi++) d.push_back(item_of_part[pi]), q0 = P.part_q1[pi];
       }
       for (int q = q0; q < P.dtr_ptr[k + 1]; q++) d.push_back(item_of_slot[P.dtr_slot[q]]);
-      cost[it] = 3000.0 + 300.0 * (P.dtr_ptr[k + 1] - q0) +
-                 (split ? 150.0 * (P.dpart_ptr[k + 1] - P.dpart_ptr[k]) : 0.0);
+      const int nu = P.dtr_ptr[k + 1] - q0;
+      const double np = split ? (double)(P.dpart_ptr[k + 1] - P.dpart_ptr[k]) : 0.0;
+      pub[it] = kCostDiag0 + kCostUpd * nu + kCostPartIn * np;
+      cost[it] = pub[it] + kCostFwd0 + kCostFwdUpd * nu;  // + the forward step y_k
     } else {
       d.push_back(item_of_slot[P.task_col[v]]);
       int q0 = P.task_tr_ptr[v];
@@ -202,8 +212,8 @@ static void schedule_items(SparsePlan &P) {
         for (int pi = P.opart_ptr[v]; pi < P.opart_ptr[v + 1]; pi++) d.push_back(item_of_part[pi]), q0 = P.part_q1[pi];
       }
       for (int q = q0; q < P.task_tr_ptr[v + 1]; q++) d.push_back(item_of_slot[P.tr_a[q]]);
-      cost[it] = 800.0 + 300.0 * (P.task_tr_ptr[v + 1] - q0) +
-                 (split ? 150.0 * (P.opart_ptr[v + 1] - P.opart_ptr[v]) : 0.0);
+      cost[it] = pub[it] = kCostOff0 + kCostUpd * (P.task_tr_ptr[v + 1] - q0) +
+                           (split ? kCostPartIn * (P.opart_ptr[v + 1] - P.opart_ptr[v]) : 0.0);
     }
     std::sort(d.begin(), d.end());
     d.erase(std::unique(d.begin(), d.end()), d.end());
@@ -215,7 +225,7 @@ static void schedule_items(SparsePlan &P) {
   for (int it = n - 1; it >= 0; it--) {
     double best = 0.0;
     for (int s2 : succ[it]) best = std::max(best, rank[s2]);
-    rank[it] = cost[it] + best;
+    rank[it] = pub[it] + kHop + best;
   }
   std::vector<int> missing(n);
   std::vector<double> ready_at(n, 0.0);
@@ -225,8 +235,14 @@ static void schedule_items(SparsePlan &P) {
     missing[it] = (int)deps[it].size();
     if (!missing[it]) ready.push({rank[it], -it});
   }
+  // Simulated list scheduling onto the kernel's waves; the order in which
+  // items are started is the dispatch order. The kernel's waves take items
+  // from that list dynamically (an LDS counter), so a wave never idles behind
+  // a mispredicted cost while ready work waits in another wave's queue. The
+  // list is topological: every dependency of item i is dispatched before i,
+  // so the lowest unfinished dispatched item can always run (progress).
   std::vector<double> free_at(kLltWaves, 0.0);
-  std::vector<std::vector<int32_t>> seq(kLltWaves);
+  P.witems.clear();
   while (!ready.empty()) {
     const int it = -ready.top().second;
     ready.pop();
@@ -234,20 +250,17 @@ static void schedule_items(SparsePlan &P) {
     for (int x = 1; x < kLltWaves; x++)
       if (free_at[x] < free_at[w]) w = x;
     const double start = std::max(free_at[w], ready_at[it]);
-    const double finish = start + cost[it];
-    free_at[w] = finish;
-    seq[w].push_back(P.items[it]);
+    free_at[w] = start + cost[it];
+    const double published = start + pub[it] + kHop;
+    P.witems.push_back(P.items[it]);
     for (int s2 : succ[it]) {
-      ready_at[s2] = std::max(ready_at[s2], finish);
+      ready_at[s2] = std::max(ready_at[s2], published);
       if (--missing[s2] == 0) ready.push({rank[s2], -s2});
     }
   }
+  // wave_ptr = {0, n}: one dispatch list shared by all waves
   P.wave_ptr.assign(1, 0);
-  P.witems.clear();
-  for (int w = 0; w < kLltWaves; w++) {
-    P.witems.insert(P.witems.end(), seq[w].begin(), seq[w].end());
-    P.wave_ptr.push_back((int32_t)P.witems.size());
-  }
+  P.wave_ptr.push_back((int32_t)P.witems.size());
 }
 
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,

@@ -44,8 +44,9 @@ struct SparsePlan {
   // DIAG(k) targets, tr list for OFF(t)); target code -1-k or t.
   std::vector<int32_t> part_q0, part_q1, part_tgt;
   std::vector<int32_t> dpart_ptr, opart_ptr;  // parts of DIAG(k) / OFF(t), contiguous
-  // the items assigned to the kernel's waves by host list scheduling: wave w
-  // runs witems[wave_ptr[w] .. wave_ptr[w+1]) in order
+  // dispatch order of the items (host list scheduling by upward rank; a
+  // topological order): the kernel's waves take witems[0 .. wave_ptr[1]) in
+  // this order from a shared counter
   std::vector<int32_t> wave_ptr, witems;
 };
 

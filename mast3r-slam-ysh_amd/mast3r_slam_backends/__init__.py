@@ -213,7 +213,7 @@ def sparse_plan(N, ri, rj, split=0, max_parts=0):
     lens = {"perm": m, "col_ptr": m + 1, "lev_ptr": L + 1, "lev_col": m, "dtr_ptr": m + 1,
             "task_lev_ptr": L + 1, "task_dst": T, "task_col": T, "task_tr_ptr": T + 1,
             "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1,
-            "items": m + T + NP, "wave_ptr": 17, "witems": m + T + NP,
+            "items": m + T + NP, "wave_ptr": 2, "witems": m + T + NP,
             "part_q0": NP, "part_q1": NP, "part_tgt": NP,
             "dpart_ptr": m + 1 if sp else 0, "opart_ptr": T + 1 if sp else 0}
     for name, ln in lens.items():

@@ -47,11 +47,14 @@ def run_plan(p, Hjj, gj):
             ent = p["g_edge"][t]
             y[v] += gj[ent >> 1] * (1 if ent & 1 else -1)
     W = np.zeros((m, 7, 7))
-    # the kernel's dataflow: wave w runs witems[wave_ptr[w]:wave_ptr[w+1]] in
-    # order and waits on the blocks an item reads. Simulated by stepping the
-    # waves round-robin; a full round without progress would be a deadlock.
+    # the kernel's dataflow: 16 waves take items from the dispatch list
+    # witems[0:wave_ptr[1]] in order (a shared counter) and wait on the blocks
+    # an item reads. Simulated by stepping the waves round-robin; a full round
+    # without progress would be a deadlock.
     sdone = np.zeros(S, bool)
-    pos = [p["wave_ptr"][w] for w in range(16)]
+    n_disp = p["wave_ptr"][1]
+    held = [-1] * 16  # dispatch index a wave is working on
+    nxt = 0
 
     T = len(p["task_dst"])
     NP = p["n_parts"]
@@ -121,12 +124,15 @@ def run_plan(p, Hjj, gj):
             L[dst] = A @ W[k].T
             sdone[dst] = True
 
-    while any(pos[w] < p["wave_ptr"][w + 1] for w in range(16)):
+    while nxt < n_disp or any(h >= 0 for h in held):
         progressed = False
         for w in range(16):
-            if pos[w] < p["wave_ptr"][w + 1] and ready(p["witems"][pos[w]]):
-                run(p["witems"][pos[w]])
-                pos[w] += 1
+            if held[w] < 0 and nxt < n_disp:
+                held[w], nxt = nxt, nxt + 1
+                progressed = True
+            if held[w] >= 0 and ready(p["witems"][held[w]]):
+                run(p["witems"][held[w]])
+                held[w] = -1
                 progressed = True
         assert progressed, "wave schedule deadlocks"
     assert sorted(p["witems"].tolist()) == sorted(p["items"].tolist())

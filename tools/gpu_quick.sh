@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+echo "torch import"; timeout -k 10 300 python -c "import torch; print(torch.cuda.is_available())" && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
 if [ -f variants/lib_T.so ]; then
   M3S_LIB=$R/variants/lib_T.so NS=${NS:-32,64,128,256} timeout -k 10 300 python tools/llt_timing.py > $OUT/llt_t.txt 2>&1 || { echo "llt timing failed"; tail -20 $OUT/llt_t.txt; exit 1; }

@@ -35,9 +35,9 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
         torch.cuda.synchronize()
     ts = wst[lay["A"]: lay["A"] + 32 * n_it].clone().view(torch.int64).cpu().numpy().reshape(n_it, 4)
     T = len(p["task_dst"])
-    wave_of = np.zeros(n_it, int)
-    for w in range(16):
-        wave_of[p["wave_ptr"][w]:p["wave_ptr"][w + 1]] = w
+    # dynamic dispatch: the wave that ran an item is in bits 58.. of stamp 0
+    wave_of = (ts[:, 0] >> 58).astype(int)
+    ts[:, 0] &= (1 << 58) - 1
     items = p["witems"]
     pos = {int(v): i for i, v in enumerate(items)}
     t0 = ts[:, 0].min()
@@ -90,6 +90,19 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
             out.append(slot_pub[int(p["tr_a"][q])])
         return out
 
+    # dense top clique: trailing columns whose structure is every later column
+    cnt = np.diff(p["col_ptr"])
+    cq = 0
+    for k in range(m - 1, -1, -1):
+        if cnt[k] != m - 1 - k:
+            break
+        cq += 1
+    dk = np.where(items < 0, -1 - items, -1)
+    pre = (items < 0) & (dk < m - cq)
+    cl = (items < 0) & (dk >= m - cq)
+    if pre.any() and cl.any():
+        print(f"  clique {cq} columns: last non-clique L_kk at {ts[pre, 3].max()}, clique L_kk from "
+              f"{ts[cl, 3].min()} to {ts[cl, 3].max()} cycles")
     cur, stamp = int(np.argmax(ts[:, 2])), 2
     comp = defaultdict(float)
     chain = 0
@@ -97,8 +110,8 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
         chain += 1
         comp[names[kind[cur]] + " busy"] += ts[cur, stamp] - ts[cur, 1]
         dl = deps(int(items[cur]))
-        first = p["wave_ptr"][wave_of[cur]]
-        prev_same = cur - 1 if cur > first else None
+        same = [i for i in range(n_it) if wave_of[i] == wave_of[cur] and ts[i, 0] < ts[cur, 0]]
+        prev_same = max(same, key=lambda i: ts[i, 0]) if same else None
         dmax = max(dl, key=lambda d: ts[d[0], d[1]]) if dl else None
         # what the item started after: its wave's previous item or its last input
         if dmax is not None and ts[dmax[0], dmax[1]] > ts[cur, 0]:

@@ -136,8 +136,9 @@ def main():
     # ---- roofline: the dominant kernel alone, HIP events on its stream ----
     # GN iterations 2..10 of a call run linearize_packed_kernel (the first one
     # runs the gathering kernel that also stores the target-side planes). The
-    # launches are queued behind a device sleep so that the event pair brackets
-    # back-to-back GPU work only, not host enqueue gaps.
+    # timed launches follow warm ones back to back; a launch is enqueued in
+    # ~10-20 us and runs ~100 us, so the queue never drains and the event pair
+    # brackets GPU work only.
     n_loc = ee - eb
     kf_touched = torch.unique(torch.cat([ii[eb:ee], jj[eb:ee]])).numel() if n_loc else 0
     bytes_alg = HW * (13 * n_loc + 16 * kf_touched)  # SURVEY.md §8(d) per (edge, px) and (KF, px)
@@ -145,9 +146,9 @@ def main():
     be.gn_prepare(solver.args, solver.keep)
     stream = torch.cuda.current_stream(dev)
     solver.linearize_only()  # first launch: gathering kernel + planes
-    torch.cuda.synchronize()
+    for _ in range(5):  # warm launches (clocks, caches) right before the timed ones
+        solver.linearize_only()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda._sleep(20_000_000)
     ev0.record(stream)
     for _ in range(args.lin_reps):
         solver.linearize_only()

@@ -1,0 +1,107 @@
+"""GPU check of the edge-sharded GN path (mast3r_slam_amd/distributed.py over
+the stepwise C ABI m3s_gn_prepare / m3s_gn_linearize / m3s_gn_solve) that
+bench.py runs at N > 1 GPUs.
+
+One process, one GPU: R "ranks" are R HipOps instances, each with its own
+workspace, pose tensor and edge slice; the all-gather of the per-edge normal
+equations is a torch.cat. Every rank must end with bitwise-identical poses
+(identical inputs, deterministic kernels: nothing is broadcast in the real
+run), and the poses must match the single-call gauss_newton_* entry point
+(different reduction grouping: fused per-edge finalize vs edge_reduce, same
+tolerance as the oracle tests) and the CPU oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def be():
+    import mast3r_slam_backends as be
+
+    return be
+
+
+def sharded_solve(be, mode, g, Xs, world, iters, delta, sig):
+    from mast3r_slam_amd.distributed import HipOps, edge_slice
+
+    E = g.n_edges
+    ranks = []
+    for r in range(world):
+        eb, ee, per = edge_slice(E, r, world)
+        Twc = g.T_init.data.clone().to(DEV).contiguous()
+        ops = HipOps(mode, Twc, Xs, g.Cs.to(DEV).contiguous(), g.ii.to(DEV), g.jj.to(DEV),
+                     g.idx_ii2jj[eb:ee].to(DEV).contiguous(), g.valid_match[eb:ee].to(DEV).contiguous(),
+                     g.Q[eb:ee].to(DEV).contiguous(), E, g.K.to(DEV) if mode == be.MODE_CALIB else None,
+                     **sig)
+        es = torch.zeros(per, ops.stride, dtype=torch.float64, device=DEV)
+        ranks.append((eb, ee, per, Twc, ops, es))
+    for *_, ops, _ in ranks:
+        ops.prepare(delta)
+    for _ in range(iters):
+        for eb, ee, per, Twc, ops, es in ranks:
+            if ee > eb:
+                ops.linearize(eb, ee, es)
+        es_all = torch.cat([es for *_, es in ranks])  # the all_gather_into_tensor payload
+        for *_, ops, _ in ranks:
+            ops.solve(es_all)
+    torch.cuda.synchronize()
+    return [Twc.cpu().numpy() for _, _, _, Twc, _, _ in ranks], [ops.info.cpu().numpy() for *_, ops, _ in ranks]
+
+
+@pytest.mark.parametrize("mode,world", [("rays", 2), ("calib", 3), ("calib", 2)])
+def test_sharded_ranks_agree_and_match_single_call(be, mode, world):
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(7, 48, 64, seed=41)
+    if mode == "calib":
+        rays = synthetic.pixel_rays(g.H, g.W, g.K)
+        Xs = (g.Xs[..., 2:3] * rays[None]).to(DEV).contiguous()
+        sig = dict(sigma_a=1.0, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5, height=g.H, width=g.W,
+                   pixel_border=-10, z_eps=1e-6)
+        m = be.MODE_CALIB
+    else:
+        Xs = g.Xs.to(DEV).contiguous()
+        sig = dict(sigma_a=0.003, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5)
+        m = be.MODE_RAYS
+    iters = 5
+    poses, infos = sharded_solve(be, m, g, Xs, world, iters, 0.0, sig)
+    for r in range(1, world):
+        np.testing.assert_array_equal(poses[r], poses[0])
+    for inf in infos:
+        assert int(inf[be.INFO_ITERS]) == iters
+
+    Twc = g.T_init.data.clone().to(DEV).contiguous()
+    info = torch.zeros(8, dtype=torch.int32, device=DEV)
+    args = [t.to(DEV).contiguous() for t in (g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q)]
+    if mode == "calib":
+        Cs, ii, jj, idx, valid, Q = args
+        be.gauss_newton_calib(Twc, Xs, Cs, g.K.to(DEV), ii, jj, idx, valid, Q, g.H, g.W, -10, 1e-6,
+                              1.0, 10.0, 0.0, 1.5, iters, 0.0, info=info)
+    else:
+        Cs, ii, jj, idx, valid, Q = args
+        be.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5, iters, 0.0,
+                             info=info)
+    torch.cuda.synchronize()
+    ref = Twc.cpu().numpy()
+    # fp32 per-pixel sums grouped differently (edge_reduce vs the fused
+    # per-edge finalize); cond(H) amplifies it: DESIGN.md §5 pose tolerance
+    np.testing.assert_allclose(poses[0], ref, rtol=0, atol=1e-4)
+    assert not np.array_equal(poses[0], g.T_init.data.numpy())  # the solve moved the poses
+
+
+def test_sharded_natural_termination(be):
+    """delta > 0: the device stop flag ends every rank after the same step."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(5, 32, 48, seed=43)
+    sig = dict(sigma_a=0.003, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5)
+    poses, infos = sharded_solve(be, be.MODE_RAYS, g, g.Xs.to(DEV).contiguous(), 2, 20, 1e-3, sig)
+    np.testing.assert_array_equal(poses[0], poses[1])
+    its = [int(i[be.INFO_ITERS]) for i in infos]
+    assert its[0] == its[1] < 20
+    assert all(int(i[be.INFO_CONVERGED]) == 1 for i in infos)

@@ -1011,6 +1011,7 @@ struct SparseDev {
   int m, S, levels, n_items;
   int n_tasks, n_parts;  // OFF tasks; PART items (0: no split updates)
   int E, asm_lds;        // asm_lds: assemble in-kernel from fin staged in LDS (else assemble_slots_kernel)
+  int nc;                // dense-tail columns (m3s_symbolic.h, clq); 0: none
   double *parts;         // [n_parts][56] partial update blocks (+ partial RHS)
   int64_t *dbg;  // M3S_LLT_TIMING: per-column DIAG completion stamps
   double *L;     // [S][49] (global variant)
@@ -1233,6 +1234,77 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
 
 // One 1024-thread workgroup: assembly -> dataflow block LLT + forward
 // substitution -> dataflow back-substitution -> dx, retraction, ||dx||.
+// DIAG of one column: v (entry layout, lane = 7r + c) = D_k after all its
+// updates -> L_kk (row-major, upper part 0) into Lb[k], W_k = L_kk^-1
+// (row-major) into Di[k]; Lr (strictly lower L_kk) and dinv = 1 / diag, wave-
+// uniform, for the forward step. Returns true on a non-positive pivot.
+__device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double *Di, double *scr, int lane,
+                                            int l7, double (&Lr)[7][7], double (&dinv)[7]) {
+  // entry layout -> row layout through the wave's scratch
+  if (lane < 49) scr[lane] = v;
+  wave_lds_fence();
+  double a[7];
+#pragma unroll
+  for (int qq = 0; qq < 7; qq++) a[qq] = scr[l7 + qq];
+  wave_lds_fence();
+  // Cholesky: lane r holds row r; column j of L broadcast by readlane
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    const double d = readlane_d(a[j], j);
+    bad |= !(d > 0.0);
+    const double inv = rsqrt_nr(d);
+    dinv[j] = inv;
+    a[j] = (lane > j) ? a[j] * inv : ((lane == j) ? d * inv : 0.0);
+#pragma unroll
+    for (int cc = j + 1; cc < 7; cc++) {
+      const double lcj = readlane_d(a[j], cc);
+      if (lane >= cc) a[cc] -= a[j] * lcj;
+    }
+  }
+  // strictly-lower entries of L_kk as wave-uniform values
+#pragma unroll
+  for (int rr = 1; rr < 7; rr++)
+#pragma unroll
+    for (int mm = 0; mm < rr; mm++) Lr[rr][mm] = readlane_d(a[mm], rr);
+  // W = L^-1: lane c computes column c
+  double w[7];
+#pragma unroll
+  for (int rr = 0; rr < 7; rr++) {
+    double acc = (rr == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * w[mm];
+    w[rr] = (rr >= lane) ? acc * dinv[rr] : 0.0;
+  }
+  if (lane < 7) {
+#pragma unroll
+    for (int qq = 0; qq < 7; qq++) {
+      Lb[(size_t)k * 49 + lane * 7 + qq] = (qq <= lane) ? a[qq] : 0.0;  // row `lane` of L_kk
+      Di[(size_t)k * 49 + qq * 7 + lane] = w[qq];                       // column `lane` of W
+    }
+  }
+  return bad;
+}
+
+// y_k = L_kk^-1 b (lane r < 7 holds b_r), stored to yk_out[0..7)
+__device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7][7], const double (&dinv)[7],
+                                                double *yk_out, int lane) {
+  double yk[7];
+#pragma unroll
+  for (int rr = 0; rr < 7; rr++) {
+    double acc = readlane_d(bb, rr);
+#pragma unroll
+    for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * yk[mm];
+    yk[rr] = acc * dinv[rr];
+  }
+  if (lane < 7) {
+    double yo = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < 7; qq++) yo = (qq == lane) ? yk[qq] : yo;
+    yk_out[lane] = yo;
+  }
+}
+
 // STORE: 1 = factor, plan and flags in LDS (small graphs); 2 = factor and
 // flags in LDS, plan in global memory; 0 = factor in global memory, flags and
 // the per-wave stage areas in LDS (large graphs).
@@ -1242,7 +1314,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   constexpr bool IN_LDS = STORE != 0;
   constexpr bool STAGE = STORE == 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int fail_s, next_item, next_col;
+  __shared__ int fail_s, next_item, next_col, next_b0;
   __shared__ float nrm[16];
   __shared__ double scratch[16][64];
   const int m = D.m, S = D.S;
@@ -1327,7 +1399,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
     for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
   }
-  if (tid == 0) fail_s = 0, next_item = 0, next_col = 0;
+  if (tid == 0) fail_s = 0, next_item = 0, next_col = 0, next_b0 = 0;
   __syncthreads();
   M3S_TS(1)
 
@@ -1376,51 +1448,8 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
       M3S_IT(1)
-      // entry layout -> row layout through the wave's scratch
-      if (act49) scr[lane] = v;
-      wave_lds_fence();
-      double a[7];
-#pragma unroll
-      for (int qq = 0; qq < 7; qq++) a[qq] = scr[l7 + qq];
-      wave_lds_fence();
-      // Cholesky: lane r holds row r; column j of L broadcast by readlane
-      bool bad = false;
-      double dinv[7];  // 1 / L_jj
-#pragma unroll
-      for (int j = 0; j < 7; j++) {
-        const double d = readlane_d(a[j], j);
-        bad |= !(d > 0.0);
-        const double inv = rsqrt_nr(d);
-        dinv[j] = inv;
-        a[j] = (lane > j) ? a[j] * inv : ((lane == j) ? d * inv : 0.0);
-#pragma unroll
-        for (int cc = j + 1; cc < 7; cc++) {
-          const double lcj = readlane_d(a[j], cc);
-          if (lane >= cc) a[cc] -= a[j] * lcj;
-        }
-      }
-      // strictly-lower entries of L_kk as wave-uniform values
-      double Lr[7][7];
-#pragma unroll
-      for (int rr = 1; rr < 7; rr++)
-#pragma unroll
-        for (int mm = 0; mm < rr; mm++) Lr[rr][mm] = readlane_d(a[mm], rr);
-      // W = L^-1: lane c computes column c
-      double w[7];
-#pragma unroll
-      for (int rr = 0; rr < 7; rr++) {
-        double acc = (rr == lane) ? 1.0 : 0.0;
-#pragma unroll
-        for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * w[mm];
-        w[rr] = (rr >= lane) ? acc * dinv[rr] : 0.0;
-      }
-      if (lane < 7) {
-#pragma unroll
-        for (int qq = 0; qq < 7; qq++) {
-          Lb[(size_t)k * 49 + lane * 7 + qq] = (qq <= lane) ? a[qq] : 0.0;  // row `lane` of L_kk
-          Di[(size_t)k * 49 + qq * 7 + lane] = w[qq];                       // column `lane` of W
-        }
-      }
+      double Lr[7][7], dinv[7];
+      const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, Lr, dinv);
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1430,20 +1459,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       double bb = y[k * 7 + lane7];
       for (int pi = p0; pi < p1; pi++) bb += D.parts[(size_t)pi * 56 + 49 + lane7];
       M3S_POLL(q0, q1, flag_set(&ydone[dtr_p[q]]), (bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, qa, qb, y, lane7, lane49, lane, stg)));
-      double yk[7];
-#pragma unroll
-      for (int rr = 0; rr < 7; rr++) {
-        double acc = readlane_d(bb, rr);
-#pragma unroll
-        for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * yk[mm];
-        yk[rr] = acc * dinv[rr];
-      }
-      if (lane < 7) {
-        double yo = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < 7; qq++) yo = (qq == lane) ? yk[qq] : yo;
-        y[k * 7 + lane] = yo;
-      }
+      fwd_solve_store(bb, Lr, dinv, y + (size_t)k * 7, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&ydone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       M3S_IT(2)
@@ -1483,6 +1499,161 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   if (tid == 0) printf("factor done fail %d\n", fail_s);
 #endif
 
+  // 1b. dense tail: the top clique of the elimination tree (nc columns from
+  // c0 whose structure is every later column) factored right-looking,
+  // bulk-synchronously, after the dataflow items (which cover columns < c0,
+  // including the border blocks L_ik, i >= c0 > k, and all y_p, p < c0).
+  M3S_TS(5)
+  if (D.nc > 0) {
+    const int32_t *clq = pl + D.off[28];
+    const int nc = clq[0], c0 = clq[1];
+    const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
+    // B0: border updates (columns p < c0) of every tail block and tail RHS
+    const int nt0 = nc * (nc + 1) / 2;
+    for (;;) {
+      const int t = wave_ticket(&next_b0);
+      if (t >= nt0) break;
+      int ci = 0, rem = t;  // t -> (ci, ri), ci <= ri < nc, column-major
+      while (rem >= nc - ci) rem -= nc - ci, ci++;
+      const int ri = ci + rem, k = c0 + ci;
+      if (ri == ci) {
+        const int q0 = dtr_ptr[k], q1 = bend[ci * nc + ci];
+        double v = Lb[(size_t)k * 49 + lane49];
+        v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+        double bb = y[k * 7 + lane7];
+        bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+        if (act49) Lb[(size_t)k * 49 + lane] = v;
+        if (lane < 7) y[k * 7 + lane] = bb;
+      } else {
+        const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
+        const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
+        double v = Lb[(size_t)dst * 49 + lane49];
+        v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+        if (act49) Lb[(size_t)dst * 49 + lane] = v;
+      }
+    }
+    __syncthreads();
+    M3S_TS(6)
+    // B1: per tail column k: L_kk, W_k, y_k (one wave) | L_ik = A_ik W_k^T,
+    // y_i -= L_ik y_k (a wave per row; global factors also copy column k into
+    // an LDS panel) | A_ij -= L_ik L_jk^T (kStage destination blocks per wave,
+    // their loads in flight together). Tail slots are arithmetic: the
+    // off-diagonal blocks of the tail are the last slots, column-major.
+    const int cbase = S - nc * (nc - 1) / 2;
+    double *panel = stg - (size_t)wave * kStageDoubles;  // the stage areas (global factors only)
+#if M3S_LLT_TIMING  // experiment: wave 0's cycles in B1 sub-steps, summed over the tail
+    int64_t bt[7] = {0, 0, 0, 0, 0, 0, 0}, t_0 = clock64();
+#define M3S_BT(i) { const int64_t t_ = clock64(); bt[i] += t_ - t_0; t_0 = t_; }
+#else
+#define M3S_BT(i)
+#endif
+    for (int ci = 0; ci < nc; ci++) {
+      const int k = c0 + ci;
+      const int col0 = cbase + ci * nc - ci * (ci + 1) / 2;  // slot of L_{k+1, k}
+      if (wave == 0) {
+        const double v = Lb[(size_t)k * 49 + lane49];
+        double Lr[7][7], dinv[7];
+        const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, Lr, dinv);
+        if (bad && lane == 0) fail_s = 1;
+        fwd_solve_store(y[k * 7 + lane7], Lr, dinv, y + (size_t)k * 7, lane);
+      }
+      M3S_BT(0)
+      __syncthreads();
+      M3S_BT(1)
+      const int nr = nc - ci - 1;
+      for (int rr = wave; rr < nr; rr += NW) {
+        const int dst = col0 + rr;
+        const double av = Lb[(size_t)dst * 49 + lane49];
+        if (act49) scr[lane] = av;
+        wave_lds_fence();
+        double x = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * Di[(size_t)k * 49 + c7 + mm];
+        wave_lds_fence();
+        if (act49) {
+          Lb[(size_t)dst * 49 + lane] = x, scr[lane] = x;
+          if (STAGE) panel[rr * 49 + lane] = x;
+        }
+        wave_lds_fence();
+        double yv = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) yv += scr[l7 + mm] * y[k * 7 + mm];
+        if (lane < 7) y[(k + 1 + rr) * 7 + lane] -= yv;
+        wave_lds_fence();
+      }
+      M3S_BT(2)
+      __syncthreads();
+      M3S_BT(3)
+      const double *Pk = STAGE ? panel : Lb + (size_t)col0 * 49;  // L_{k+1+rr, k} at Pk + 49 rr
+      const int npair = nr * (nr + 1) / 2;
+      for (int b0 = wave * kStage; b0 < npair; b0 += NW * kStage) {
+        const int nb = (npair - b0 < kStage) ? npair - b0 : kStage;
+        int cc = 0, rem = b0;  // first pair -> (rr >= cc) of the trailing nr x nr, column-major
+        while (rem >= nr - cc) rem -= nr - cc, cc++;
+        int rr = cc + rem;
+        int ra[kStage], rb[kStage], sd[kStage];
+#pragma unroll
+        for (int bq = 0; bq < kStage; bq++) {
+          ra[bq] = rr, rb[bq] = cc;
+          // destination (k + 1 + rr, k + 1 + cc)
+          const int cj = ci + 1 + cc;
+          sd[bq] = (rr == cc) ? k + 1 + rr : cbase + cj * nc - cj * (cj + 1) / 2 + (rr - cc - 1);
+          if (bq + 1 < nb && ++rr == nr) ++cc, rr = cc;  // past the end: repeat the last pair
+        }
+        // the destination loads are branch-free (a repeated pair reloads a
+        // valid block), so the batch's loads are in flight together
+        double vd[kStage];
+#pragma unroll
+        for (int bq = 0; bq < kStage; bq++) vd[bq] = Lb[(size_t)sd[bq] * 49 + lane49];
+#pragma unroll
+        for (int bq = 0; bq < kStage; bq++)
+          if (bq < nb) {
+            const double *A = Pk + (size_t)ra[bq] * 49, *B = Pk + (size_t)rb[bq] * 49;
+            double sm = 0.0;
+#pragma unroll
+            for (int mm = 0; mm < 7; mm++) sm += A[r7 + mm] * B[c7 + mm];
+            vd[bq] -= sm;
+          }
+        if (act49) {
+#pragma unroll
+          for (int bq = 0; bq < kStage; bq++)
+            if (bq < nb) Lb[(size_t)sd[bq] * 49 + lane] = vd[bq];
+        }
+      }
+      M3S_BT(4)
+      __syncthreads();
+      M3S_BT(5)
+    }
+#if M3S_LLT_TIMING
+    if (tid == 0)
+      for (int i = 0; i < 6; i++) D.dbg[i] = bt[i];
+#endif
+    M3S_TS(7)
+    // B2: back-substitution of the tail, x_k = W_k^T y_k (one wave), then
+    // y_j -= L_kj^T x_k for the tail columns j < k (a wave per column)
+    for (int ci = nc - 1; ci >= 0; ci--) {
+      const int k = c0 + ci;
+      if (wave == 0) {
+        const double rr = y[k * 7 + lane7];
+        double xk = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) xk += Di[(size_t)k * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
+        if (lane < 7) y[k * 7 + lane] = xk;
+      }
+      __syncthreads();
+      for (int cj = wave; cj < ci; cj += NW) {
+        const int blk = cbase + cj * nc - cj * (cj + 1) / 2 + (ci - cj - 1);  // L_{k, c0 + cj}
+        double t = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) t += Lb[(size_t)blk * 49 + mm * 7 + lane7] * y[k * 7 + mm];
+        if (lane < 7) y[(c0 + cj) * 7 + lane] -= t;
+      }
+      __syncthreads();
+    }
+    for (int q = tid; q < nc; q += 1024) done2[c0 + q] = 1;
+    __syncthreads();
+  }
+
   if (fail_s) {
     fail_step(7 * m, D.dx_out, D.info, D.flags + kFlagStop, D.delta_thresh);
     return;
@@ -1497,6 +1668,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     const int t = wave_ticket(&next_col);
     if (t >= m) break;
     const int k = lev_col[m - 1 - t];
+    if (k >= m - D.nc) continue;  // dense tail: done above
 #if M3S_LLT_DEBUG
     if (lane == 0) printf("wave %d backsub t %d k %d\n", wave, t, k);
 #endif
@@ -1747,12 +1919,19 @@ int read_K(const float *K, ResidualParams &P, hipStream_t st) {
 
 // Host registry of the per-call plan (keyed by workspace): the stepwise API
 // calls prepare and solve separately.
+// smallest top clique solved as a dense tail (M3S_DENSE_TAIL_MIN overrides;
+// 0 disables it)
+inline int dense_tail_min() {
+  const char *e = std::getenv("M3S_DENSE_TAIL_MIN");
+  return e ? std::atoi(e) : kDenseTailMin;
+}
+
 struct PlanMeta {
   bool sparse = false;
   int store = 0;  // sparse_llt_kernel<STORE>
   bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
   size_t lds_bytes = 0;
-  int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0;
+  int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0, nc = 0;
   PlanImage img;  // offsets (data vector cleared after upload)
   // linearize state of this solve call: edge ranks, the task table of the
   // edge range last linearized (host copy stays alive for the async upload)
@@ -1909,11 +2088,12 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         I.off_task_dst, I.off_task_col,     I.off_task_tr_ptr, I.off_tr_a,  I.off_tr_b,
         I.off_asm_ptr,  I.off_asm_edge,     I.off_g_ptr,    I.off_g_edge,   I.off_ctask_ptr,
         I.off_items,    I.off_wave_ptr,     I.off_witems,
-        I.off_part_q0,  I.off_part_q1,      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr};
+        I.off_part_q0,  I.off_part_q1,      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr, I.off_clq};
     for (int q = 0; q < kPlanSections; q++) D.off[q] = (int)offs[q];
     D.n_items = meta.n_items;
     D.n_tasks = meta.n_tasks;
     D.n_parts = meta.n_parts;
+    D.nc = meta.nc;
     D.E = (int)a->E;
     D.asm_lds = meta.asm_lds ? 1 : 0;
     D.parts = at<double>(ws, Ly.parts);
@@ -2002,6 +2182,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
 struct PlanCacheEntry {
   int64_t N = 0, HW = 0, E = 0;
   bool dense = false;
+  int tail_min = 0;  // dense_tail_min() the plan was built with
   std::vector<int32_t> ri, rj;
   PlanMeta meta;
 };
@@ -2030,9 +2211,9 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
     SparsePlan P;
     // split long update lists only when the factor lives in global memory
     // (its products are the slow, staged ones there)
-    build_sparse_plan((int)a->N, ri, rj, P);
+    build_sparse_plan((int)a->N, ri, rj, P, 0, 0, dense_tail_min());
     if (sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) > kMaxLdsBytes)
-      build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1);
+      build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1, dense_tail_min());
     PlanImage img;
     flatten_plan(P, img);
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
@@ -2045,6 +2226,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       meta.n_items = (int)P.items.size();
       meta.n_tasks = (int)P.task_dst.size();
       meta.n_parts = (int)P.part_q0.size();
+      meta.nc = P.nc;
       // LDS plan of sparse_llt_kernel<STORE>: flags always, factor + W + y if
       // they fit, the plan too if it fits as well; else global factor with
       // per-wave stage areas
@@ -2117,7 +2299,8 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       std::lock_guard<std::mutex> g(g_cache_mu);
       for (size_t q = 0; q < g_cache.size(); q++) {
         const PlanCacheEntry &C = g_cache[q];
-        if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense && C.ri == ri && C.rj == rj) {
+        if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense &&
+            C.tail_min == dense_tail_min() && C.ri == ri && C.rj == rj) {
           meta = C.meta;
           std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
           hit = true;
@@ -2129,6 +2312,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       meta = build_plan_meta(a, Ly, ri, rj, force_dense);
       PlanCacheEntry C;
       C.N = a->N, C.HW = a->HW, C.E = E, C.dense = force_dense, C.ri = ri, C.rj = rj, C.meta = meta;
+      C.tail_min = dense_tail_min();
       std::lock_guard<std::mutex> g(g_cache_mu);
       g_cache.insert(g_cache.begin(), std::move(C));
       if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
@@ -2409,7 +2593,7 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
                               int32_t max_parts, int32_t *out, int64_t cap, int32_t *meta) {
   std::vector<int32_t> a(ri, ri + E), b(rj, rj + E);
   SparsePlan P;
-  build_sparse_plan(N, a, b, P, split, max_parts);
+  build_sparse_plan(N, a, b, P, split, max_parts, dense_tail_min());
   PlanImage I;
   flatten_plan(P, I);
   const int64_t offs[kPlanSections] = {
@@ -2418,7 +2602,7 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
       I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a,     I.off_tr_b,
       I.off_asm_ptr,  I.off_asm_edge, I.off_g_ptr,       I.off_g_edge,   I.off_ctask_ptr,
       I.off_items,    I.off_wave_ptr, I.off_witems,    I.off_part_q0,  I.off_part_q1,
-      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr};
+      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr, I.off_clq};
   if (meta) {
     meta[0] = P.m, meta[1] = P.S, meta[2] = P.levels;
     for (int k = 0; k < kPlanSections; k++) meta[3 + k] = (int32_t)offs[k];

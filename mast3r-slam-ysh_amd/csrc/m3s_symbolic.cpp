@@ -264,7 +264,7 @@ static void schedule_items(SparsePlan &P) {
 }
 
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
-                       SparsePlan &P, int split, int64_t max_parts) {
+                       SparsePlan &P, int split, int64_t max_parts, int dense_min) {
   const int m = N > 1 ? N - 1 : 0;
   const int64_t E = (int64_t)ri.size();
   P = SparsePlan();
@@ -324,6 +324,12 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   std::vector<std::vector<int>> rowst(m);
   for (int p = 0; p < m; p++)
     for (int i : st[p]) rowst[i].push_back(p);
+  // dense tail: trailing columns whose structure is every later column
+  int nc = 0;
+  while (nc < m && (int)st[m - 1 - nc].size() == nc) nc++;
+  if (dense_min <= 0 || nc < dense_min) nc = 0;
+  const int c0 = m - nc;
+  P.nc = nc;
   // left-looking updates
   P.dtr_ptr.assign(1, 0);
   for (int k = 0; k < m; k++) {
@@ -336,34 +342,59 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   P.task_lev_ptr.assign(1, 0);
   P.task_tr_ptr.assign(1, 0);
   P.ctask_ptr.assign(1, 0);
+  std::vector<int32_t> ct0(nc, 0), bend((size_t)nc * nc, 0);
+  for (int ci = 0; ci < nc; ci++) {  // DIAG border prefixes (dtr_p ascending)
+    const int k = c0 + ci;
+    int q = P.dtr_ptr[k];
+    while (q < P.dtr_ptr[k + 1] && P.dtr_p[q] < c0) q++;
+    bend[(size_t)ci * nc + ci] = q;
+  }
   for (int l = 0; l < P.levels; l++) {
     for (int t = P.lev_ptr[l]; t < P.lev_ptr[l + 1]; t++) {
       const int k = P.lev_col[t];
       P.ctask_ptr.push_back(P.ctask_ptr.back() + (int32_t)st[k].size());
-      P.items.push_back(-1 - k);
-      for (size_t q = 0; q < st[k].size(); q++) P.items.push_back((int32_t)P.task_dst.size() + (int32_t)q);
+      if (k < c0) {  // dense-tail columns are not dataflow items
+        P.items.push_back(-1 - k);
+        for (size_t q = 0; q < st[k].size(); q++) P.items.push_back((int32_t)P.task_dst.size() + (int32_t)q);
+      } else {
+        ct0[k - c0] = (int32_t)P.task_dst.size();
+      }
       for (int i : st[k]) {
         P.task_dst.push_back(sl(i, k));
         P.task_col.push_back(k);
         for (int p : rowst[k]) {
           // i in struct(p)?  (struct lists are sorted)
           if (Sb.test(p, i)) {
+            if (k >= c0 && p < c0) bend[(size_t)(k - c0) * nc + (i - c0)] = (int32_t)P.tr_a.size() + 1;
             P.tr_a.push_back(sl(i, p));
             P.tr_b.push_back(sl(k, p));
           }
         }
+        if (k >= c0 && bend[(size_t)(k - c0) * nc + (i - c0)] == 0)  // no border updates
+          bend[(size_t)(k - c0) * nc + (i - c0)] = P.task_tr_ptr.back();
         P.task_tr_ptr.push_back((int32_t)P.tr_a.size());
       }
     }
     P.task_lev_ptr.push_back((int32_t)P.task_dst.size());
   }
+  // the kernel addresses tail blocks arithmetically: off-diagonal slots of
+  // the tail columns are the last nc (nc - 1) / 2 slots, column-major
+  for (int ci = 0; ci < nc; ci++)
+    for (int ri = ci + 1; ri < nc; ri++)
+      if (P.task_dst[ct0[ci] + ri - ci - 1] != P.S - nc * (nc - 1) / 2 + ci * nc - ci * (ci + 1) / 2 + ri - ci - 1)
+        nc = -1;  // not contiguous (never expected): no dense tail
+  if (nc < 0) return build_sparse_plan(N, ri, rj, P, split, max_parts, 0);
+  P.clq.assign(1, nc);
+  P.clq.push_back(c0);
+  P.clq.insert(P.clq.end(), ct0.begin(), ct0.end());
+  P.clq.insert(P.clq.end(), bend.begin(), bend.end());
   if (split > 0) {
     // count parts first; widen the split until they fit the buffer
     auto n_parts = [&](int sp) {
       int64_t c = 0;
-      for (int k = 0; k < m; k++) c += std::max(0, (P.dtr_ptr[k + 1] - P.dtr_ptr[k] - 1) / sp);
+      for (int k = 0; k < c0; k++) c += std::max(0, (P.dtr_ptr[k + 1] - P.dtr_ptr[k] - 1) / sp);
       for (size_t t = 0; t < P.task_dst.size(); t++)
-        c += std::max(0, (P.task_tr_ptr[t + 1] - P.task_tr_ptr[t] - 1) / sp);
+        if (P.task_col[t] < c0) c += std::max(0, (P.task_tr_ptr[t + 1] - P.task_tr_ptr[t] - 1) / sp);
       return c;
     };
     while (n_parts(split) > max_parts) split *= 2;
@@ -385,8 +416,9 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     };
     // part indices are assigned target by target (DIAG targets in column
     // order, then OFF tasks in task order) so each target's parts are contiguous
-    for (int k = 0; k < m; k++) add_parts(-1 - k, P.dtr_ptr[k], P.dtr_ptr[k + 1], dparts[k]);
-    for (int t = 0; t < T; t++) add_parts(t, P.task_tr_ptr[t], P.task_tr_ptr[t + 1], oparts[t]);
+    for (int k = 0; k < c0; k++) add_parts(-1 - k, P.dtr_ptr[k], P.dtr_ptr[k + 1], dparts[k]);
+    for (int t = 0; t < T; t++)
+      if (P.task_col[t] < c0) add_parts(t, P.task_tr_ptr[t], P.task_tr_ptr[t + 1], oparts[t]);
     for (int k = 0; k < m; k++) P.dpart_ptr[k + 1] = P.dpart_ptr[k] + (int32_t)dparts[k].size();
     P.opart_ptr[0] = P.dpart_ptr[m];  // OFF parts follow the DIAG parts
     for (int t = 0; t < T; t++) P.opart_ptr[t + 1] = P.opart_ptr[t] + (int32_t)oparts[t].size();
@@ -394,6 +426,10 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     for (int l = 0; l < P.levels; l++)
       for (int pos = P.lev_ptr[l]; pos < P.lev_ptr[l + 1]; pos++) {
         const int k = P.lev_col[pos];
+        if (k >= c0) {  // dense tail
+          t += (int)st[k].size();
+          continue;
+        }
         for (int32_t pi : dparts[k]) items.push_back(T + pi);
         for (int q = 0; q < (int)st[k].size(); q++)
           for (int32_t pi : oparts[t + q]) items.push_back(T + pi);
@@ -462,6 +498,7 @@ void flatten_plan(const SparsePlan &P, PlanImage &img) {
   img.off_part_tgt = put(P.part_tgt);
   img.off_dpart_ptr = put(P.dpart_ptr);
   img.off_opart_ptr = put(P.opart_ptr);
+  img.off_clq = put(P.clq);
 }
 
 }  // namespace m3s

@@ -48,6 +48,16 @@ struct SparsePlan {
   // topological order): the kernel's waves take witems[0 .. wave_ptr[1]) in
   // this order from a shared counter
   std::vector<int32_t> wave_ptr, witems;
+  // Dense tail: the trailing nc columns whose structure is every later column
+  // (the top of the elimination tree is a dense clique) are not dataflow
+  // items; sparse_llt_kernel factors them after the items, bulk-synchronously
+  // and right-looking. clq = {nc, c0 = m - nc, ct0[nc], bend[nc * nc]}:
+  // ct0[ci] = first OFF task of column c0 + ci (task of row c0 + ri is
+  // ct0[ci] + ri - ci - 1); bend[ci * nc + ri] = end of the border prefix
+  // (updates from columns p < c0) of the target (c0 + ri, c0 + ci) in its
+  // update list (dtr list for ri == ci, tr list otherwise). nc = 0: none.
+  int nc = 0;
+  std::vector<int32_t> clq;
 };
 
 // ranks of (ii, jj) in sorted-unique(cat(ii, jj)); returns the unique count
@@ -56,8 +66,10 @@ int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int3
 
 // Build the plan for N poses (rank 0 fixed) and edges with ranks (ri, rj).
 // split > 0 enables PART items of `split` updates each (at most max_parts).
+// dense_min: smallest top clique handled as a dense tail (0: never)
+constexpr int kDenseTailMin = 24;  // measured: a win at 42 (N = 256), neutral at 18, a loss at 10
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
-                       SparsePlan &P, int split = 0, int64_t max_parts = 0);
+                       SparsePlan &P, int split = 0, int64_t max_parts = 0, int dense_min = kDenseTailMin);
 
 // Flattened int32 image of the plan (offsets of each array into it).
 struct PlanImage {
@@ -66,9 +78,9 @@ struct PlanImage {
       off_dtr_slot, off_dtr_p, off_task_lev_ptr, off_task_dst, off_task_col, off_task_tr_ptr,
       off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge, off_ctask_ptr,
       off_items, off_wave_ptr, off_witems, off_part_q0, off_part_q1, off_part_tgt, off_dpart_ptr,
-      off_opart_ptr;
+      off_opart_ptr, off_clq;
 };
-constexpr int kPlanSections = 28;
+constexpr int kPlanSections = 29;
 constexpr int kLltWaves = 16;  // waves of sparse_llt_kernel (1024 threads)
 void flatten_plan(const SparsePlan &P, PlanImage &img);
 

@@ -175,7 +175,7 @@ def version() -> str:
 PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col", "dtr_ptr",
                  "dtr_slot", "dtr_p", "task_lev_ptr", "task_dst", "task_col", "task_tr_ptr", "tr_a",
                  "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items", "wave_ptr", "witems",
-                 "part_q0", "part_q1", "part_tgt", "dpart_ptr", "opart_ptr")
+                 "part_q0", "part_q1", "part_tgt", "dpart_ptr", "opart_ptr", "clq")
 
 
 LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
@@ -191,7 +191,8 @@ def workspace_layout(N, HW, E):
 
 def sparse_plan(N, ri, rj, split=0, max_parts=0):
     """Host symbolic plan of the block-sparse LLT (diagnostics/tests; CPU only).
-    split > 0: long update lists cut into PART items (global-factor solves)."""
+    split > 0: long update lists cut into PART items (global-factor solves).
+    The dense tail (clq) follows M3S_DENSE_TAIL_MIN like the solver."""
     import numpy as np
 
     ri = np.ascontiguousarray(ri, dtype=np.int32)
@@ -210,10 +211,13 @@ def sparse_plan(N, ri, rj, split=0, max_parts=0):
     m, S, L, NP = plan["m"], plan["S"], plan["levels"], plan["n_parts"]
     T = int(plan["task_lev_ptr"][L])
     sp = NP > 0 or split > 0
+    nc = int(plan["clq"][0])  # dense-tail columns: not dataflow items
+    plan["nc"] = nc
+    n_items = (m - nc) + (T - nc * (nc - 1) // 2) + NP
     lens = {"perm": m, "col_ptr": m + 1, "lev_ptr": L + 1, "lev_col": m, "dtr_ptr": m + 1,
             "task_lev_ptr": L + 1, "task_dst": T, "task_col": T, "task_tr_ptr": T + 1,
-            "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1,
-            "items": m + T + NP, "wave_ptr": 2, "witems": m + T + NP,
+            "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1, "clq": 2 + nc + nc * nc,
+            "items": n_items, "wave_ptr": 2, "witems": n_items,
             "part_q0": NP, "part_q1": NP, "part_tgt": NP,
             "dpart_ptr": m + 1 if sp else 0, "opart_ptr": T + 1 if sp else 0}
     for name, ln in lens.items():

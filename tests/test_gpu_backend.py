@@ -280,12 +280,15 @@ def test_gn_tiled_cholesky_singular_zero_dx(be):
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
 
 
-@pytest.mark.parametrize("N", [6, 32, 70])
-def test_sparse_llt_matches_dense_llt(be, N, monkeypatch):
+@pytest.mark.parametrize("N,tail", [(6, "8"), (32, "8"), (70, "8"), (32, "3"), (70, "0"), (140, "8")])
+def test_sparse_llt_matches_dense_llt(be, N, tail, monkeypatch):
     """Block-sparse LLT (default; LDS-resident for small plans, global for
-    N=70) against the dense fallback (M3S_DENSE=1) on identical inputs."""
+    N >= 70; the top clique as a dense right-looking tail when it has at least
+    M3S_DENSE_TAIL_MIN columns, 0 = never) against the dense fallback
+    (M3S_DENSE=1) on identical inputs."""
     from mast3r_slam_amd import synthetic
 
+    monkeypatch.setenv("M3S_DENSE_TAIL_MIN", tail)
     g = synthetic.make_graph(N, 24, 32, seed=90 + N)
     T_s, dx_s, info_s = run_gpu(be, "rays", g, 3, 0.0)
     monkeypatch.setenv("M3S_DENSE", "1")

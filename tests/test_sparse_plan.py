@@ -136,11 +136,53 @@ def run_plan(p, Hjj, gj):
                 progressed = True
         assert progressed, "wave schedule deadlocks"
     assert sorted(p["witems"].tolist()) == sorted(p["items"].tolist())
-    assert sdone.all() and pdone.all()
+    nc = p["nc"]
+    c0 = m - nc
+    assert pdone.all()
+    assert all(sdone[k] for k in range(c0))  # every non-tail block is final
     done = np.zeros(m, bool)
-    done[:] = False
+    if nc:
+        # the kernel's dense tail (sparse_llt_kernel 1b), right-looking
+        clq = p["clq"]
+        ct0, bend = clq[2:2 + nc], clq[2 + nc:].reshape(nc, nc)
+
+        def slot(i, j):  # block (c0 + i, c0 + j), i >= j
+            return c0 + i if i == j else p["task_dst"][ct0[j] + i - j - 1]
+
+        for ci in range(nc):  # B0: border updates (columns < c0)
+            k = c0 + ci
+            for q in range(p["dtr_ptr"][k], bend[ci, ci]):
+                assert p["dtr_p"][q] < c0
+                A = L[p["dtr_slot"][q]]
+                L[k] -= A @ A.T
+                y[k] -= A @ y[p["dtr_p"][q]]
+            assert bend[ci, ci] == p["dtr_ptr"][k + 1] or p["dtr_p"][bend[ci, ci]] >= c0
+            for ri in range(ci + 1, nc):
+                t = ct0[ci] + ri - ci - 1
+                assert p["task_col"][t] == k and p["task_dst"][t] == slot(ri, ci)
+                for q in range(p["task_tr_ptr"][t], bend[ci, ri]):
+                    L[slot(ri, ci)] -= L[p["tr_a"][q]] @ L[p["tr_b"][q]].T
+        for ci in range(nc):  # B1
+            k = c0 + ci
+            Lk = np.linalg.cholesky(L[k])
+            L[k], W[k] = Lk, np.linalg.inv(Lk)
+            y[k] = W[k] @ y[k]
+            for ri in range(ci + 1, nc):
+                L[slot(ri, ci)] = L[slot(ri, ci)] @ W[k].T
+                y[c0 + ri] -= L[slot(ri, ci)] @ y[k]
+            for cc in range(ci + 1, nc):
+                for rr in range(cc, nc):
+                    L[slot(rr, cc)] -= L[slot(rr, ci)] @ L[slot(cc, ci)].T
+        for ci in range(nc - 1, -1, -1):  # B2
+            k = c0 + ci
+            y[k] = W[k].T @ y[k]
+            for cj in range(ci):
+                y[c0 + cj] -= L[slot(ci, cj)].T @ y[k]
+        done[c0:] = True
     for t in range(m - 1, -1, -1):
         k = p["lev_col"][t]
+        if k >= c0:
+            continue
         r = y[k].copy()
         for q in range(p["col_ptr"][k], p["col_ptr"][k + 1]):
             assert done[p["col_row"][q]]
@@ -153,9 +195,11 @@ def run_plan(p, Hjj, gj):
     return x.reshape(-1)
 
 
-@pytest.mark.parametrize("N,seed,split", [(2, 0, 0), (5, 1, 0), (32, 2, 0), (70, 3, 0), (32, 4, 2), (70, 5, 3),
-                                          (128, 6, 8)])
-def test_plan_executes_to_dense_solution(be, N, seed, split):
+@pytest.mark.parametrize("N,seed,split,tail", [(2, 0, 0, 8), (5, 1, 0, 8), (32, 2, 0, 8), (70, 3, 0, 8),
+                                               (32, 4, 2, 8), (70, 5, 3, 8), (128, 6, 8, 8), (70, 3, 0, 0),
+                                               (128, 6, 8, 0), (40, 7, 0, 3), (90, 8, 4, 4)])
+def test_plan_executes_to_dense_solution(be, N, seed, split, tail, monkeypatch):
+    monkeypatch.setenv("M3S_DENSE_TAIL_MIN", str(tail))
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 2, 2, seed=seed, edge_range=(0, 0), kf_ids=np.arange(N) * 3 + 5)
@@ -180,6 +224,8 @@ def test_plan_executes_to_dense_solution(be, N, seed, split):
     H, gv = dense_system(N, ri, rj, Hjj, gj)
     x = run_plan(p, Hjj, gj)
     np.testing.assert_allclose(x, np.linalg.solve(H, gv), rtol=1e-9, atol=1e-9)
+    if tail and N >= 70:
+        assert p["nc"] >= tail  # the dense tail is exercised
 
 
 def test_plan_fill_is_sparse_on_loop_graph(be):

@@ -22,8 +22,13 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
     for rep in range(6):
         assert be._lib.m3s_gauss_newton_rays(ctypes.byref(a), st) == 0
         torch.cuda.synchronize()
-        ts = wst[lay["flags"] + 64: lay["flags"] + 64 + 40].clone().view(torch.int64).cpu().tolist()
-        res.append([(ts[i + 1] - ts[i]) / 100.0 for i in range(4)])
+        ts = wst[lay["flags"] + 64: lay["flags"] + 64 + 64].clone().view(torch.int64).cpu().tolist()
+        us = lambda a, b: (ts[b] - ts[a]) / 100.0
+        # stamps: 0 start, 1 assembled, 5 items done, 6 tail border, 7 tail factor, 2 factor+tail, 3 backsub, 4 end
+        tail = [us(1, 5), us(5, 6), us(6, 7), us(7, 2)] if ts[7] > ts[6] > ts[5] > 0 else None
+        res.append([us(0, 1), us(1, 2), us(2, 3), us(3, 4), tail])
+        for i in (5, 6, 7):
+            wst[lay["flags"] + 64 + 8 * i: lay["flags"] + 72 + 8 * i] = 0
     r = res[-1]
     plan = be.sparse_plan(N, *[torch.searchsorted(torch.unique(torch.cat([g.ii, g.jj])), t).cpu().numpy() for t in (g.ii, g.jj)])
     import numpy as np
@@ -44,3 +49,9 @@ for N in [int(x) for x in os.environ.get("NS", "32,64,128").split(",")]:
                     print(f"    {name} items with {lo}-{hi - 1} updates: n={mk.sum()} mean {dd[mk].mean():.0f} cycles")
     print(f"N={N} levels={plan['levels']} S={plan['S']}: assembly {r[0]:.1f} us, factor {r[1]:.1f} us, "
           f"backsub {r[2]:.1f} us, retract {r[3]:.1f} us")
+    if r[4] and os.environ.get("BT") == "1":
+        bt = wst[lay["A"]: lay["A"] + 48].clone().view(torch.int64).cpu().tolist()
+        print("    wave 0 tail cycles: diag %d, barrier %d, off %d, barrier %d, trailing %d, barrier %d" % tuple(bt))
+    if r[4]:
+        print(f"    dense tail {plan['nc']} columns: items {r[4][0]:.1f} us, border {r[4][1]:.1f} us, "
+              f"tail factor {r[4][2]:.1f} us, tail backsub {r[4][3]:.1f} us")

@@ -2415,16 +2415,41 @@ __global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackS
 
 // reduce chunk partials, 7x7 fp64 Cholesky, tau = -H^-1 g, retraction,
 // convergence (nonlinear_optimizer.py:5-25), outputs.
-__global__ void __launch_bounds__(64) track_solve_kernel(const float *__restrict__ partials, int64_t chunks,
-                                                         TrackState *st, int32_t *info, float rel_error,
-                                                         float delta_norm, float *T_WCf_out,
-                                                         float *T_CkCf_out) {
+constexpr int kTrackSolveThreads = 256;
+__global__ void __launch_bounds__(kTrackSolveThreads) track_solve_kernel(const float *__restrict__ partials,
+                                                                         int64_t chunks, TrackState *st,
+                                                                         int32_t *info, float rel_error,
+                                                                         float delta_norm, float *T_WCf_out,
+                                                                         float *T_CkCf_out) {
   if (st->done) return;
-  __shared__ double s[kNP];
-  const int t = threadIdx.x;
+  // fp64 sums of the chunk partials: thread t adds chunks t, t + 256, ... (all
+  // 36 values of a chunk are loaded together), then a fixed tree over the
+  // threads (wave butterfly, then the 4 waves in order): deterministic, and
+  // every load is in flight at once instead of one dependent chain per value
+  __shared__ double s[kNP], wpart[kTrackSolveThreads / 64][kNP];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double acc[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) acc[k] = 0.0;
+  for (int64_t c = t; c < chunks; c += kTrackSolveThreads) {
+    const float4 *p4 = reinterpret_cast<const float4 *>(partials + (size_t)c * kNP);
+#pragma unroll
+    for (int q = 0; q < kNP / 4; q++) {
+      const float4 v = p4[q];
+      acc[4 * q] += (double)v.x, acc[4 * q + 1] += (double)v.y;
+      acc[4 * q + 2] += (double)v.z, acc[4 * q + 3] += (double)v.w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kNP; k++) {
+    const double v = wave_sum(acc[k]);
+    if (lane == 0) wpart[wv][k] = v;
+  }
+  __syncthreads();
   if (t < kNP) {
     double a = 0.0;
-    for (int64_t c = 0; c < chunks; c++) a += (double)partials[(size_t)c * kNP + t];
+#pragma unroll
+    for (int w = 0; w < kTrackSolveThreads / 64; w++) a += wpart[w][t];
     s[t] = a;
   }
   __syncthreads();
@@ -2525,7 +2550,7 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
                    vec_ok(a->valid, 4);
   for (int it = 0; it < a->max_iters; it++) {
     if ((rc = dispatch_linearize<true>(mode, L, L.chunks, vec, 0, st))) return rc;
-    track_solve_kernel<<<1, 64, 0, st>>>(partials, L.chunks, ts, a->info, a->rel_error, a->delta_norm,
+    track_solve_kernel<<<1, kTrackSolveThreads, 0, st>>>(partials, L.chunks, ts, a->info, a->rel_error, a->delta_norm,
                                          a->T_WCf_out, a->T_CkCf_out);
     if ((rc = launch_ok())) return rc;
     if (a->sync_every > 0 && (it + 1) % a->sync_every == 0 && it + 1 < a->max_iters) {

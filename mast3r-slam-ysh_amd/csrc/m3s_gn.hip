@@ -146,6 +146,18 @@ inline T *at(void *base, size_t off) {
   return reinterpret_cast<T *>(static_cast<char *>(base) + off);
 }
 
+// tracker state (workspace, one per call): the relative pose being refined,
+// the convergence state, and the chunk arrival counter of the fused solve
+struct TrackState {
+  float T_rel[8];   // T_CkCf
+  float T_WCk[8];
+  double old_cost;
+  int32_t done;
+  uint32_t arrive;  // linearize chunks arrived (all iterations of the call)
+};
+struct LinArgs;
+__device__ void track_solve_block(const LinArgs &A);
+
 // ------------------------------------------------------------- linearize --
 struct LinArgs {
   const float *Twc;        // backend: poses (rank order)
@@ -164,6 +176,10 @@ struct LinArgs {
   float *partials;         // [task][36]
   uint32_t *edge_cnt;      // non-null: the last chunk of an edge to finish also finalizes it into fin
   double *fin;             // [E][kFin] per-edge blocks M L M^T, M g (fused finalize)
+  TrackState *track;       // tracker: the last chunk of an iteration runs the 7x7 solve (else null)
+  int32_t *info;           // tracker outputs / convergence rule
+  float *T_WCf_out, *T_CkCf_out;
+  float rel_error, delta_norm;
   int64_t HW, edge_begin, chunks, chunk_pix;
   ResidualParams P;
 };
@@ -368,6 +384,24 @@ __device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64
   finalize_edge(esl, A.Twc + 8 * (size_t)A.rank_i[e], A.fin + (size_t)e * kFin);
 }
 
+// Fused tracker solve: the iteration's last chunk to arrive (ticket =
+// chunks - 1 mod chunks; the counter runs over the call's iterations and is
+// zeroed by track_init_kernel) reduces the partials and updates the pose.
+__device__ __forceinline__ void track_tail(const LinArgs &A) {
+  __shared__ int last_t;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's sc1 partial is stored
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t ch = (uint32_t)A.chunks;
+    const uint32_t old = __hip_atomic_fetch_add(&A.track->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_t = (old % ch) == ch - 1;
+  }
+  __syncthreads();
+  if (!last_t) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other chunks' partials, not stale L1 lines
+  track_solve_block(A);
+}
+
 // WPACK: also store the target-side planes for the packed kernel (first GN
 // iteration of a solve call).
 template <int MODE, bool TRACK, bool VEC, bool WPACK>
@@ -475,6 +509,7 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
   acc.fold(sums);
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
+  if (TRACK && A.track) track_tail(A);
 }
 
 // Later GN iterations of a solve call: target-side inputs from the planes the
@@ -2388,13 +2423,6 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
 }
 
 // --------------------------------------------------------------- tracker --
-struct TrackState {
-  float T_rel[8];   // T_CkCf
-  float T_WCk[8];
-  double old_cost;
-  int32_t done;
-  int32_t pad;
-};
 
 constexpr size_t kTrackStateOff = 0;
 inline size_t track_partials_off() { return 256; }
@@ -2408,6 +2436,7 @@ __global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackS
   store_sim3(st->T_WCk, Tk);
   st->old_cost = __builtin_inf();
   st->done = 0;
+  st->arrive = 0;
   for (int k = 0; k < 8; k++) info[k] = 0;
   store_sim3(T_CkCf_out, R);
   store_sim3(T_WCf_out, Tf);
@@ -2415,13 +2444,14 @@ __global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackS
 
 // reduce chunk partials, 7x7 fp64 Cholesky, tau = -H^-1 g, retraction,
 // convergence (nonlinear_optimizer.py:5-25), outputs.
-constexpr int kTrackSolveThreads = 256;
-__global__ void __launch_bounds__(kTrackSolveThreads) track_solve_kernel(const float *__restrict__ partials,
-                                                                         int64_t chunks, TrackState *st,
-                                                                         int32_t *info, float rel_error,
-                                                                         float delta_norm, float *T_WCf_out,
-                                                                         float *T_CkCf_out) {
-  if (st->done) return;
+constexpr int kTrackSolveThreads = 256;  // = the linearize block (the fused solve runs in one)
+__device__ void track_solve_block(const LinArgs &A) {
+  const float *__restrict__ partials = A.partials;
+  const int64_t chunks = A.chunks;
+  TrackState *st = A.track;
+  int32_t *info = A.info;
+  const float rel_error = A.rel_error, delta_norm = A.delta_norm;
+  float *T_WCf_out = A.T_WCf_out, *T_CkCf_out = A.T_CkCf_out;
   // fp64 sums of the chunk partials: thread t adds chunks t, t + 256, ... (all
   // 36 values of a chunk are loaded together), then a fixed tree over the
   // threads (wave butterfly, then the 4 waves in order): deterministic, and
@@ -2459,10 +2489,17 @@ __global__ void __launch_bounds__(kTrackSolveThreads) track_solve_kernel(const f
     for (int c = 0; c < 7; c++) H[a][c] = s[kL + tri(a < c ? a : c, a < c ? c : a)];
   for (int a = 0; a < 7; a++) g[a] = s[kG + a];
   const double cost = 0.5 * s[kCost];
+  // one thread, fully unrolled; 1/L_kk by rsqrt + 2 Newton steps (no IEEE
+  // sqrt / division sequences on the serial chain)
+  double dinv[7];
+#pragma unroll
   for (int a = 0; a < 7; a++)
+#pragma unroll
     for (int c = 0; c < 7; c++) L[a][c] = 0.0;
+#pragma unroll
   for (int k = 0; k < 7; k++) {
     double d = H[k][k];
+#pragma unroll
     for (int p = 0; p < k; p++) d -= L[k][p] * L[k][p];
     if (!(d > 0.0)) {  // torch.linalg.cholesky raises -> tracking failure
       info[M3S_INFO_SOLVE_FAIL] = 1;
@@ -2470,23 +2507,30 @@ __global__ void __launch_bounds__(kTrackSolveThreads) track_solve_kernel(const f
       st->done = 1;
       return;
     }
-    L[k][k] = sqrt(d);
+    dinv[k] = rsqrt_nr(d);
+    L[k][k] = d * dinv[k];
+#pragma unroll
     for (int i = k + 1; i < 7; i++) {
       double v = H[i][k];
+#pragma unroll
       for (int p = 0; p < k; p++) v -= L[i][p] * L[k][p];
-      L[i][k] = v / L[k][k];
+      L[i][k] = v * dinv[k];
     }
   }
   // tau = H^-1 (-g): kernel g = sum w e J with e = pred - meas  (tracker.py:165-169)
+#pragma unroll
   for (int i = 0; i < 7; i++) {
     double v = -g[i];
+#pragma unroll
     for (int p = 0; p < i; p++) v -= L[i][p] * y[p];
-    y[i] = v / L[i][i];
+    y[i] = v * dinv[i];
   }
+#pragma unroll
   for (int i = 6; i >= 0; i--) {
     double v = y[i];
+#pragma unroll
     for (int p = i + 1; p < 7; p++) v -= L[p][i] * x[p];
-    x[i] = v / L[i][i];
+    x[i] = v * dinv[i];
   }
   float tau[7];
   float n2 = 0.0f;
@@ -2546,13 +2590,14 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   L.chunks = chunks_for(a->HW, 1);
   L.chunk_pix = chunk_pixels(a->HW, L.chunks);
   L.P = P;
+  L.track = ts;  // one launch per iteration: the last chunk runs the solve
+  L.info = a->info;
+  L.T_WCf_out = a->T_WCf_out, L.T_CkCf_out = a->T_CkCf_out;
+  L.rel_error = a->rel_error, L.delta_norm = a->delta_norm;
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xf, 16) && vec_ok(a->Xk, 16) && vec_ok(a->Qk, 16) &&
                    vec_ok(a->valid, 4);
   for (int it = 0; it < a->max_iters; it++) {
     if ((rc = dispatch_linearize<true>(mode, L, L.chunks, vec, 0, st))) return rc;
-    track_solve_kernel<<<1, kTrackSolveThreads, 0, st>>>(partials, L.chunks, ts, a->info, a->rel_error, a->delta_norm,
-                                         a->T_WCf_out, a->T_CkCf_out);
-    if ((rc = launch_ok())) return rc;
     if (a->sync_every > 0 && (it + 1) % a->sync_every == 0 && it + 1 < a->max_iters) {
       int32_t done = 0;
       if (hipMemcpyAsync(&done, &ts->done, sizeof done, hipMemcpyDeviceToHost, st) != hipSuccess)

@@ -322,9 +322,70 @@ __device__ __forceinline__ void finalize_edge(const double *es, const float *Ti,
 // Each lane owns 4 consecutive pixels (one 16-B vector per stream); a wave
 // sweeps 256 pixels per trip, a block 1024.
 // 36 per-thread sums -> one block partial
+#ifndef M3S_XREDUCE
+#define M3S_XREDUCE 1
+#endif
+// Transposed wave reduction of N values: each butterfly step (xor 32, 16,
+// ..., 1) a lane keeps one half of its values and sends the other half to its
+// partner, so the count halves every step: 18 + 9 + 5 + 3 + 2 + 1 = 38
+// shuffles for 36 values instead of 36 x 6. Lane l ends with the full sum of
+// value index `idx` (valid when the path never took a padding slot).
+template <int N, int M>
+__device__ __forceinline__ void xreduce_step(const float (&v)[N], float (&o)[(N + 1) / 2], bool hi) {
+  constexpr int H = (N + 1) / 2;
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    const float lo_v = v[i];
+    const float hi_v = (i + H < N) ? v[i + H] : 0.0f;
+    const float keep = hi ? hi_v : lo_v, send = hi ? lo_v : hi_v;
+    o[i] = keep + __shfl_xor(send, M, 64);
+  }
+}
+__device__ __forceinline__ float xreduce36(const float (&v)[kNP], int lane, int &idx, bool &valid) {
+  float a[18], b[9], c[5], d[3], e[2], f[1];
+  xreduce_step<36, 32>(v, a, lane & 32);
+  xreduce_step<18, 16>(a, b, lane & 16);
+  xreduce_step<9, 8>(b, c, lane & 8);
+  xreduce_step<5, 4>(c, d, lane & 4);
+  xreduce_step<3, 2>(d, e, lane & 2);
+  xreduce_step<2, 1>(e, f, lane & 1);
+  // the value index a lane ends with: array sizes 36, 18, 9, 5, 3, 2 (the
+  // halves H are compile-time); r = real (non-padding) values on the path
+  int base = 0, r = kNP, sz = kNP;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const int h = (sz + 1) / 2;
+    if (lane & m)
+      base += h, r = r > h ? r - h : 0;
+    else
+      r = r < h ? r : h;
+    sz = h;
+  }
+  idx = base;
+  valid = r == 1;
+  return f[0];
+}
+
 __device__ __forceinline__ void store_partial(const float *acc, float *out) {
 #if M3S_LDS_REDUCE
   block_reduce_store(acc, out);
+#elif M3S_XREDUCE
+  __shared__ float red[kThreads / 64][kNP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float v[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) v[k] = acc[k];
+  int idx;
+  bool valid;
+  const float s = xreduce36(v, lane, idx, valid);
+  if (valid) red[wave][idx] = s;
+  __syncthreads();
+  if (threadIdx.x < kNP) {
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) t += red[w][threadIdx.x];
+    store_sc1(out + threadIdx.x, t);
+  }
 #else
   // wave64 butterfly, then the 4 waves through LDS
   __shared__ float red[kThreads / 64][kNP];

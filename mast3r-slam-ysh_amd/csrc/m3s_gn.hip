@@ -330,19 +330,20 @@ __device__ __forceinline__ void finalize_edge(const double *es, const float *Ti,
 // partner, so the count halves every step: 18 + 9 + 5 + 3 + 2 + 1 = 38
 // shuffles for 36 values instead of 36 x 6. Lane l ends with the full sum of
 // value index `idx` (valid when the path never took a padding slot).
-template <int N, int M>
-__device__ __forceinline__ void xreduce_step(const float (&v)[N], float (&o)[(N + 1) / 2], bool hi) {
+template <int N, int M, typename T>
+__device__ __forceinline__ void xreduce_step(const T (&v)[N], T (&o)[(N + 1) / 2], bool hi) {
   constexpr int H = (N + 1) / 2;
 #pragma unroll
   for (int i = 0; i < H; i++) {
-    const float lo_v = v[i];
-    const float hi_v = (i + H < N) ? v[i + H] : 0.0f;
-    const float keep = hi ? hi_v : lo_v, send = hi ? lo_v : hi_v;
+    const T lo_v = v[i];
+    const T hi_v = (i + H < N) ? v[i + H] : T(0);
+    const T keep = hi ? hi_v : lo_v, send = hi ? lo_v : hi_v;
     o[i] = keep + __shfl_xor(send, M, 64);
   }
 }
-__device__ __forceinline__ float xreduce36(const float (&v)[kNP], int lane, int &idx, bool &valid) {
-  float a[18], b[9], c[5], d[3], e[2], f[1];
+template <typename T>
+__device__ __forceinline__ T xreduce36(const T (&v)[kNP], int lane, int &idx, bool &valid) {
+  T a[18], b[9], c[5], d[3], e[2], f[1];
   xreduce_step<36, 32>(v, a, lane & 32);
   xreduce_step<18, 16>(a, b, lane & 16);
   xreduce_step<9, 8>(b, c, lane & 8);
@@ -2531,11 +2532,10 @@ __device__ void track_solve_block(const LinArgs &A) {
       acc[4 * q + 2] += (double)v.z, acc[4 * q + 3] += (double)v.w;
     }
   }
-#pragma unroll
-  for (int k = 0; k < kNP; k++) {
-    const double v = wave_sum(acc[k]);
-    if (lane == 0) wpart[wv][k] = v;
-  }
+  int xi;
+  bool xv;
+  const double xs = xreduce36(acc, lane, xi, xv);  // transposed wave reduction (store_partial)
+  if (xv) wpart[wv][xi] = xs;
   __syncthreads();
   if (t < kNP) {
     double a = 0.0;

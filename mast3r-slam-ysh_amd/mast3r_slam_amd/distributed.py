@@ -153,6 +153,28 @@ class ShardedGN:
             self.ops.solve(es)
         return [self.ops.dx]
 
+    def solve_timed(self, max_iter: int, delta_thresh: float, stream):
+        """solve() with a HIP event pair on `stream` around every linearize
+        launch (the kernel plus its small per-edge reduce, in the solve's own
+        launch pattern). Returns the per-iteration durations in ms."""
+        self.ops.prepare(delta_thresh)
+        evs = []
+        for _ in range(int(max_iter)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            if self.ee > self.eb:
+                self.ops.linearize(self.eb, self.ee, self.es_loc)
+            e1.record(stream)
+            evs.append((e0, e1))
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.es_all, self.es_loc, group=self.group)
+                es = self.es_all
+            else:
+                es = self.es_loc
+            self.ops.solve(es)
+        torch.cuda.synchronize()
+        return [a.elapsed_time(b) for a, b in evs]
+
     def linearize_only(self):
         """Timing hook: just the linearize kernel on this rank's slice."""
         if self.ee > self.eb:

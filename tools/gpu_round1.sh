@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 cd $R
 echo "torch import"; timeout -k 10 300 python -c "import torch; print(torch.cuda.is_available())" && timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
+echo "smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || { echo "smoke failed"; exit 1; }
 timeout -k 10 600 python bench.py > $OUT/bench1.json 2> $OUT/bench1.err || { echo "bench failed"; tail -30 $OUT/bench1.err; exit 1; }
 cat $OUT/bench1.json
 cd /tmp

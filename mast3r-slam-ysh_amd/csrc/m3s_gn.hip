@@ -84,13 +84,19 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      tasks, planes, total;
+      tasks, dtile, dx_vec, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
 
 constexpr int kTile = 64;  // tiled Cholesky tile (large systems)
 inline int64_t aug_ld(int64_t n) { return (n + 1 + kTile - 1) / kTile * kTile; }
+
+// flags of the persistent dense LLT: ntr*ntc tiles + ntc x segments + ticket/abort
+inline size_t pd_flag_bytes(int64_t ld) {
+  const size_t nt = (size_t)(ld / 32);
+  return sizeof(int32_t) * (nt * nt + nt + 8);
+}
 
 inline size_t edge_cnt_bytes(int64_t E) { return (sizeof(uint32_t) * (size_t)(E + 1) + 15) & ~size_t(15); }
 
@@ -134,6 +140,11 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
+  // persistent dense LLT: tile / x-segment flags + ticket, then x
+  L.dtile = off;
+  off = align_up(off + pd_flag_bytes(L.ld), 256);
+  L.dx_vec = off;
+  off = align_up(off + sizeof(double) * (size_t)L.ld, 256);
   // target-side planes of every edge (5 planes = rays, the widest mode)
   L.planes = off;
   off = align_up(off + sizeof(float) * 5 * (size_t)E * (size_t)HW, 256);
@@ -1036,6 +1047,296 @@ __global__ void __launch_bounds__(1024) backsolve_kernel(const double *__restric
   }
   __syncthreads();
   finish_step(rhs, dxs, nrm, n, Twc, N, dx_out, info, flags + kFlagStop, delta_thresh);
+}
+
+// ------------------------------------- persistent dense LLT (large graphs) --
+// For systems whose elimination tree has a large dense top (random long-range
+// loop edges at N >= ~100 KFs), the single-CU sparse LLT is bound by one CU's
+// dependent memory round trips. This kernel factors the RHS-augmented dense
+// system of assemble_kernel on the whole chip: left-looking over 32x32 fp64
+// tiles, one task per lower tile (i, j) (its updates sum_k L_ik L_jk^T on the
+// fp64 MFMA, v_mfma_f64_16x16x4f64, k ascending; then the diagonal
+// factorisation or the triangular solve against L_jj), then one task per tile
+// column of the back-substitution (contributions in fixed order i = top..j+1).
+// Tasks are drawn in a topological order from one global ticket counter, so a
+// task only ever waits for tasks drawn before it by running workgroups:
+// progress does not depend on co-residency. Completion is published per tile
+// / per x segment with an agent-scope release (every workgroup of every XCD
+// sees it after its acquire). Every sum runs in a fixed order, so the result
+// is bitwise reproducible (the sharded solve relies on identical ranks).
+// Bounded waits: a stuck flag sets `abort` and the step becomes a failure.
+#ifndef M3S_PD_SPINS
+#define M3S_PD_SPINS (1 << 22)
+#endif
+#ifndef M3S_PD_DEBUG
+#define M3S_PD_DEBUG 0
+#endif
+constexpr int kPT = 32;          // tile edge
+constexpr int kPDThreads = 256;  // 4 waves: one 16x16 MFMA output block each
+constexpr int kPDGrid = 256;     // persistent workgroups (one per CU)
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+struct PDenseArgs {
+  double *A;
+  int64_t ld;
+  int n, ntr, ntc, n_tile_tasks;
+  int32_t *tflag;  // [ntr * ntc] lower tile (i, j) final
+  int32_t *xflag;  // [ntc] x segment j published
+  int32_t *ctr;    // [0] ticket, [1] abort
+  double *x;       // [ntr * kPT] solution (0 beyond n)
+  float *Twc;
+  int64_t N;
+  float *dx_out;
+  int32_t *info;
+  int32_t *flags;
+  float delta_thresh;
+};
+
+// Called by a whole wave: every lane loads the flag and the loop condition is
+// made wave-uniform (readfirstlane), so the spin is scalar control flow (no
+// exec-masked loop around s_sleep next to the block's barriers).
+__device__ __forceinline__ bool pd_wait(int32_t *flag, int32_t *abort_flag) {
+  int spins = 0;
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+      return false;
+    if (++spins > M3S_PD_SPINS) {
+#if M3S_PD_DEBUG
+      printf("pdense: wait timeout block %d flag %p\n", (int)blockIdx.x, (void *)flag);
+#endif
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+// whole block: wave 0 waits for every flag in `fl[0..cnt)`, then all acquire
+__device__ __forceinline__ void pd_wait_block(int32_t *const *fl, int cnt, int32_t *abort_flag) {
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
+    for (int q = 0; q < cnt; q++) pd_wait(fl[q], abort_flag);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ __forceinline__ void pd_publish(int32_t *flag) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 32x32 tile (row-major in A, leading dim ld) -> LDS [32][33]
+__device__ __forceinline__ void pd_load_tile(const double *__restrict__ T, int64_t ld, double (*S)[kPT + 1]) {
+  for (int k = threadIdx.x; k < kPT * kPT / 2; k += kPDThreads) {
+    const int r = k >> 4, c = (k & 15) * 2;
+    const double2 v = *reinterpret_cast<const double2 *>(T + (size_t)r * ld + c);
+    S[r][c] = v.x;
+    S[r][c + 1] = v.y;
+  }
+}
+
+__device__ void pd_tile_task(const PDenseArgs &P, int i, int j, double (*Si)[kPT + 1], double (*Sj)[kPT + 1],
+                             double (*Sv)[kPT + 1], double *col) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int bi = w >> 1, bj = w & 1;  // this wave's 16x16 output block
+  const int64_t ld = P.ld;
+  double *Aij = P.A + (size_t)i * kPT * ld + (size_t)j * kPT;
+  int32_t *abort_flag = P.ctr + 1;
+  // ---- sum_k L_ik L_jk^T on the MFMA (k ascending, 8 k-steps of 4 per tile)
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < j; k++) {
+    int32_t *fl[2] = {P.tflag + (size_t)i * P.ntc + k, P.tflag + (size_t)j * P.ntc + k};
+    pd_wait_block(fl, i == j ? 1 : 2, abort_flag);
+    pd_load_tile(P.A + (size_t)i * kPT * ld + (size_t)k * kPT, ld, Si);
+    if (i != j) pd_load_tile(P.A + (size_t)j * kPT * ld + (size_t)k * kPT, ld, Sj);
+    __syncthreads();
+    double(*Lj)[kPT + 1] = (i == j) ? Si : Sj;
+#pragma unroll
+    for (int s = 0; s < kPT / 4; s++) {
+      const double a = Si[16 * bi + (lane & 15)][4 * s + (lane >> 4)];
+      const double b = Lj[16 * bj + (lane & 15)][4 * s + (lane >> 4)];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // ---- v = A_ij - acc into LDS (f64 MFMA C/D map: col = lane&15, row = (lane>>4) + 4 r)
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = 16 * bi + (lane >> 4) + 4 * r, cc = 16 * bj + (lane & 15);
+    Sv[row][cc] = Aij[(size_t)row * ld + cc] - acc[r];
+  }
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: tile (%d,%d) wave %d updates done\n", i, j, w);
+#endif
+  __syncthreads();
+  const int tx = t & 15, ty = t >> 4;  // 2x2 entries per thread: (ty + 16a, tx + 16b)
+  const int cmax = min(kPT, P.n - j * kPT);  // columns that are factored (augmented / padding excluded)
+  if (i == j) {
+    // right-looking Cholesky of the diagonal tile (as potrf_tile_kernel)
+    // fixed trip count and no early exit: every wave meets the same barriers
+    // whatever the data (columns >= cmax are left untouched; a non-positive
+    // pivot flags the step as failed and the rest of the tile is don't-care)
+    bool bad = false;
+    for (int c = 0; c < kPT; c++) {
+      const bool act = c < cmax;
+      const double d = Sv[c][c];
+      if (act && !(d > 0.0)) bad = true;
+      const double inv = 1.0 / sqrt(d);
+      if (act && t < kPT) col[t] = Sv[t][c] * inv;
+      __syncthreads();
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+          const int r = ty + 16 * a, q = tx + 16 * b;
+          if (act && q > c && r >= q) Sv[r][q] -= col[r] * col[q];
+        }
+      if (act && t < kPT && t >= c) Sv[t][c] = col[t];
+      __syncthreads();
+    }
+    if (bad && t == 0) __hip_atomic_store(P.flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    int32_t *fl[1] = {P.tflag + (size_t)j * P.ntc + j};
+    pd_wait_block(fl, 1, abort_flag);
+    pd_load_tile(P.A + (size_t)j * kPT * ld + (size_t)j * kPT, ld, Si);  // L_jj
+    __syncthreads();
+    // X L_jj^T = V, column by column (as trsm_tile_kernel), fixed trip count
+    for (int c = 0; c < kPT; c++) {
+      const bool act = c < cmax;
+      const double inv = 1.0 / Si[c][c];
+      if (act && t < kPT) col[t] = Sv[t][c] * inv;
+      __syncthreads();
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+          const int r = ty + 16 * a, q = tx + 16 * b;
+          if (act && q > c) Sv[r][q] -= col[r] * Si[q][c];
+        }
+      if (act && t < kPT) Sv[t][c] = col[t];
+      __syncthreads();
+    }
+  }
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: tile (%d,%d) wave %d factored\n", i, j, w);
+#endif
+  for (int k = t; k < kPT * kPT; k += kPDThreads) Aij[(size_t)(k >> 5) * ld + (k & 31)] = Sv[k >> 5][k & 31];
+  pd_publish(P.tflag + (size_t)i * P.ntc + j);
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: tile (%d,%d) wave %d published\n", i, j, w);
+#endif
+}
+
+// back-substitution of tile column j: L_jj^T x_j = y_j - sum_{i>j} L_ij^T x_i
+__device__ void pd_back_task(const PDenseArgs &P, int j, double (*Si)[kPT + 1], double (*Sv)[kPT + 1],
+                             double *xs, double *red) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int c = t & 31, rg = t >> 5;  // column c, rows 4 rg .. 4 rg + 3
+  const int64_t ld = P.ld;
+  int32_t *abort_flag = P.ctr + 1;
+  const int rn = P.n / kPT;  // tile row holding the augmented row n (y)
+  double part = 0.0;
+  for (int i = P.ntc - 1; i > j; i--) {
+    int32_t *fl[2] = {P.xflag + i, P.tflag + (size_t)i * P.ntc + j};
+    pd_wait_block(fl, 2, abort_flag);
+    const double *Lt = P.A + (size_t)i * kPT * ld + (size_t)j * kPT;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int r = 4 * rg + q;
+      part += Lt[(size_t)r * ld + c] * P.x[i * kPT + r];
+    }
+  }
+  red[t] = part;
+  int32_t *fl[2] = {P.tflag + (size_t)rn * P.ntc + j, P.tflag + (size_t)j * P.ntc + j};
+  pd_wait_block(fl, 2, abort_flag);
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: back %d wave %d waited\n", j, t >> 6);
+#endif
+  pd_load_tile(P.A + (size_t)j * kPT * ld + (size_t)j * kPT, ld, Si);
+  __syncthreads();
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: back %d wave %d loaded\n", j, t >> 6);
+#endif
+  if (t < 64) {
+    double r = 0.0, xv = 0.0;
+    if (lane < kPT) {
+      double s = 0.0;
+      for (int g = 0; g < 8; g++) s += red[g * 32 + lane];
+      r = P.A[(size_t)P.n * ld + j * kPT + lane] - s;  // y_j - sum
+    }
+    for (int cc = kPT - 1; cc >= 0; cc--) {
+      if (j * kPT + cc >= P.n) continue;  // uniform
+      const double xc = __shfl(r, cc, 64) / Si[cc][cc];
+      if (lane < cc) r -= Si[cc][lane] * xc;
+      if (lane == cc) xv = xc;
+    }
+    if (lane < kPT) {
+      const double v = (j * kPT + lane < P.n) ? xv : 0.0;
+      P.x[j * kPT + lane] = v;
+      xs[j * kPT + lane] = v;
+    }
+  }
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: back %d wave %d solved\n", j, t >> 6);
+#endif
+  pd_publish(P.xflag + j);
+#if M3S_PD_DEBUG
+  if ((t & 63) == 0) printf("pdense: back %d wave %d published\n", j, t >> 6);
+#endif
+}
+
+__global__ void __launch_bounds__(kPDThreads) pdense_llt_kernel(PDenseArgs P) {
+  if (P.flags[kFlagStop]) return;
+  __shared__ double Si[kPT][kPT + 1], Sj[kPT][kPT + 1], Sv[kPT][kPT + 1];
+  __shared__ double col[kPT], red[kPDThreads];
+  __shared__ int tk_s, last_s;
+  __shared__ float nrm[16];
+  extern __shared__ __attribute__((aligned(16))) double pd_dyn[];
+  double *xs = pd_dyn;                                                // n doubles (last task)
+  float *dxs = reinterpret_cast<float *>(pd_dyn + P.ntr * kPT);       // n floats
+  const int T = P.n_tile_tasks + P.ntc;
+  for (;;) {
+    // ticket drawn by all 64 lanes of wave 0 (one folded add of 64; ticket =
+    // old / 64): the lane-0-only form hung behind later waits on gfx950
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+      const int o = __hip_atomic_fetch_add(P.ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) tk_s = __builtin_amdgcn_readfirstlane(o) >> 6;
+    }
+    __syncthreads();
+    const int tk = __builtin_amdgcn_readfirstlane(tk_s);
+    __syncthreads();
+#if M3S_PD_DEBUG
+    if (threadIdx.x == 0) printf("pdense: block %d ticket %d of %d (n %d ntr %d ntc %d)\n", (int)blockIdx.x, tk, T, P.n, P.ntr, P.ntc);
+#endif
+    if (tk >= T) break;
+    if (tk < P.n_tile_tasks) {  // column-major lower tiles: column j holds ntr - j tiles
+      int j = 0, base = 0;
+      while (base + (P.ntr - j) <= tk) base += P.ntr - j, j++;
+      pd_tile_task(P, j + (tk - base), j, Si, Sj, Sv, col);
+    } else {
+      const int j = P.ntc - 1 - (tk - P.n_tile_tasks);
+      pd_back_task(P, j, Si, Sv, xs, red);
+      if (j == 0) {  // x_0 is the last segment: every other segment is published
+        for (int k = threadIdx.x; k < P.n; k += kPDThreads)
+          xs[k] = __hip_atomic_load(P.x + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0)
+          last_s = __hip_atomic_load(P.flags + kFlagFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                   __hip_atomic_load(P.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int failed = __builtin_amdgcn_readfirstlane(last_s);
+#if M3S_PD_DEBUG
+        if ((threadIdx.x & 63) == 0) printf("pdense: finish wave %d fail %d\n", (int)threadIdx.x >> 6, last_s);
+#endif
+        if (failed) {
+          fail_step(P.n, P.dx_out, P.info, P.flags + kFlagStop, P.delta_thresh);
+          if (threadIdx.x == 0) P.flags[kFlagFail] = 0;
+        } else {
+          finish_step(xs, dxs, nrm, P.n, P.Twc, P.N, P.dx_out, P.info, P.flags + kFlagStop, P.delta_thresh);
+        }
+      }
+    }
+  }
 }
 
 // ------------------------------------------------- block-sparse LLT ----
@@ -2025,6 +2326,7 @@ inline int dense_tail_min() {
 
 struct PlanMeta {
   bool sparse = false;
+  bool pdense = false;  // persistent multi-workgroup dense LLT (pdense_llt_kernel)
   int store = 0;  // sparse_llt_kernel<STORE>
   bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
   size_t lds_bytes = 0;
@@ -2233,6 +2535,39 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
   assemble_kernel<<<dim3((unsigned)a->N), dim3(256), 0, st>>>(
       edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, ld, A, stop);
   if ((rc = launch_ok())) return rc;
+  if (meta.pdense) {
+    const int ntr = (int)(n / kPT) + 1, ntc = (int)((n + kPT - 1) / kPT);
+    int32_t *pf = at<int32_t>(ws, Ly.dtile);
+    if (hipMemsetAsync(pf, 0, pd_flag_bytes(ld), st) != hipSuccess) return M3S_ELAUNCH;
+    PDenseArgs P;
+    P.A = A;
+    P.ld = ld;
+    P.n = (int)n;
+    P.ntr = ntr;
+    P.ntc = ntc;
+    P.n_tile_tasks = ntc * ntr - ntc * (ntc - 1) / 2;  // sum over tile columns j of (ntr - j)
+    P.tflag = pf;
+    P.xflag = pf + (size_t)ntr * ntc;
+    P.ctr = P.xflag + ntc;
+    P.x = at<double>(ws, Ly.dx_vec);
+    P.Twc = a->Twc;
+    P.N = a->N;
+    P.dx_out = dx;
+    P.info = a->info;
+    P.flags = flags;
+    P.delta_thresh = a->delta_thresh;
+    const size_t dyn = (size_t)ntr * kPT * (sizeof(double) + sizeof(float));
+    if (dyn > 48 * 1024) {
+      static std::once_flag once;
+      std::call_once(once, [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(pdense_llt_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
+      });
+    }
+    const int T = P.n_tile_tasks + ntc;
+    pdense_llt_kernel<<<dim3((unsigned)std::min(T, kPDGrid)), dim3(kPDThreads), dyn, st>>>(P);
+    return launch_ok();
+  }
   const int np = (int)n + 1;
   if (np <= kMaxSmallNp) {
     const int nbc = (np + 31) / 32;
@@ -2273,6 +2608,26 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
 
 // Per call: zero state, bring ii/jj to the host (the reference's _unique /
 // searchsorted also synchronise), rank them, build and upload the sparse plan.
+// Solver choice. M3S_SOLVER=sparse|pdense overrides. The persistent dense
+// LLT is opt-in: measured on MI355X it is correct and bitwise reproducible
+// but 2-6x slower than the sparse LLT at every size (270 us at 32 KFs, 2.5 ms
+// at 256; DESIGN.md §4 "A/B: persistent dense LLT"), so no graph size takes
+// it by default.
+constexpr int64_t kPDenseMinN = INT64_MAX;
+int solver_override() {
+  const char *e = std::getenv("M3S_SOLVER");
+  if (!e) return 0;
+  if (!strcmp(e, "sparse")) return 1;
+  if (!strcmp(e, "pdense")) return 2;
+  return 0;
+}
+bool want_pdense(int64_t N) {
+  const int o = solver_override();
+  if (o == 1) return false;
+  if (o == 2) return N > 1;
+  return N >= kPDenseMinN;
+}
+
 // Host symbolic plans of recent edge sets (the same factor graph is usually
 // solved many times: every keyframe's local/global optimisation, every bench
 // step). Keyed by (N, HW, E, dense override, remapped ranks).
@@ -2280,6 +2635,7 @@ struct PlanCacheEntry {
   int64_t N = 0, HW = 0, E = 0;
   bool dense = false;
   int tail_min = 0;  // dense_tail_min() the plan was built with
+  int solver = 0;    // solver_override() the plan was built with
   std::vector<int32_t> ri, rj;
   PlanMeta meta;
 };
@@ -2304,7 +2660,8 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
                          const std::vector<int32_t> &rj, bool force_dense) {
   PlanMeta meta;
   const int64_t E = a->E;
-  if (a->N > 1) {
+  meta.pdense = !force_dense && want_pdense(a->N);
+  if (a->N > 1 && !meta.pdense) {
     SparsePlan P;
     // split long update lists only when the factor lives in global memory
     // (its products are the slow, staged ones there)
@@ -2397,7 +2754,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       for (size_t q = 0; q < g_cache.size(); q++) {
         const PlanCacheEntry &C = g_cache[q];
         if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense &&
-            C.tail_min == dense_tail_min() && C.ri == ri && C.rj == rj) {
+            C.tail_min == dense_tail_min() && C.solver == solver_override() && C.ri == ri && C.rj == rj) {
           meta = C.meta;
           std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
           hit = true;
@@ -2410,6 +2767,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       PlanCacheEntry C;
       C.N = a->N, C.HW = a->HW, C.E = E, C.dense = force_dense, C.ri = ri, C.rj = rj, C.meta = meta;
       C.tail_min = dense_tail_min();
+      C.solver = solver_override();
       std::lock_guard<std::mutex> g(g_cache_mu);
       g_cache.insert(g_cache.begin(), std::move(C));
       if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();

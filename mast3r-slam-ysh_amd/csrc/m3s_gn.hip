@@ -1528,6 +1528,12 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int kStage = 8;                  // updates per staged batch
 constexpr int kSplitUpdates = 8;           // updates per PART item (global factors)
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
+#ifndef M3S_TAIL_TR  // dense-tail trailing update tile, in 7x7 blocks
+#define M3S_TAIL_TR 2
+#endif
+#ifndef M3S_TAIL_TC
+#define M3S_TAIL_TC 2
+#endif
 
 // v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
 template <bool STAGE, bool SAME>
@@ -1934,7 +1940,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     M3S_TS(6)
     // B1: per tail column k: L_kk, W_k, y_k (one wave) | L_ik = A_ik W_k^T,
     // y_i -= L_ik y_k (a wave per row; global factors also copy column k into
-    // an LDS panel) | A_ij -= L_ik L_jk^T (kStage destination blocks per wave,
+    // an LDS panel) | A_ij -= L_ik L_jk^T (kTR x kTC block tiles per wave,
     // their loads in flight together). Tail slots are arithmetic: the
     // off-diagonal blocks of the tail are the last slots, column-major.
     const int cbase = S - nc * (nc - 1) / 2;
@@ -1983,39 +1989,56 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       __syncthreads();
       M3S_BT(3)
       const double *Pk = STAGE ? panel : Lb + (size_t)col0 * 49;  // L_{k+1+rr, k} at Pk + 49 rr
-      const int npair = nr * (nr + 1) / 2;
-      for (int b0 = wave * kStage; b0 < npair; b0 += NW * kStage) {
-        const int nb = (npair - b0 < kStage) ? npair - b0 : kStage;
-        int cc = 0, rem = b0;  // first pair -> (rr >= cc) of the trailing nr x nr, column-major
-        while (rem >= nr - cc) rem -= nr - cc, cc++;
-        int rr = cc + rem;
-        int ra[kStage], rb[kStage], sd[kStage];
+      // trailing tiles of kTR block rows x kTC block columns (rr >= cc): each
+      // panel row is read from LDS once per tile and used for every block of
+      // the tile ((kTR + kTC) * 7 LDS reads per lane for kTR * kTC blocks
+      // instead of 14 per block)
+      constexpr int kTR = M3S_TAIL_TR, kTC = M3S_TAIL_TC, kTB = kTR * kTC;
+      const int nrt = (nr + kTR - 1) / kTR, nct = (nr + kTC - 1) / kTC;
+      int ntile = 0;
+      for (int ct = 0; ct < nct; ct++) ntile += nrt - ct * kTC / kTR;
+      for (int t = wave; t < ntile; t += NW) {
+        int ct = 0, rem = t;  // t -> (ct, rt), rt >= ct * kTC / kTR, column-major
+        while (rem >= nrt - ct * kTC / kTR) rem -= nrt - ct * kTC / kTR, ct++;
+        const int r_0 = kTR * (ct * kTC / kTR + rem), c_0 = kTC * ct;
+        int sd[kTB];
 #pragma unroll
-        for (int bq = 0; bq < kStage; bq++) {
-          ra[bq] = rr, rb[bq] = cc;
-          // destination (k + 1 + rr, k + 1 + cc)
-          const int cj = ci + 1 + cc;
-          sd[bq] = (rr == cc) ? k + 1 + rr : cbase + cj * nc - cj * (cj + 1) / 2 + (rr - cc - 1);
-          if (bq + 1 < nb && ++rr == nr) ++cc, rr = cc;  // past the end: repeat the last pair
+        for (int q = 0; q < kTB; q++) {
+          const int rr = r_0 + q / kTC, cc = c_0 + q % kTC, cj = ci + 1 + cc;
+          // destination (k + 1 + rr, k + 1 + cc); outside the triangle: a valid
+          // block is loaded (branch-free loads, all in flight) and not stored
+          sd[q] = !(rr < nr && cc <= rr) ? k + 1
+                  : (rr == cc) ? k + 1 + rr : cbase + cj * nc - cj * (cj + 1) / 2 + (rr - cc - 1);
         }
-        // the destination loads are branch-free (a repeated pair reloads a
-        // valid block), so the batch's loads are in flight together
-        double vd[kStage];
+        double vd[kTB];
 #pragma unroll
-        for (int bq = 0; bq < kStage; bq++) vd[bq] = Lb[(size_t)sd[bq] * 49 + lane49];
+        for (int q = 0; q < kTB; q++) vd[q] = Lb[(size_t)sd[q] * 49 + lane49];
+        double Bv[kTC][7];
 #pragma unroll
-        for (int bq = 0; bq < kStage; bq++)
-          if (bq < nb) {
-            const double *A = Pk + (size_t)ra[bq] * 49, *B = Pk + (size_t)rb[bq] * 49;
-            double sm = 0.0;
+        for (int bq = 0; bq < kTC; bq++) {
+          const double *B = Pk + (size_t)min(c_0 + bq, nr - 1) * 49;
 #pragma unroll
-            for (int mm = 0; mm < 7; mm++) sm += A[r7 + mm] * B[c7 + mm];
-            vd[bq] -= sm;
+          for (int mm = 0; mm < 7; mm++) Bv[bq][mm] = B[c7 + mm];
+        }
+#pragma unroll
+        for (int aq = 0; aq < kTR; aq++) {
+          const double *A = Pk + (size_t)min(r_0 + aq, nr - 1) * 49;
+          double sm[kTC];
+#pragma unroll
+          for (int bq = 0; bq < kTC; bq++) sm[bq] = 0.0;
+#pragma unroll
+          for (int mm = 0; mm < 7; mm++) {
+            const double a = A[r7 + mm];
+#pragma unroll
+            for (int bq = 0; bq < kTC; bq++) sm[bq] += a * Bv[bq][mm];
           }
+#pragma unroll
+          for (int bq = 0; bq < kTC; bq++) vd[kTC * aq + bq] -= sm[bq];
+        }
         if (act49) {
 #pragma unroll
-          for (int bq = 0; bq < kStage; bq++)
-            if (bq < nb) Lb[(size_t)sd[bq] * 49 + lane] = vd[bq];
+          for (int q = 0; q < kTB; q++)
+            if (r_0 + q / kTC < nr && c_0 + q % kTC <= r_0 + q / kTC) Lb[(size_t)sd[q] * 49 + lane] = vd[q];
         }
       }
       M3S_BT(4)

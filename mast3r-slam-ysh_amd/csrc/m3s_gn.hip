@@ -1528,6 +1528,9 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int kStage = 8;                  // updates per staged batch
 constexpr int kSplitUpdates = 8;           // updates per PART item (global factors)
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
+#ifndef M3S_MFMA_PRODUCTS  // staged block products on the f64 MFMA
+#define M3S_MFMA_PRODUCTS 0
+#endif
 #ifndef M3S_TAIL_TR  // dense-tail trailing update tile, in 7x7 blocks
 #define M3S_TAIL_TR 2
 #endif
@@ -1563,6 +1566,51 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
     }
     return v;
   }
+#if M3S_MFMA_PRODUCTS
+  // sum_q A_q B_q^T as one K = 7 nq product on the f64 MFMA: the A_q (B_q)
+  // concatenate along k; lane l holds A[row l&15][k 4s + (l>>4)] and
+  // B[k 4s + (l>>4)][col l&15] = B_q(col, kk) (rows / cols >= 7 are zero).
+  // Operands come straight from global memory (no LDS staging); the 7x7
+  // result is moved to the entry layout through the wave's stage area once.
+  {
+    const int rc = lane & 15, kl = lane >> 4;
+    const bool live = rc < 7;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int q = q0; q < q1; q += 4) {
+      const int nb = (q1 - q < 4) ? q1 - q : 4;
+      int ia[4], ib[4];
+#pragma unroll
+      for (int bq = 0; bq < 4; bq++) {
+        ia[bq] = sa[q + (bq < nb ? bq : 0)];
+        ib[bq] = SAME ? ia[bq] : sb[q + (bq < nb ? bq : 0)];
+      }
+      double a[7], b[7];
+#pragma unroll
+      for (int st = 0; st < 7; st++) {
+        const int kg = 4 * st + kl, qq = kg / 7, kk = kg - 7 * qq;  // qq < 4
+        const int sa_ = qq == 0 ? ia[0] : qq == 1 ? ia[1] : qq == 2 ? ia[2] : ia[3];
+        const int sb_ = qq == 0 ? ib[0] : qq == 1 ? ib[1] : qq == 2 ? ib[2] : ib[3];
+        const bool on = live && qq < nb;
+        a[st] = on ? Lb[(size_t)sa_ * 49 + rc * 7 + kk] : 0.0;
+        b[st] = on ? (SAME ? a[st] : Lb[(size_t)sb_ * 49 + rc * 7 + kk]) : 0.0;
+      }
+#pragma unroll
+      for (int st = 0; st < 7; st++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], b[st], acc, 0, 0, 0);
+    }
+    // C/D map: col = lane&15, row = (lane>>4) + 4 i
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int row = kl + 4 * i;
+        if (row < 7) stg[row * 7 + rc] = acc[i];
+      }
+    }
+    wave_lds_fence();
+    v -= stg[lane49];
+    wave_lds_fence();
+    return v;
+  }
+#endif
   double *SA = stg, *SB = SAME ? stg : stg + kStage * 49;
   for (int q = q0; q < q1; q += kStage) {
     const int nb = (q1 - q < kStage) ? q1 - q : kStage;

@@ -15,3 +15,6 @@ cat $OUT/bench1.json
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/prof1 -o run --output-format csv -- python $R/bench.py --steps 5 --warmup 1 --no-cpu --no-tracker > $OUT/prof1_bench.json 2> $OUT/prof1.err || { echo "rocprof failed"; tail -30 $OUT/prof1.err; exit 1; }
 find $OUT/prof1 -name "*stats*" | head
+cd $R
+MODES=sparse timeout -k 10 300 python tools/weak_emul.py > $OUT/weak_emul.txt 2>&1 || { echo "weak_emul failed"; tail -20 $OUT/weak_emul.txt; exit 1; }
+cat $OUT/weak_emul.txt

@@ -64,6 +64,7 @@ constexpr int64_t kMaxLd = 8192;     // tiled path: back-substitution keeps x in
 // workspace-resident flags (int32)
 constexpr int kFlagStop = 0;  // set when converged / bad input: later launches no-op
 constexpr int kFlagFail = 1;  // set by the tiled Cholesky on a non-positive pivot (per iteration)
+constexpr int kFlagSplitFail = 2;  // sparse LLT split launches: a pivot failure before the tail border
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -1422,6 +1423,8 @@ struct SparseDev {
   int32_t *info;
   int32_t *flags;
   float delta_thresh;
+  int phase;  // global factors with a dense tail: 0 whole solve, 1 up to the
+              // tail border, 2 from the tail factor (border_kernel between)
 };
 
 // Broadcast lane `l` (a compile-time / wave-uniform index) of a double:
@@ -1757,6 +1760,38 @@ __device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7]
   }
 }
 
+// Border update of one dense-tail block (column-major task t over the nc x nc
+// lower triangle): the updates from the sparse columns p < c0, and for a
+// diagonal block also the tail RHS. Tasks are independent (used in
+// sparse_llt_kernel and, spread over the chip, by border_kernel).
+template <bool STAGE>
+__device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t *pl, const int *off, double *Lb,
+                                            double *y, int r7, int c7, int lane49, int lane, int lane7, bool act49,
+                                            double *stg) {
+  const int32_t *dtr_ptr = pl + off[6], *dtr_slot = pl + off[7], *dtr_p = pl + off[8], *task_dst = pl + off[10],
+                *task_tr_ptr = pl + off[12], *tr_a = pl + off[13], *tr_b = pl + off[14];
+  const int32_t *clq = pl + off[28];
+  const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
+  int ci = 0, rem = t;  // t -> (ci, ri), ci <= ri < nc, column-major
+  while (rem >= nc - ci) rem -= nc - ci, ci++;
+  const int ri = ci + rem, k = c0 + ci;
+  if (ri == ci) {
+    const int q0 = dtr_ptr[k], q1 = bend[ci * nc + ci];
+    double v = Lb[(size_t)k * 49 + lane49];
+    v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+    double bb = y[k * 7 + lane7];
+    bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+    if (act49) Lb[(size_t)k * 49 + lane] = v;
+    if (lane < 7) y[k * 7 + lane] = bb;
+  } else {
+    const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
+    const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
+    double v = Lb[(size_t)dst * 49 + lane49];
+    v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+    if (act49) Lb[(size_t)dst * 49 + lane] = v;
+  }
+}
+
 // STORE: 1 = factor, plan and flags in LDS (small graphs); 2 = factor and
 // flags in LDS, plan in global memory; 0 = factor in global memory, flags and
 // the per-wave stage areas in LDS (large graphs).
@@ -1765,6 +1800,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   if (D.flags[kFlagStop]) return;
   constexpr bool IN_LDS = STORE != 0;
   constexpr bool STAGE = STORE == 0;
+  const int phase = STAGE ? D.phase : 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int fail_s, next_item, next_col, next_b0;
   __shared__ float nrm[16];
@@ -1809,7 +1845,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
 #if M3S_LLT_TIMING  // experiment: phase timestamps (100 MHz wall clock) into flags[16..]
   int64_t *tsv = reinterpret_cast<int64_t *>(D.flags + 16);
-  if (tid == 0) tsv[0] = wall_clock64();
+  if (tid == 0 && phase != 2) tsv[0] = wall_clock64();
 #define M3S_TS(i) if (tid == 0) tsv[i] = wall_clock64();
 #else
 #define M3S_TS(i)
@@ -1822,6 +1858,12 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #endif
   double *scr = scratch[wave];
 
+  if (phase == 2) {  // after border_kernel: y and the failure flag from global memory
+    for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
+    if (tid == 0) fail_s = D.flags[kFlagSplitFail], next_col = 0;
+    __syncthreads();
+    M3S_TS(6)
+  } else {
   // 0. assembly. LDS factor with room: the per-edge blocks (fin) are staged
   // in LDS with coalesced loads, then summed per slot in edge order (the sums
   // of assemble_slots_kernel); otherwise that kernel assembled into the global
@@ -1951,6 +1993,14 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   if (tid == 0) printf("factor done fail %d\n", fail_s);
 #endif
 
+  if (phase == 1) {  // hand y and the failure flag to border_kernel / phase 2
+    for (int idx = tid; idx < m * 7; idx += 1024) const_cast<double *>(D.rhs)[idx] = y[idx];
+    if (tid == 0) D.flags[kFlagSplitFail] = fail_s;
+    M3S_TS(5)
+    return;
+  }
+  }  // phase != 2
+
   // 1b. dense tail: the top clique of the elimination tree (nc columns from
   // c0 whose structure is every later column) factored right-looking,
   // bulk-synchronously, after the dataflow items (which cover columns < c0,
@@ -1962,30 +2012,13 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
     // B0: border updates (columns p < c0) of every tail block and tail RHS
     const int nt0 = nc * (nc + 1) / 2;
-    for (;;) {
+    for (; phase == 0;) {
       const int t = wave_ticket(&next_b0);
       if (t >= nt0) break;
-      int ci = 0, rem = t;  // t -> (ci, ri), ci <= ri < nc, column-major
-      while (rem >= nc - ci) rem -= nc - ci, ci++;
-      const int ri = ci + rem, k = c0 + ci;
-      if (ri == ci) {
-        const int q0 = dtr_ptr[k], q1 = bend[ci * nc + ci];
-        double v = Lb[(size_t)k * 49 + lane49];
-        v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
-        double bb = y[k * 7 + lane7];
-        bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
-        if (act49) Lb[(size_t)k * 49 + lane] = v;
-        if (lane < 7) y[k * 7 + lane] = bb;
-      } else {
-        const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
-        const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
-        double v = Lb[(size_t)dst * 49 + lane49];
-        v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
-        if (act49) Lb[(size_t)dst * 49 + lane] = v;
-      }
+      border_task<STAGE>(t, nc, c0, pl, D.off, Lb, y, r7, c7, lane49, lane, lane7, act49, stg);
     }
     __syncthreads();
-    M3S_TS(6)
+    if (phase == 0) { M3S_TS(6) }
     // B1: per tail column k: L_kk, W_k, y_k (one wave) | L_ik = A_ik W_k^T,
     // y_i -= L_ik y_k (a wave per row; global factors also copy column k into
     // an LDS panel) | A_ij -= L_ik L_jk^T (kTR x kTC block tiles per wave,
@@ -2390,6 +2423,33 @@ int read_K(const float *K, ResidualParams &P, hipStream_t st) {
 // calls prepare and solve separately.
 // smallest top clique solved as a dense tail (M3S_DENSE_TAIL_MIN overrides;
 // 0 disables it)
+// Dense-tail border updates spread over the chip (global factors, between
+// sparse_llt_kernel phases 1 and 2): one task per wave, 4 waves per
+// workgroup, y in global memory (D.rhs, written by phase 1). The tasks are
+// independent; in the single-workgroup kernel they took ~290 us at N = 256.
+constexpr int kBorderWaves = 4;
+__global__ void __launch_bounds__(64 * kBorderWaves) border_kernel(SparseDev D) {
+  if (D.flags[kFlagStop]) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int32_t *pl = D.plan;
+  const int32_t *clq = pl + D.off[28];
+  const int nc = clq[0], c0 = clq[1], nt0 = nc * (nc + 1) / 2;
+  const int r = lane / 7, c = lane % 7;
+  const bool act49 = lane < 49;
+  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
+  const int lane7 = lane < 7 ? lane : 0;
+  double *stg = smem + (size_t)wave * kStageDoubles;
+  double *y = const_cast<double *>(D.rhs);
+  for (int t = blockIdx.x * kBorderWaves + wave; t < nt0; t += gridDim.x * kBorderWaves)
+    border_task<true>(t, nc, c0, pl, D.off, D.L, y, r7, c7, lane49, lane, lane7, act49, stg);
+}
+
+inline bool border_split() {  // M3S_BORDER_SPLIT=0: tail border inside the one-workgroup kernel (A/B)
+  const char *e = std::getenv("M3S_BORDER_SPLIT");
+  return !(e && e[0] == '0');
+}
+
 inline int dense_tail_min() {
   const char *e = std::getenv("M3S_DENSE_TAIL_MIN");
   return e ? std::atoi(e) : kDenseTailMin;
@@ -2550,6 +2610,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     }
     const PlanImage &I = meta.img;
     SparseDev D;
+    D.phase = 0;
     D.plan = at<int32_t>(ws, Ly.plan);
     D.plan_len = meta.plan_len;
     const int64_t offs[kPlanSections] = {
@@ -2591,7 +2652,15 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.store == 2)
       sparse_llt_kernel<2><<<1, 1024, meta.lds_bytes, st>>>(D);
-    else
+    else if (meta.nc > 0 && border_split()) {
+      D.phase = 1;
+      sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
+      const int nt0 = meta.nc * (meta.nc + 1) / 2;
+      border_kernel<<<(nt0 + kBorderWaves - 1) / kBorderWaves, 64 * kBorderWaves,
+                      kBorderWaves * kStageDoubles * sizeof(double), st>>>(D);
+      D.phase = 2;
+      sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
+    } else
       sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
     return launch_ok();
   }

@@ -280,7 +280,7 @@ def test_gn_tiled_cholesky_singular_zero_dx(be):
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
 
 
-@pytest.mark.parametrize("N,tail", [(6, "8"), (32, "8"), (70, "8"), (32, "3"), (70, "0"), (140, "8")])
+@pytest.mark.parametrize("N,tail", [(6, "8"), (32, "8"), (70, "8"), (32, "3"), (70, "0"), (140, "8"), (256, "24")])
 def test_sparse_llt_matches_dense_llt(be, N, tail, monkeypatch):
     """Block-sparse LLT (default; LDS-resident for small plans, global for
     N >= 70; the top clique as a dense right-looking tail when it has at least
@@ -298,6 +298,24 @@ def test_sparse_llt_matches_dense_llt(be, N, tail, monkeypatch):
     assert info_s[be.INFO_ITERS] == info_d[be.INFO_ITERS] == 3
     np.testing.assert_allclose(dx_s, dx_d, atol=1e-6 + 1e-5 * np.abs(dx_d).max())
     np.testing.assert_allclose(T_s, T_d, atol=1e-5)
+
+
+def test_border_split_is_bitwise_identical(be, monkeypatch):
+    """Global factor with a dense tail: the tail border updates spread over the
+    chip (border_kernel between sparse_llt_kernel phases 1 and 2, the default)
+    give bitwise the same poses as the one-workgroup kernel
+    (M3S_BORDER_SPLIT=0): same tasks, same per-task arithmetic."""
+    from mast3r_slam_amd import synthetic
+
+    monkeypatch.setenv("M3S_DENSE_TAIL_MIN", "8")
+    monkeypatch.setenv("M3S_SOLVER", "sparse")
+    g = synthetic.make_graph(140, 24, 32, seed=77)
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    monkeypatch.setenv("M3S_BORDER_SPLIT", "0")
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    np.testing.assert_array_equal(T_a, T_b)
+    np.testing.assert_array_equal(dx_a, dx_b)
 
 
 @pytest.mark.parametrize("N", [2, 6, 33, 70, 140, 260])

@@ -1540,6 +1540,12 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_TC
 #define M3S_TAIL_TC 2
 #endif
+#ifndef M3S_TAIL2_TR  // the same, in the phase-2 (tail-only) kernel instance
+#define M3S_TAIL2_TR 2
+#endif
+#ifndef M3S_TAIL2_TC
+#define M3S_TAIL2_TC 2
+#endif
 
 // v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
 template <bool STAGE, bool SAME>
@@ -1795,12 +1801,14 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
 // STORE: 1 = factor, plan and flags in LDS (small graphs); 2 = factor and
 // flags in LDS, plan in global memory; 0 = factor in global memory, flags and
 // the per-wave stage areas in LDS (large graphs).
-template <int STORE>
+// TAIL: the phase-2 instance (tail factor and back-substitution only), with
+// its own register budget (room for larger trailing-update tiles).
+template <int STORE, bool TAIL = false>
 __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   if (D.flags[kFlagStop]) return;
   constexpr bool IN_LDS = STORE != 0;
   constexpr bool STAGE = STORE == 0;
-  const int phase = STAGE ? D.phase : 0;
+  const int phase = TAIL ? 2 : STAGE ? D.phase : 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int fail_s, next_item, next_col, next_b0;
   __shared__ float nrm[16];
@@ -2005,7 +2013,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // c0 whose structure is every later column) factored right-looking,
   // bulk-synchronously, after the dataflow items (which cover columns < c0,
   // including the border blocks L_ik, i >= c0 > k, and all y_p, p < c0).
-  M3S_TS(5)
+  if (phase == 0) { M3S_TS(5) }
   if (D.nc > 0) {
     const int32_t *clq = pl + D.off[28];
     const int nc = clq[0], c0 = clq[1];
@@ -2074,7 +2082,8 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       // panel row is read from LDS once per tile and used for every block of
       // the tile ((kTR + kTC) * 7 LDS reads per lane for kTR * kTC blocks
       // instead of 14 per block)
-      constexpr int kTR = M3S_TAIL_TR, kTC = M3S_TAIL_TC, kTB = kTR * kTC;
+      constexpr int kTR = TAIL ? M3S_TAIL2_TR : M3S_TAIL_TR, kTC = TAIL ? M3S_TAIL2_TC : M3S_TAIL_TC,
+                    kTB = kTR * kTC;
       const int nrt = (nr + kTR - 1) / kTR, nct = (nr + kTC - 1) / kTC;
       int ntile = 0;
       for (int ct = 0; ct < nct; ct++) ntile += nrt - ct * kTC / kTR;
@@ -2659,7 +2668,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       border_kernel<<<(nt0 + kBorderWaves - 1) / kBorderWaves, 64 * kBorderWaves,
                       kBorderWaves * kStageDoubles * sizeof(double), st>>>(D);
       D.phase = 2;
-      sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
+      sparse_llt_kernel<0, true><<<1, 1024, meta.lds_bytes, st>>>(D);
     } else
       sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
     return launch_ok();
@@ -2787,6 +2796,8 @@ void set_lds_attributes_once() {
   static std::once_flag once;
   std::call_once(once, [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<0, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);

@@ -1540,6 +1540,9 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_TC
 #define M3S_TAIL_TC 2
 #endif
+#ifndef M3S_TAIL_LOOKAHEAD  // DIAG(k+1) inside step k's trailing update (dense tail)
+#define M3S_TAIL_LOOKAHEAD 1
+#endif
 #ifndef M3S_TAIL2_TR  // the same, in the phase-2 (tail-only) kernel instance
 #define M3S_TAIL2_TR 2
 #endif
@@ -1810,7 +1813,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   constexpr bool STAGE = STORE == 0;
   const int phase = TAIL ? 2 : STAGE ? D.phase : 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int fail_s, next_item, next_col, next_b0;
+  __shared__ int fail_s, next_item, next_col, next_b0, next_tile;
   __shared__ float nrm[16];
   __shared__ double scratch[16][64];
   const int m = D.m, S = D.S;
@@ -2040,18 +2043,29 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #else
 #define M3S_BT(i)
 #endif
+    // diagonal block kk: L_kk, W_k, forward step y_k (wave 0)
+    auto tail_diag = [&](int kk) {
+      const double v = Lb[(size_t)kk * 49 + lane49];
+      double Lr[7][7], dinv[7];
+      const bool bad = diag_factor(v, kk, Lb, Di, scr, lane, l7, Lr, dinv);
+      if (bad && lane == 0) fail_s = 1;
+      fwd_solve_store(y[kk * 7 + lane7], Lr, dinv, y + (size_t)kk * 7, lane);
+    };
+#if M3S_TAIL_LOOKAHEAD
+    // look-ahead: DIAG(k+1) runs on wave 0 inside step k's trailing update,
+    // right after its first tile (which holds block (k+1, k+1)), so each
+    // column costs two workgroup barriers instead of three
+    if (wave == 0) tail_diag(c0);
+    __syncthreads();
+#endif
     for (int ci = 0; ci < nc; ci++) {
       const int k = c0 + ci;
       const int col0 = cbase + ci * nc - ci * (ci + 1) / 2;  // slot of L_{k+1, k}
-      if (wave == 0) {
-        const double v = Lb[(size_t)k * 49 + lane49];
-        double Lr[7][7], dinv[7];
-        const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, Lr, dinv);
-        if (bad && lane == 0) fail_s = 1;
-        fwd_solve_store(y[k * 7 + lane7], Lr, dinv, y + (size_t)k * 7, lane);
-      }
+#if !M3S_TAIL_LOOKAHEAD
+      if (wave == 0) tail_diag(k);
       M3S_BT(0)
       __syncthreads();
+#endif
       M3S_BT(1)
       const int nr = nc - ci - 1;
       for (int rr = wave; rr < nr; rr += NW) {
@@ -2074,6 +2088,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
         if (lane < 7) y[(k + 1 + rr) * 7 + lane] -= yv;
         wave_lds_fence();
       }
+      if (tid == 0) next_tile = 64;  // trailing tiles 1.. by ticket (tile 0: wave 0)
       M3S_BT(2)
       __syncthreads();
       M3S_BT(3)
@@ -2087,7 +2102,13 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       const int nrt = (nr + kTR - 1) / kTR, nct = (nr + kTC - 1) / kTC;
       int ntile = 0;
       for (int ct = 0; ct < nct; ct++) ntile += nrt - ct * kTC / kTR;
+#if M3S_TAIL_LOOKAHEAD
+      // tile 0 holds block (k+1, k+1): wave 0 takes it, then runs DIAG(k+1),
+      // then joins the others on the ticketed remaining tiles
+      for (int t = wave == 0 ? 0 : wave_ticket(&next_tile); t < ntile; t = wave_ticket(&next_tile)) {
+#else
       for (int t = wave; t < ntile; t += NW) {
+#endif
         int ct = 0, rem = t;  // t -> (ct, rt), rt >= ct * kTC / kTR, column-major
         while (rem >= nrt - ct * kTC / kTR) rem -= nrt - ct * kTC / kTR, ct++;
         const int r_0 = kTR * (ct * kTC / kTR + rem), c_0 = kTC * ct;
@@ -2130,6 +2151,14 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
           for (int q = 0; q < kTB; q++)
             if (r_0 + q / kTC < nr && c_0 + q % kTC <= r_0 + q / kTC) Lb[(size_t)sd[q] * 49 + lane] = vd[q];
         }
+#if M3S_TAIL_LOOKAHEAD
+        if (t == 0) {  // wave 0: block (k+1, k+1) is final (this tile, rr = cc = 0)
+          wave_lds_fence();
+          M3S_BT(4)
+          tail_diag(k + 1);
+          M3S_BT(0)
+        }
+#endif
       }
       M3S_BT(4)
       __syncthreads();

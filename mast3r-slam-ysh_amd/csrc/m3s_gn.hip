@@ -1528,8 +1528,14 @@ __device__ __forceinline__ void wave_lds_fence() {
 // flight. Global factors (large graphs) are staged: every lane loads its own
 // entry of up to kStage blocks at once (one memory latency per batch), the
 // wave parks them in its LDS stage area and the products run from LDS.
-constexpr int kStage = 8;                  // updates per staged batch
-constexpr int kSplitUpdates = 8;           // updates per PART item (global factors)
+#ifndef M3S_STAGE
+#define M3S_STAGE 8
+#endif
+#ifndef M3S_SPLIT_UPDATES
+#define M3S_SPLIT_UPDATES 32
+#endif
+constexpr int kStage = M3S_STAGE;                  // updates per staged batch
+constexpr int kSplitUpdates = M3S_SPLIT_UPDATES;   // updates per PART item (global factors)
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_MFMA_PRODUCTS  // staged block products on the f64 MFMA
 #define M3S_MFMA_PRODUCTS 0

@@ -67,7 +67,7 @@ int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int3
 // Build the plan for N poses (rank 0 fixed) and edges with ranks (ri, rj).
 // split > 0 enables PART items of `split` updates each (at most max_parts).
 // dense_min: smallest top clique handled as a dense tail (0: never)
-constexpr int kDenseTailMin = 24;  // measured: a win at 42 (N = 256), neutral at 18, a loss at 10
+constexpr int kDenseTailMin = 16;  // measured (ab_dense_tail_min.txt): a win at 42 (N = 256) and at 18 (N = 128, factor + back-sub 339 -> 253 us), a loss at 10 (N = 64)
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
                        SparsePlan &P, int split = 0, int64_t max_parts = 0, int dense_min = kDenseTailMin);
 

@@ -5,29 +5,48 @@ Workload (BASELINE.json configs[2], "C3"): a 32-keyframe loop-closure
 FactorGraph in the calib residual model (config/calib.yaml -> use_calib), i.e.
 ``mast3r_slam_backends.gauss_newton_calib`` as ``FactorGraph.solve_GN_calib``
 calls it (global_opt.py:190-210), 512x512 synthetic pointmaps, two-way edges
-(E_dir ~ 98), max_iter = 10 with delta_thresh = 0 so every step runs exactly 10
-GN iterations (BASELINE.md §2).
+(E_dir = 98), max_iter = 10 with delta_thresh = 0 so every step runs exactly 10
+GN iterations (SURVEY.md §8d).
 
 One "step" = one full solve call (10 GN iterations). Multi-GPU (weak scaling):
-N GPUs solve a graph of 32*N keyframes (~98*N directed edges) with the edges
+N GPUs solve one graph of 32*N keyframes (~98*N directed edges) with the edges
 sharded across ranks and one RCCL all-gather of per-edge normal equations per
 GN iteration (mast3r_slam_amd/distributed.py).
 
-value = directed 512x512 pair-linearisations inside full GN iterations per
-second, whole job (= E_dir * GN iterations / s); ``gn_iters_per_s`` is given
+value = GN iterations per second in units of the C3 graph (SURVEY.md §8d
+"completed backend GN iterations / wall time"): at N = 1 exactly the GN
+iterations/s of the 32-KF graph; at N GPUs the whole job's E_dir * GN it/s
+divided by the C3 graph's E_dir, so that a weak-scaling run that keeps every
+GPU as busy as one GPU on C3 reports N x the single-GPU value. The raw GN
+iterations/s of the run's own graph (``gn_iters_per_s``) and the directed
+512x512 pair-linearisations per second (``pair_iters_per_s``) are given
 beside it. Inputs are resident in HBM before the timed region.
 
+Launch: ``python bench.py --gpus N`` spawns N ranks (one process per GPU,
+RCCL) when it is not already running under torch.distributed.run; under a
+launcher, --gpus must equal WORLD_SIZE (else exit 2). ``--dry-run`` runs the
+same orchestration on CPU/gloo with no-op per-rank compute (a plumbing check:
+its timings mean nothing).
+
 Extra legs on rank 0 at N = 1:
-  roofline     — the linearize kernel timed alone with HIP events on its stream
+  cold         — the same steps with the host plan cache off (M3S_PLAN_CACHE=0):
+                 the per-call symbolic analysis inside the timed region
+  roofline     — the linearize kernel timed with HIP events on its stream
+                 (+ the first-iteration gathering kernel and the solve launches)
+  hbm_copy     — a measured device-to-device copy rate next to the 8 TB/s spec
   cpu_baseline — the CPU oracle (C restatement of gn_kernels.cu, OpenMP) on one
-                 GN iteration of the same graph
+                 GN iteration of the same graph (median of 5), and the numpy
+                 tracker restatement on the C2 pair (median of 3)
   tracker_c2   — configs[1]: single-pair tracker GN at 512x512, fixed 10 iters
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import statistics
 import sys
 import time
 
@@ -42,9 +61,11 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_PATH = os.path.join(ROOT, "profiles", "pmc", "linearize_c3.json")
+SEED = 1003  # 1000 + config number
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -53,104 +74,256 @@ def parse():
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--mode", choices=("calib", "rays"), default="calib")
     ap.add_argument("--lin-reps", type=int, default=30)
+    ap.add_argument("--cold-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo orchestration check with no-op compute (no GPU)")
+    return ap.parse_args(argv)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
+class NullOps:
+    """--dry-run per-rank compute: the HipOps interface with no work, so the
+    spawn / gloo collective / timing / JSON path runs on a CPU-only host."""
+
+    stride = 36
+
+    def __init__(self, N):
+        self.device = torch.device("cpu")
+        self.dx = torch.zeros(max(N - 1, 0), 7)
+        self.info = torch.zeros(8, dtype=torch.int32)
+        self.args = self.keep = None
+
+    def prepare(self, delta):
+        pass
+
+    def linearize(self, eb, ee, es_loc):
+        if es_loc is not None:
+            es_loc.zero_()
+
+    def solve(self, es):
+        self.info[0] += 1
+
+    def close(self):
+        pass
+
+
+def lib_digest():
+    import mast3r_slam_backends as be
+
+    h = hashlib.sha256()
+    with open(be.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def base_edges(args):
+    """E_dir of the one-GPU (C3) graph: the unit of `value`."""
+    from mast3r_slam_amd import synthetic
+
+    return synthetic.make_graph(args.kf_per_gpu, 4, 4, seed=SEED, edge_range=(0, 0)).n_edges
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dry = args.dry_run
+    if dry:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        log(f"[rank {rank}] backend={dist.get_backend()} world_size={dist.get_world_size()} "
+            f"local_rank={local} device={dev}")
 
-    import mast3r_slam_backends as be
     from mast3r_slam_amd import synthetic
     from mast3r_slam_amd.distributed import ShardedGN, edge_slice
 
-    H, W = args.height, args.width
+    H, W = (8, 8) if dry else (args.height, args.width)
     HW = H * W
     N = args.kf_per_gpu * world
+    calib_mode = args.mode == "calib"
     # full edge list first (cheap), then only this rank's slice of edge data
-    probe = synthetic.make_graph(N, 4, 4, seed=1003, edge_range=(0, 0))
+    probe = synthetic.make_graph(N, 4, 4, seed=SEED, edge_range=(0, 0))
     E = probe.n_edges
+    E_base = base_edges(args)
     eb, ee, _ = edge_slice(E, rank, world)
     t0 = time.time()
-    g = synthetic.make_graph(N, H, W, seed=1003, device=dev, edge_range=(eb, ee))
+    g = synthetic.make_graph(N, H, W, seed=SEED, device=dev, edge_range=(eb, ee))
     assert g.n_edges == E
-    # calib inputs are ray-constrained by the caller (global_opt.py:172)
-    rays = synthetic.pixel_rays(H, W, g.K)
-    Xs = (g.Xs[..., 2:3] * rays[None]).contiguous()
+    if calib_mode:  # calib inputs are ray-constrained by the caller (global_opt.py:172)
+        rays = synthetic.pixel_rays(H, W, g.K)
+        Xs = (g.Xs[..., 2:3] * rays[None]).contiguous()
+    else:
+        Xs = g.Xs.contiguous()
     Cs = g.Cs.contiguous()
     T_init = g.T_init.data.contiguous()
     Twc = T_init.clone()
     ii, jj = g.ii.contiguous(), g.jj.contiguous()
     idx, valid, Q = g.idx_ii2jj, g.valid_match, g.Q
-    torch.cuda.synchronize()
+    if not dry:
+        torch.cuda.synchronize()
     log(f"[rank {rank}] graph N={N} E_dir={E} slice=[{eb},{ee}) built in {time.time() - t0:.1f}s")
 
-    calib = dict(sigma_a=1.0, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5, height=H, width=W,
-                 pixel_border=-10, z_eps=1e-6)
-    solver = ShardedGN(be.MODE_CALIB, Twc, Xs, Cs, ii, jj, idx, valid, Q, E, g.K, **calib)
+    if dry:
+        sig = dict(sigma_a=1.0)
+        ops = NullOps(N)
+        be = None
+    else:
+        import mast3r_slam_backends as be
+
+        if calib_mode:
+            sig = dict(sigma_a=1.0, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5, height=H, width=W,
+                       pixel_border=-10, z_eps=1e-6)
+        else:
+            sig = dict(sigma_a=0.003, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5)
+        ops = None
+    mode_id = 2 if calib_mode else 1  # M3S_MODE_CALIB / M3S_MODE_RAYS (include/m3s_gn.h)
+    solver = ShardedGN(mode_id, Twc, Xs, Cs, ii, jj, idx, valid, Q, E, g.K if calib_mode else None,
+                       ops=ops, **sig)
     info = torch.zeros(8, dtype=torch.int32, device=dev)
 
     def step():
         Twc.copy_(T_init)
-        if world == 1:  # the drop-in entry point itself
-            be.gauss_newton_calib(Twc, Xs, Cs, g.K, ii, jj, idx, valid, Q, H, W, -10, 1e-6, 1.0,
-                                  10.0, 0.0, 1.5, args.iters, 0.0, info=info)
+        if world == 1 and not dry:  # the drop-in entry point itself
+            if calib_mode:
+                be.gauss_newton_calib(Twc, Xs, Cs, g.K, ii, jj, idx, valid, Q, H, W, -10, 1e-6, 1.0,
+                                      10.0, 0.0, 1.5, args.iters, 0.0, info=info)
+            else:
+                be.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5,
+                                     args.iters, 0.0, info=info)
         else:
             solver.solve(args.iters, 0.0)
 
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
+
+    def timed(nsteps):
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            step()
+        sync()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        return el
+
     for _ in range(args.warmup):
         step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    elapsed = timed(args.steps)
     iters_total = args.iters * args.steps
     gn_iters_per_s = iters_total / elapsed
-    value = E * gn_iters_per_s
-    if world == 1:
+    pair_iters_per_s = E * gn_iters_per_s
+    value = pair_iters_per_s / E_base
+    if world == 1 and not dry:
         assert int(info[be.INFO_ITERS]) == args.iters and int(info[be.INFO_BAD_EDGE]) == 0
+        assert int(info[be.INFO_SOLVE_FAIL]) == 0
 
-    # ---- roofline: the dominant kernel, HIP events on its stream ----
-    # GN iterations 2..10 of a call run linearize_packed_kernel (the first one
-    # runs the gathering kernel that also stores the target-side planes). It
-    # is timed in the solve's own launch pattern (linearize -> LLT -> ...):
-    # an event pair around each linearize launch of stepwise solves of the
-    # same graph (the pair also covers the launch's ~3 us per-edge reduce).
-    # The same kernel launched back to back is timed too, for reference.
+    # cold calls: the host symbolic analysis (ordering, fill, schedule) inside
+    # the timed region, as a SLAM backend call whose edge set changed pays it
+    os.environ["M3S_PLAN_CACHE"] = "0"
+    cold_el = timed(args.cold_steps) if args.cold_steps > 0 else None
+    del os.environ["M3S_PLAN_CACHE"]
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GN iterations/s of the 32-KF C3 graph (E_dir x GN it/s / 98; = GN it/s at N=1), whole job",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded ray-cast room, SURVEY.md §8d); no datasets/weights offline",
+        "config": {
+            "workload": "%s: %d-KF loop-closure FactorGraph, gauss_newton_%s, %dx%d, "
+                        "%d GN iterations per step (delta_thresh=0)"
+                        % ("C3" if world == 1 and calib_mode else "weak-scaled C3", N, args.mode, H, W,
+                           args.iters),
+            "keyframes": N,
+            "directed_edges": E,
+            "pixels_per_pointmap": HW,
+            "gn_iters_per_step": args.iters,
+            "solve": "fp64 block-sparse 7x7 LLT on device (min-degree order), n=%d" % (7 * (N - 1)),
+            "parallelism": "edge-sharded x%d, RCCL all-gather of per-edge normal equations" % world
+            if world > 1 else "single GPU",
+        },
+        "gn_iters_per_s": round(gn_iters_per_s, 2),
+        "pair_iters_per_s": round(pair_iters_per_s, 1),
+        "cold": {
+            "ms_per_step": round(cold_el / args.cold_steps * 1e3, 4) if cold_el else None,
+            "gn_iters_per_s": round(args.iters * args.cold_steps / cold_el, 2) if cold_el else None,
+            "note": "plan cache off (M3S_PLAN_CACHE=0): every call re-runs the host symbolic "
+                    "analysis, as a call on a changed edge set does",
+        },
+    }
+    if dry:
+        out["dry_run"] = True
+        out["data"] = "dry run: CPU/gloo orchestration with no-op compute; timings are meaningless"
+    else:
+        out["roofline"] = roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per_s,
+                                       world, dev)
+
+    if rank == 0 and world == 1 and not dry:
+        out["hbm_copy"] = copy_leg(dev)
+        if not args.no_tracker:
+            out["tracker_c2"] = tracker_leg(be, synthetic, dev, H, W)
+            out["matching_512"] = matching_leg(be, synthetic, dev, H, W)
+        if not args.no_cpu:
+            out["cpu_baseline"] = cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E, calib_mode,
+                                          not args.no_tracker)
+    solver.ops.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per_s, world, dev):
+    """The dominant kernel: GN iterations 2..10 of a call run
+    linearize_packed_kernel (the first runs the gathering kernel that also
+    stores the target-side planes). Timed in the solve's own launch pattern
+    (linearize -> LLT -> ...): a HIP event pair on the launch stream around
+    each linearize and each solve launch of stepwise solves of the same graph
+    (the linearize pair also covers the launch's ~3 us per-edge reduce). The
+    same kernel launched back to back is timed too, for reference."""
     n_loc = ee - eb
     kf_touched = torch.unique(torch.cat([ii[eb:ee], jj[eb:ee]])).numel() if n_loc else 0
     bytes_alg = HW * (13 * n_loc + 16 * kf_touched)  # SURVEY.md §8(d) per (edge, px) and (KF, px)
     stream = torch.cuda.current_stream(dev)
-    in_solve = []
+    lin, first, slv = [], [], []
     for rep in range(4):
         Twc.copy_(T_init)
-        t = solver.solve_timed(args.iters, 0.0, stream)
+        t_lin, t_slv = solver.solve_timed(args.iters, 0.0, stream)
         if rep:  # the first call is a warm-up
-            in_solve += t[1:]  # iterations 2.. (packed kernel)
-    lin_ms = sum(in_solve) / len(in_solve)
+            first.append(t_lin[0])
+            lin += t_lin[1:]  # iterations 2.. (packed kernel)
+            slv += t_slv
+    lin_ms = sum(lin) / len(lin)
     Twc.copy_(T_init)
     be.gn_prepare(solver.args, solver.keep)
     solver.linearize_only()  # first launch: gathering kernel + planes
@@ -162,73 +335,68 @@ def main():
         solver.linearize_only()
     ev1.record(stream)
     torch.cuda.synchronize()
-    b2b_ms = ev0.elapsed_time(ev1) / args.lin_reps  # back-to-back launches, per-launch average
+    b2b_ms = ev0.elapsed_time(ev1) / args.lin_reps
     achieved = bytes_alg / (lin_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_linearize_c3.json")
-    if os.path.exists(pmc_path) and world == 1:
-        try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    out = {
-        "metric": METRIC,
-        "value": round(value, 1),
-        "unit": "512x512-pair GN iterations/s (E_dir x GN iterations per second, whole job)",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (seeded ray-cast room, SURVEY.md §8d); no datasets/weights offline",
-        "config": {
-            "workload": "C3: %d-KF loop-closure FactorGraph, gauss_newton_calib, %dx%d, "
-                        "%d GN iterations per step (delta_thresh=0)" % (N, H, W, args.iters),
-            "keyframes": N,
-            "directed_edges": E,
-            "pixels_per_pointmap": HW,
-            "gn_iters_per_step": args.iters,
-            "solve": "fp64 block-sparse 7x7 LLT on device (min-degree order), n=%d" % (7 * (N - 1)),
-            "parallelism": "edge-sharded x%d, RCCL all-gather of per-edge normal equations" % world
-            if world > 1 else "single GPU",
+    first_ms = sum(first) / len(first)
+    traffic, traffic_note = None, "no PMC record"
+    if os.path.exists(PMC_PATH) and world == 1 and args.mode == "calib":
+        rec = json.load(open(PMC_PATH))
+        if rec.get("lib_sha256_16") == lib_digest() and rec.get("kf") == args.kf_per_gpu:
+            traffic = rec.get("hbm_bytes_per_launch")
+            traffic_note = rec.get("note", "PMC pass of this library build")
+        else:
+            traffic_note = "PMC record is of another library build: not reported"
+    return {
+        "bound": "hbm",
+        "kernel": "linearize_packed_kernel<%s> (%d edges x %d px per launch; GN iterations 2..%d "
+                  "of each call)" % (args.mode, n_loc, HW, args.iters),
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_note": traffic_note,
+        "algorithmic_bytes_per_launch": bytes_alg,
+        "avg_launch_ms": round(lin_ms, 5),
+        "timing": "HIP events around each linearize launch of stepwise solves (its launch pattern "
+                  "in the timed region); back_to_back_ms = the same kernel launched back to back",
+        "back_to_back_ms": round(b2b_ms, 5),
+        "gather_kernel": {
+            "kernel": "linearize_kernel (first GN iteration: gathers Xi/Ci through idx, stores planes)",
+            "avg_launch_ms": round(first_ms, 5),
+            "achieved": round(bytes_alg / (first_ms * 1e-3) / 1e9, 1),
+            "frac": round(bytes_alg / (first_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         },
-        "gn_iters_per_s": round(gn_iters_per_s, 2),
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "linearize_packed_kernel<calib> (%d edges x %d px per launch; GN "
-                      "iterations 2..%d of each call)" % (n_loc, HW, args.iters),
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_alg,
-            "avg_launch_ms": round(lin_ms, 5),
-            "timing": "HIP events around each linearize launch of stepwise solves (its launch pattern "
-                      "in the timed region); back_to_back_ms = the same kernel launched back to back",
-            "back_to_back_ms": round(b2b_ms, 5),
-            "iteration_level": {
-                "achieved": round(bytes_alg * gn_iters_per_s / 1e9, 1) if world == 1 else None,
-                "note": "SURVEY.md §8(d) B_iter x GN iterations/s (whole iteration: linearize, "
-                        "reduce, assemble, LLT, retraction)",
-            },
+        "solve": {
+            "kernels": "fp64 sparse LLT + retraction (sparse_llt_kernel [+ border_kernel]), stepwise "
+                       "path (finalize + assemble launches included)",
+            "avg_ms": round(sum(slv) / len(slv), 5),
+            "bound": "latency (elimination-tree critical path, DESIGN.md §4)",
+        },
+        "iteration_level": {
+            "achieved": round(bytes_alg * gn_iters_per_s / 1e9, 1) if world == 1 else None,
+            "note": "SURVEY.md §8(d) B_iter x GN iterations/s (whole iteration: linearize, "
+                    "reduce, assemble, LLT, retraction)",
         },
     }
 
-    if rank == 0 and world == 1 and not args.no_tracker:
-        out["tracker_c2"] = tracker_leg(be, synthetic, dev, H, W)
-        out["matching_512"] = matching_leg(be, synthetic, dev, H, W)
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+
+def copy_leg(dev, nbytes=1 << 30, reps=10):
+    """Device-to-device copy rate (read + write bytes) as a measured HBM
+    ceiling beside the 8 TB/s spec."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"GB_per_s": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes_moved": 2 * nbytes,
+            "note": "torch copy_ of 1 GiB, read + write bytes"}
 
 
 def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
@@ -248,7 +416,9 @@ def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
     assert int(out[2][0]) == iters
     return {"workload": "C2: 1 frame->keyframe pair, rays+dist Sim3 GN, %dx%d, %d fixed iterations"
                         % (H, W, iters),
-            "gn_iters_per_s": round(reps * iters / dt, 1), "ms_per_solve": round(dt / reps * 1e3, 4)}
+            "gn_iters_per_s": round(reps * iters / dt, 1), "ms_per_solve": round(dt / reps * 1e3, 4),
+            "bytes_per_iter": 45 * H * W,
+            "hbm_frac": round(45 * H * W * reps * iters / dt / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def matching_leg(be, synthetic, dev, H, W, reps=20):
@@ -283,22 +453,82 @@ def matching_leg(be, synthetic, dev, H, W, reps=20):
             "ms_prep_rays": times["prep_rays"]}
 
 
-def cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E):
-    """The CPU oracle (oracle/gn_oracle.c, OpenMP) on one GN iteration of the
-    same graph; reported, not the target."""
+def cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E, calib_mode, with_tracker, runs=5):
+    """Reported, not the target. Backend: the C oracle (oracle/gn_oracle.c,
+    OpenMP over edges) on one full GN iteration of the same graph, median of
+    `runs`. Tracker: the numpy restatement of tracker.py on the C2 pair, 10
+    fixed iterations, median of 3."""
+    from mast3r_slam_amd import synthetic
     from oracle import oracle as orc
+    from oracle import tracker_oracle as tro
 
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    p = orc.make_params(orc.MODE_CALIB, 1.0, 10.0, 0.0, 1.5, K=g.K.cpu().numpy(), height=H, width=W,
-                        pixel_border=-10, z_eps=1e-6)
+    if calib_mode:
+        p = orc.make_params(orc.MODE_CALIB, 1.0, 10.0, 0.0, 1.5, K=g.K.cpu().numpy(), height=H, width=W,
+                            pixel_border=-10, z_eps=1e-6)
+    else:
+        p = orc.make_params(orc.MODE_RAYS, 0.003, 10.0, 0.0, 1.5)
     host = [t.cpu().numpy() for t in (T_init, Xs, g.Cs, ii, jj, idx, valid, Q)]
-    t0 = time.perf_counter()
-    _, _, it, _ = orc.gn(p, *host, 1, 0.0)
-    dt = time.perf_counter() - t0
-    return {"value": round(E * it / dt, 2), "unit": "512x512-pair GN iterations/s", "cores": cores,
-            "kind": "port",
-            "sample": "1 full GN iteration (linearise %d directed edges + fp64 solve) of the same graph, "
-                      "%.1f s" % (E, dt)}
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        _, _, it, _ = orc.gn(p, *host, 1, 0.0)
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    out = {"value": round(it / med, 3), "unit": "GN iterations/s of the same graph (C oracle)",
+           "cores": cores, "kind": "port",
+           "pair_iters_per_s": round(E * it / med, 2),
+           "sample": "1 full GN iteration (linearise %d directed edges + fp64 solve) of the same graph, "
+                     "median of %d runs: %.3f s (min %.3f, max %.3f)" % (E, runs, med, min(ts), max(ts))}
+    if with_tracker:
+        pr = synthetic.make_pair(H, W, seed=1002)
+        cfg = dict(tro.TRACKING_CFG, max_iters=10, rel_error=0.0, delta_norm=0.0)
+        args = (pr.Xf.numpy(), pr.Xk.numpy(), pr.T_WCf_init.data.numpy(), pr.T_WCk.data.numpy(),
+                pr.Qk.numpy(), pr.valid.numpy(), cfg)
+        tt = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, _, it2 = tro.track_rays(*args)
+            tt.append(time.perf_counter() - t0)
+        tm = statistics.median(tt)
+        out["tracker"] = {"gn_iters_per_s": round(it2 / tm, 3), "cores": 1, "kind": "port",
+                          "sample": "C2 pair %dx%d, %d fixed iterations of the numpy restatement of "
+                                    "tracker.py, median of 3: %.3f s" % (H, W, it2, tm)}
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(local_rank, argv, world, port):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def main(argv=None):
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; refusing to run")
+            sys.exit(2)
+        run(args)
+        return
+    if args.gpus <= 1:
+        run(args)
+        return
+    # one process per GPU, spawned before this process touches the GPU
+    import torch.multiprocessing as mp
+
+    log(f"bench.py: spawning {args.gpus} ranks")
+    mp.start_processes(_rank_entry, args=(sys.argv[1:] if argv is None else argv, args.gpus, _free_port()),
+                       nprocs=args.gpus, join=True, start_method="spawn")
 
 
 if __name__ == "__main__":

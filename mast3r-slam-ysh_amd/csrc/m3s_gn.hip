@@ -53,10 +53,7 @@ namespace {
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
-#ifndef M3S_TARGET_BLOCKS
-#define M3S_TARGET_BLOCKS 2048
-#endif
-constexpr int kTargetBlocks = M3S_TARGET_BLOCKS;  // linearize grid target (edges x chunks)
+constexpr int kTargetBlocks = 2048;  // linearize grid target (edges x chunks)
 constexpr int kMaxSmallNp = 224;     // register Cholesky limit (n + 1 <= 7 * 32)
 constexpr int kCholThreads = 512;    // 16 x 32 thread grid
 constexpr int64_t kMaxLd = 8192;     // tiled path: back-substitution keeps x in LDS
@@ -85,19 +82,13 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      tasks, dtile, dx_vec, planes, total;
+      tasks, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
 
 constexpr int kTile = 64;  // tiled Cholesky tile (large systems)
 inline int64_t aug_ld(int64_t n) { return (n + 1 + kTile - 1) / kTile * kTile; }
-
-// flags of the persistent dense LLT: ntr*ntc tiles + ntc x segments + ticket/abort
-inline size_t pd_flag_bytes(int64_t ld) {
-  const size_t nt = (size_t)(ld / 32);
-  return sizeof(int32_t) * (nt * nt + nt + 8);
-}
 
 inline size_t edge_cnt_bytes(int64_t E) { return (sizeof(uint32_t) * (size_t)(E + 1) + 15) & ~size_t(15); }
 
@@ -141,11 +132,6 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
-  // persistent dense LLT: tile / x-segment flags + ticket, then x
-  L.dtile = off;
-  off = align_up(off + pd_flag_bytes(L.ld), 256);
-  L.dx_vec = off;
-  off = align_up(off + sizeof(double) * (size_t)L.ld, 256);
   // target-side planes of every edge (5 planes = rays, the widest mode)
   L.planes = off;
   off = align_up(off + sizeof(float) * 5 * (size_t)E * (size_t)HW, 256);
@@ -237,16 +223,13 @@ __device__ __forceinline__ void store_sc1(float *p, float v) {
 // its row (16-B stores), then 252 threads each add a 1/7 slice of one column,
 // then 36 threads combine the 7 slices. ~100 instructions per thread instead
 // of 36 wave-wide shuffle trees.
-#ifndef M3S_RED_PASSES
-#define M3S_RED_PASSES 2  // 1: one 36 KB LDS pass; 2: two 18 KB passes (more blocks per CU)
-#endif
-constexpr int kRedW = kNP / M3S_RED_PASSES;  // values per pass (36 or 18)
+constexpr int kRedW = kNP / 2;  // values per pass (36 or 18)
 __device__ __forceinline__ void block_reduce_store(const float *acc, float *out) {
   __shared__ __attribute__((aligned(16))) float red[kThreads * kRedW];
   __shared__ float part[kRedW][8];
   const int t = threadIdx.x;
 #pragma unroll
-  for (int pass = 0; pass < M3S_RED_PASSES; pass++) {
+  for (int pass = 0; pass < 2; pass++) {
     if (pass) __syncthreads();
     float2 *row = reinterpret_cast<float2 *>(red + (size_t)t * kRedW);
 #pragma unroll
@@ -272,29 +255,11 @@ __device__ __forceinline__ void block_reduce_store(const float *acc, float *out)
   }
 }
 
-#ifndef M3S_NT
-#define M3S_NT 1  // non-temporal loads for the once-per-iteration edge stream
-#endif
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T *p) {
-#if M3S_NT
   return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
 }
 
-#ifndef M3S_LIN_MINWAVES
-#define M3S_LIN_MINWAVES 0
-#endif
-#if M3S_LIN_MINWAVES > 0
-#define M3S_LIN_BOUNDS __launch_bounds__(kThreads, M3S_LIN_MINWAVES)
-#else
-#define M3S_LIN_BOUNDS __launch_bounds__(kThreads)
-#endif
-#ifndef M3S_LDS_REDUCE
-#define M3S_LDS_REDUCE 0
-#endif
 
 // Per edge: H_jj = M L M^T and g_j = M l in fp64 (M = Adj(T_i)^-T), written
 // as fin[0:49] (row-major) and fin[49:56], from the edge's 36 local sums `es`
@@ -334,9 +299,6 @@ __device__ __forceinline__ void finalize_edge(const double *es, const float *Ti,
 // Each lane owns 4 consecutive pixels (one 16-B vector per stream); a wave
 // sweeps 256 pixels per trip, a block 1024.
 // 36 per-thread sums -> one block partial
-#ifndef M3S_XREDUCE
-#define M3S_XREDUCE 1
-#endif
 // Transposed wave reduction of N values: each butterfly step (xor 32, 16,
 // ..., 1) a lane keeps one half of its values and sends the other half to its
 // partner, so the count halves every step: 18 + 9 + 5 + 3 + 2 + 1 = 38
@@ -380,9 +342,6 @@ __device__ __forceinline__ T xreduce36(const T (&v)[kNP], int lane, int &idx, bo
 }
 
 __device__ __forceinline__ void store_partial(const float *acc, float *out) {
-#if M3S_LDS_REDUCE
-  block_reduce_store(acc, out);
-#elif M3S_XREDUCE
   __shared__ float red[kThreads / 64][kNP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float v[kNP];
@@ -399,23 +358,6 @@ __device__ __forceinline__ void store_partial(const float *acc, float *out) {
     for (int w = 0; w < kThreads / 64; w++) t += red[w][threadIdx.x];
     store_sc1(out + threadIdx.x, t);
   }
-#else
-  // wave64 butterfly, then the 4 waves through LDS
-  __shared__ float red[kThreads / 64][kNP];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kNP; k++) {
-    const float v = wave_sum(acc[k]);
-    if (lane == 0) red[wave][k] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < kNP) {
-    float s = 0.0f;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; w++) s += red[w][threadIdx.x];
-    store_sc1(out + threadIdx.x, s);
-  }
-#endif
 }
 
 // Fused finalize (single-GPU solve): after its chunk partial is stored, a
@@ -479,7 +421,7 @@ __device__ __forceinline__ void track_tail(const LinArgs &A) {
 // WPACK: also store the target-side planes for the packed kernel (first GN
 // iteration of a solve call).
 template <int MODE, bool TRACK, bool VEC, bool WPACK>
-__global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
+__global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   if (*A.stop) return;
   const int64_t b = block_task(A);
   if (b < 0) return;
@@ -502,14 +444,7 @@ __global__ void M3S_LIN_BOUNDS linearize_kernel(LinArgs A) {
     Cs_i = A.Cs + (size_t)ri * HW;
     Cs_j = A.Cs + (size_t)rj * HW;
   }
-#ifndef M3S_MAT_ACT
-#define M3S_MAT_ACT 1
-#endif
-#if M3S_MAT_ACT
   const Sim3Mat Tm = sim3_matrix(Tij);
-#else
-  const Sim3f &Tm = Tij;
-#endif
   // edge data (idx/valid/Q) is addressed relative to the launch's edge slice
   const size_t eoff = TRACK ? 0 : (size_t)e_loc * HW;
   const int64_t *__restrict__ idx = TRACK ? nullptr : A.idx + eoff;
@@ -602,11 +537,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
   const int64_t HW = A.HW;
   const int ri = A.rank_i[e], rj = A.rank_j[e];
   const Sim3f Tij = relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj));
-#if M3S_MAT_ACT
   const Sim3Mat Tm = sim3_matrix(Tij);
-#else
-  const Sim3f &Tm = Tij;
-#endif
   const float *__restrict__ Xs_j = A.Xs + (size_t)rj * HW * 3;
   constexpr int NPL = PixIn<MODE>::kPlanes;
   const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
@@ -615,32 +546,15 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
   acc.zero();
   const int64_t p_begin = c * A.chunk_pix;
   const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
-#ifndef M3S_PK_GROUP
-#define M3S_PK_GROUP 1
-#endif
-#ifndef M3S_PK_PREFETCH
-#define M3S_PK_PREFETCH 0
-#endif
   // one trip = 4 pixels per lane: NPL plane vectors + 3 Xj vectors (16 B each)
   auto load_trip = [&](int64_t q, f32x4 *pv, f32x4 *xv) {
-#if M3S_PK_NOLOAD  // experiment: compute floor (no memory traffic)
-    const float f = (float)(q & 1023) * 1e-3f;
-    for (int k = 0; k < NPL; k++) pv[k] = f32x4{1.0f + f, 2.0f, 0.5f, f};
-    xv[0] = f32x4{f, 0.1f, 2.0f + f, 0.2f}, xv[1] = f32x4{0.3f, 2.1f, f, 0.1f}, xv[2] = f32x4{1.9f, f, 0.2f, 2.2f};
-    return;
-#endif
 #pragma unroll
     for (int k = 0; k < NPL; k++) pv[k] = ld_stream(reinterpret_cast<const f32x4 *>(pl + (size_t)k * HW + q));
     const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * q);
     xv[0] = xj4[0], xv[1] = xj4[1], xv[2] = xj4[2];
   };
-  float sink = 0.0f;  // M3S_PK_NOCOMPUTE experiment only
+  float sink = 0.0f;  // 0 experiment only
   auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
-#if M3S_PK_NOCOMPUTE  // experiment: memory floor
-    for (int k = 0; k < NPL; k++) sink += pv[k].x + pv[k].y + pv[k].z + pv[k].w;
-    sink += xv[0].x + xv[1].y + xv[2].z;
-    return;
-#endif
     const float Xj[4][3] = {{xv[0].x, xv[0].y, xv[0].z}, {xv[0].w, xv[1].x, xv[1].y},
                             {xv[1].z, xv[1].w, xv[2].x}, {xv[2].y, xv[2].z, xv[2].w}};
 #pragma unroll
@@ -652,13 +566,9 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
       act(Tm, Xj[s], Y);
       pixel_contrib<MODE>(acc, A.P, in, Y);
       // one pixel at a time: keeps the packed kernel at ~90 VGPRs (5 waves/SIMD)
-      if ((s + 1) % M3S_PK_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+      if ((s + 1) % 1 == 0) __builtin_amdgcn_sched_barrier(0);
     }
   };
-#ifndef M3S_PK_GLDS
-#define M3S_PK_GLDS 1
-#endif
-#if M3S_PK_GLDS && !M3S_PK_NOLOAD
   // Prefetch one trip ahead through LDS with no VGPR cost: each wave's next
   // trip (NPL plane vectors + 3 Xj vectors, 16 B per lane each) is loaded by
   // global_load_lds_dwordx4 into the wave's own LDS slot while the wave
@@ -671,7 +581,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
     for (int k = 0; k < NPL; k++)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(pl + (size_t)k * HW + q),
                                        (__attribute__((address_space(3))) void *)(&stage[wv][k][0]),
-                                       16, 0, M3S_NT ? 2 : 0);
+                                       16, 0, 1 ? 2 : 0);
 #pragma unroll
     for (int k = 0; k < 3; k++)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(Xs_j + 3 * q + 4 * k),
@@ -691,27 +601,6 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
     if (p0 + kBlockPix < p_end) issue(p0 + kBlockPix);
     do_trip(pv, xv);
   }
-#elif M3S_PK_PREFETCH
-  // software pipeline: the next trip's loads are in flight during this trip's math
-  int64_t p0 = p_begin + kPixPerThread * threadIdx.x;
-  f32x4 pv[NPL], xv[3];
-  if (p0 < p_end) load_trip(p0, pv, xv);
-  for (; p0 < p_end; p0 += kBlockPix) {
-    f32x4 pn[NPL], xn[3];
-    const int64_t q = p0 + kBlockPix;
-    if (q < p_end) load_trip(q, pn, xn);
-    do_trip(pv, xv);
-#pragma unroll
-    for (int k = 0; k < NPL; k++) pv[k] = pn[k];
-    xv[0] = xn[0], xv[1] = xn[1], xv[2] = xn[2];
-  }
-#else
-  for (int64_t p0 = p_begin + kPixPerThread * threadIdx.x; p0 < p_end; p0 += kBlockPix) {
-    f32x4 pv[NPL], xv[3];
-    load_trip(p0, pv, xv);
-    do_trip(pv, xv);
-  }
-#endif
   float sums[kNP];
 #pragma unroll
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
@@ -1050,295 +939,7 @@ __global__ void __launch_bounds__(1024) backsolve_kernel(const double *__restric
   finish_step(rhs, dxs, nrm, n, Twc, N, dx_out, info, flags + kFlagStop, delta_thresh);
 }
 
-// ------------------------------------- persistent dense LLT (large graphs) --
-// For systems whose elimination tree has a large dense top (random long-range
-// loop edges at N >= ~100 KFs), the single-CU sparse LLT is bound by one CU's
-// dependent memory round trips. This kernel factors the RHS-augmented dense
-// system of assemble_kernel on the whole chip: left-looking over 32x32 fp64
-// tiles, one task per lower tile (i, j) (its updates sum_k L_ik L_jk^T on the
-// fp64 MFMA, v_mfma_f64_16x16x4f64, k ascending; then the diagonal
-// factorisation or the triangular solve against L_jj), then one task per tile
-// column of the back-substitution (contributions in fixed order i = top..j+1).
-// Tasks are drawn in a topological order from one global ticket counter, so a
-// task only ever waits for tasks drawn before it by running workgroups:
-// progress does not depend on co-residency. Completion is published per tile
-// / per x segment with an agent-scope release (every workgroup of every XCD
-// sees it after its acquire). Every sum runs in a fixed order, so the result
-// is bitwise reproducible (the sharded solve relies on identical ranks).
-// Bounded waits: a stuck flag sets `abort` and the step becomes a failure.
-#ifndef M3S_PD_SPINS
-#define M3S_PD_SPINS (1 << 22)
-#endif
-#ifndef M3S_PD_DEBUG
-#define M3S_PD_DEBUG 0
-#endif
-constexpr int kPT = 32;          // tile edge
-constexpr int kPDThreads = 256;  // 4 waves: one 16x16 MFMA output block each
-constexpr int kPDGrid = 256;     // persistent workgroups (one per CU)
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-
-struct PDenseArgs {
-  double *A;
-  int64_t ld;
-  int n, ntr, ntc, n_tile_tasks;
-  int32_t *tflag;  // [ntr * ntc] lower tile (i, j) final
-  int32_t *xflag;  // [ntc] x segment j published
-  int32_t *ctr;    // [0] ticket, [1] abort
-  double *x;       // [ntr * kPT] solution (0 beyond n)
-  float *Twc;
-  int64_t N;
-  float *dx_out;
-  int32_t *info;
-  int32_t *flags;
-  float delta_thresh;
-};
-
-// Called by a whole wave: every lane loads the flag and the loop condition is
-// made wave-uniform (readfirstlane), so the spin is scalar control flow (no
-// exec-masked loop around s_sleep next to the block's barriers).
-__device__ __forceinline__ bool pd_wait(int32_t *flag, int32_t *abort_flag) {
-  int spins = 0;
-  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-      return false;
-    if (++spins > M3S_PD_SPINS) {
-#if M3S_PD_DEBUG
-      printf("pdense: wait timeout block %d flag %p\n", (int)blockIdx.x, (void *)flag);
-#endif
-      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return true;
-}
-
-// whole block: wave 0 waits for every flag in `fl[0..cnt)`, then all acquire
-__device__ __forceinline__ void pd_wait_block(int32_t *const *fl, int cnt, int32_t *abort_flag) {
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
-    for (int q = 0; q < cnt; q++) pd_wait(fl[q], abort_flag);
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-__device__ __forceinline__ void pd_publish(int32_t *flag) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// 32x32 tile (row-major in A, leading dim ld) -> LDS [32][33]
-__device__ __forceinline__ void pd_load_tile(const double *__restrict__ T, int64_t ld, double (*S)[kPT + 1]) {
-  for (int k = threadIdx.x; k < kPT * kPT / 2; k += kPDThreads) {
-    const int r = k >> 4, c = (k & 15) * 2;
-    const double2 v = *reinterpret_cast<const double2 *>(T + (size_t)r * ld + c);
-    S[r][c] = v.x;
-    S[r][c + 1] = v.y;
-  }
-}
-
-__device__ void pd_tile_task(const PDenseArgs &P, int i, int j, double (*Si)[kPT + 1], double (*Sj)[kPT + 1],
-                             double (*Sv)[kPT + 1], double *col) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int bi = w >> 1, bj = w & 1;  // this wave's 16x16 output block
-  const int64_t ld = P.ld;
-  double *Aij = P.A + (size_t)i * kPT * ld + (size_t)j * kPT;
-  int32_t *abort_flag = P.ctr + 1;
-  // ---- sum_k L_ik L_jk^T on the MFMA (k ascending, 8 k-steps of 4 per tile)
-  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k = 0; k < j; k++) {
-    int32_t *fl[2] = {P.tflag + (size_t)i * P.ntc + k, P.tflag + (size_t)j * P.ntc + k};
-    pd_wait_block(fl, i == j ? 1 : 2, abort_flag);
-    pd_load_tile(P.A + (size_t)i * kPT * ld + (size_t)k * kPT, ld, Si);
-    if (i != j) pd_load_tile(P.A + (size_t)j * kPT * ld + (size_t)k * kPT, ld, Sj);
-    __syncthreads();
-    double(*Lj)[kPT + 1] = (i == j) ? Si : Sj;
-#pragma unroll
-    for (int s = 0; s < kPT / 4; s++) {
-      const double a = Si[16 * bi + (lane & 15)][4 * s + (lane >> 4)];
-      const double b = Lj[16 * bj + (lane & 15)][4 * s + (lane >> 4)];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  // ---- v = A_ij - acc into LDS (f64 MFMA C/D map: col = lane&15, row = (lane>>4) + 4 r)
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int row = 16 * bi + (lane >> 4) + 4 * r, cc = 16 * bj + (lane & 15);
-    Sv[row][cc] = Aij[(size_t)row * ld + cc] - acc[r];
-  }
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: tile (%d,%d) wave %d updates done\n", i, j, w);
-#endif
-  __syncthreads();
-  const int tx = t & 15, ty = t >> 4;  // 2x2 entries per thread: (ty + 16a, tx + 16b)
-  const int cmax = min(kPT, P.n - j * kPT);  // columns that are factored (augmented / padding excluded)
-  if (i == j) {
-    // right-looking Cholesky of the diagonal tile (as potrf_tile_kernel)
-    // fixed trip count and no early exit: every wave meets the same barriers
-    // whatever the data (columns >= cmax are left untouched; a non-positive
-    // pivot flags the step as failed and the rest of the tile is don't-care)
-    bool bad = false;
-    for (int c = 0; c < kPT; c++) {
-      const bool act = c < cmax;
-      const double d = Sv[c][c];
-      if (act && !(d > 0.0)) bad = true;
-      const double inv = 1.0 / sqrt(d);
-      if (act && t < kPT) col[t] = Sv[t][c] * inv;
-      __syncthreads();
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-          const int r = ty + 16 * a, q = tx + 16 * b;
-          if (act && q > c && r >= q) Sv[r][q] -= col[r] * col[q];
-        }
-      if (act && t < kPT && t >= c) Sv[t][c] = col[t];
-      __syncthreads();
-    }
-    if (bad && t == 0) __hip_atomic_store(P.flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    int32_t *fl[1] = {P.tflag + (size_t)j * P.ntc + j};
-    pd_wait_block(fl, 1, abort_flag);
-    pd_load_tile(P.A + (size_t)j * kPT * ld + (size_t)j * kPT, ld, Si);  // L_jj
-    __syncthreads();
-    // X L_jj^T = V, column by column (as trsm_tile_kernel), fixed trip count
-    for (int c = 0; c < kPT; c++) {
-      const bool act = c < cmax;
-      const double inv = 1.0 / Si[c][c];
-      if (act && t < kPT) col[t] = Sv[t][c] * inv;
-      __syncthreads();
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-          const int r = ty + 16 * a, q = tx + 16 * b;
-          if (act && q > c) Sv[r][q] -= col[r] * Si[q][c];
-        }
-      if (act && t < kPT) Sv[t][c] = col[t];
-      __syncthreads();
-    }
-  }
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: tile (%d,%d) wave %d factored\n", i, j, w);
-#endif
-  for (int k = t; k < kPT * kPT; k += kPDThreads) Aij[(size_t)(k >> 5) * ld + (k & 31)] = Sv[k >> 5][k & 31];
-  pd_publish(P.tflag + (size_t)i * P.ntc + j);
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: tile (%d,%d) wave %d published\n", i, j, w);
-#endif
-}
-
-// back-substitution of tile column j: L_jj^T x_j = y_j - sum_{i>j} L_ij^T x_i
-__device__ void pd_back_task(const PDenseArgs &P, int j, double (*Si)[kPT + 1], double (*Sv)[kPT + 1],
-                             double *xs, double *red) {
-  const int t = threadIdx.x, lane = t & 63;
-  const int c = t & 31, rg = t >> 5;  // column c, rows 4 rg .. 4 rg + 3
-  const int64_t ld = P.ld;
-  int32_t *abort_flag = P.ctr + 1;
-  const int rn = P.n / kPT;  // tile row holding the augmented row n (y)
-  double part = 0.0;
-  for (int i = P.ntc - 1; i > j; i--) {
-    int32_t *fl[2] = {P.xflag + i, P.tflag + (size_t)i * P.ntc + j};
-    pd_wait_block(fl, 2, abort_flag);
-    const double *Lt = P.A + (size_t)i * kPT * ld + (size_t)j * kPT;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int r = 4 * rg + q;
-      part += Lt[(size_t)r * ld + c] * P.x[i * kPT + r];
-    }
-  }
-  red[t] = part;
-  int32_t *fl[2] = {P.tflag + (size_t)rn * P.ntc + j, P.tflag + (size_t)j * P.ntc + j};
-  pd_wait_block(fl, 2, abort_flag);
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: back %d wave %d waited\n", j, t >> 6);
-#endif
-  pd_load_tile(P.A + (size_t)j * kPT * ld + (size_t)j * kPT, ld, Si);
-  __syncthreads();
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: back %d wave %d loaded\n", j, t >> 6);
-#endif
-  if (t < 64) {
-    double r = 0.0, xv = 0.0;
-    if (lane < kPT) {
-      double s = 0.0;
-      for (int g = 0; g < 8; g++) s += red[g * 32 + lane];
-      r = P.A[(size_t)P.n * ld + j * kPT + lane] - s;  // y_j - sum
-    }
-    for (int cc = kPT - 1; cc >= 0; cc--) {
-      if (j * kPT + cc >= P.n) continue;  // uniform
-      const double xc = __shfl(r, cc, 64) / Si[cc][cc];
-      if (lane < cc) r -= Si[cc][lane] * xc;
-      if (lane == cc) xv = xc;
-    }
-    if (lane < kPT) {
-      const double v = (j * kPT + lane < P.n) ? xv : 0.0;
-      P.x[j * kPT + lane] = v;
-      xs[j * kPT + lane] = v;
-    }
-  }
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: back %d wave %d solved\n", j, t >> 6);
-#endif
-  pd_publish(P.xflag + j);
-#if M3S_PD_DEBUG
-  if ((t & 63) == 0) printf("pdense: back %d wave %d published\n", j, t >> 6);
-#endif
-}
-
-__global__ void __launch_bounds__(kPDThreads) pdense_llt_kernel(PDenseArgs P) {
-  if (P.flags[kFlagStop]) return;
-  __shared__ double Si[kPT][kPT + 1], Sj[kPT][kPT + 1], Sv[kPT][kPT + 1];
-  __shared__ double col[kPT], red[kPDThreads];
-  __shared__ int tk_s, last_s;
-  __shared__ float nrm[16];
-  extern __shared__ __attribute__((aligned(16))) double pd_dyn[];
-  double *xs = pd_dyn;                                                // n doubles (last task)
-  float *dxs = reinterpret_cast<float *>(pd_dyn + P.ntr * kPT);       // n floats
-  const int T = P.n_tile_tasks + P.ntc;
-  for (;;) {
-    // ticket drawn by all 64 lanes of wave 0 (one folded add of 64; ticket =
-    // old / 64): the lane-0-only form hung behind later waits on gfx950
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
-      const int o = __hip_atomic_fetch_add(P.ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (threadIdx.x == 0) tk_s = __builtin_amdgcn_readfirstlane(o) >> 6;
-    }
-    __syncthreads();
-    const int tk = __builtin_amdgcn_readfirstlane(tk_s);
-    __syncthreads();
-#if M3S_PD_DEBUG
-    if (threadIdx.x == 0) printf("pdense: block %d ticket %d of %d (n %d ntr %d ntc %d)\n", (int)blockIdx.x, tk, T, P.n, P.ntr, P.ntc);
-#endif
-    if (tk >= T) break;
-    if (tk < P.n_tile_tasks) {  // column-major lower tiles: column j holds ntr - j tiles
-      int j = 0, base = 0;
-      while (base + (P.ntr - j) <= tk) base += P.ntr - j, j++;
-      pd_tile_task(P, j + (tk - base), j, Si, Sj, Sv, col);
-    } else {
-      const int j = P.ntc - 1 - (tk - P.n_tile_tasks);
-      pd_back_task(P, j, Si, Sv, xs, red);
-      if (j == 0) {  // x_0 is the last segment: every other segment is published
-        for (int k = threadIdx.x; k < P.n; k += kPDThreads)
-          xs[k] = __hip_atomic_load(P.x + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (threadIdx.x == 0)
-          last_s = __hip_atomic_load(P.flags + kFlagFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-                   __hip_atomic_load(P.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int failed = __builtin_amdgcn_readfirstlane(last_s);
-#if M3S_PD_DEBUG
-        if ((threadIdx.x & 63) == 0) printf("pdense: finish wave %d fail %d\n", (int)threadIdx.x >> 6, last_s);
-#endif
-        if (failed) {
-          fail_step(P.n, P.dx_out, P.info, P.flags + kFlagStop, P.delta_thresh);
-          if (threadIdx.x == 0) P.flags[kFlagFail] = 0;
-        } else {
-          finish_step(xs, dxs, nrm, P.n, P.Twc, P.N, P.dx_out, P.info, P.flags + kFlagStop, P.delta_thresh);
-        }
-      }
-    }
-  }
-}
 
 // ------------------------------------------------- block-sparse LLT ----
 // Per edge: H_jj = M L M^T and g_j = M l in fp64 (M = Adj(T_i)^-T), written
@@ -1412,7 +1013,7 @@ struct SparseDev {
   int E, asm_lds;        // asm_lds: assemble in-kernel from fin staged in LDS (else assemble_slots_kernel)
   int nc;                // dense-tail columns (m3s_symbolic.h, clq); 0: none
   double *parts;         // [n_parts][56] partial update blocks (+ partial RHS)
-  int64_t *dbg;  // M3S_LLT_TIMING: per-column DIAG completion stamps
+  int64_t *dbg;  // 0: per-column DIAG completion stamps
   double *L;     // [S][49] (global variant)
   double *Dinv;  // [m][49] (global variant)
   const double *fin;
@@ -1442,9 +1043,7 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   double x = __builtin_amdgcn_rsq(d);
   const double hd = 0.5 * d;
   x = x * (1.5 - hd * x * x);
-#if !M3S_RSQ_ONE_NR
   x = x * (1.5 - hd * x * x);
-#endif
   return x;
 }
 
@@ -1458,9 +1057,6 @@ __device__ __forceinline__ void wait_flag(int32_t *flag, int *fail) {
   }
   if (it >= (1 << 21)) {
     *fail = 1;
-#if M3S_LLT_DEBUG
-    printf("wait timeout on %p\n", (void *)flag);
-#endif
   }
 }
 
@@ -1537,9 +1133,6 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int kStage = M3S_STAGE;                  // updates per staged batch
 constexpr int kSplitUpdates = M3S_SPLIT_UPDATES;   // updates per PART item (global factors)
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
-#ifndef M3S_MFMA_PRODUCTS  // staged block products on the f64 MFMA
-#define M3S_MFMA_PRODUCTS 0
-#endif
 #ifndef M3S_TAIL_TR  // dense-tail trailing update tile, in 7x7 blocks
 #define M3S_TAIL_TR 2
 #endif
@@ -1548,12 +1141,6 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #endif
 #ifndef M3S_TAIL_LOOKAHEAD  // DIAG(k+1) inside step k's trailing update (dense tail)
 #define M3S_TAIL_LOOKAHEAD 1
-#endif
-#ifndef M3S_TAIL2_TR  // the same, in the phase-2 (tail-only) kernel instance
-#define M3S_TAIL2_TR 2
-#endif
-#ifndef M3S_TAIL2_TC
-#define M3S_TAIL2_TC 2
 #endif
 
 // v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
@@ -1584,51 +1171,6 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
     }
     return v;
   }
-#if M3S_MFMA_PRODUCTS
-  // sum_q A_q B_q^T as one K = 7 nq product on the f64 MFMA: the A_q (B_q)
-  // concatenate along k; lane l holds A[row l&15][k 4s + (l>>4)] and
-  // B[k 4s + (l>>4)][col l&15] = B_q(col, kk) (rows / cols >= 7 are zero).
-  // Operands come straight from global memory (no LDS staging); the 7x7
-  // result is moved to the entry layout through the wave's stage area once.
-  {
-    const int rc = lane & 15, kl = lane >> 4;
-    const bool live = rc < 7;
-    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int q = q0; q < q1; q += 4) {
-      const int nb = (q1 - q < 4) ? q1 - q : 4;
-      int ia[4], ib[4];
-#pragma unroll
-      for (int bq = 0; bq < 4; bq++) {
-        ia[bq] = sa[q + (bq < nb ? bq : 0)];
-        ib[bq] = SAME ? ia[bq] : sb[q + (bq < nb ? bq : 0)];
-      }
-      double a[7], b[7];
-#pragma unroll
-      for (int st = 0; st < 7; st++) {
-        const int kg = 4 * st + kl, qq = kg / 7, kk = kg - 7 * qq;  // qq < 4
-        const int sa_ = qq == 0 ? ia[0] : qq == 1 ? ia[1] : qq == 2 ? ia[2] : ia[3];
-        const int sb_ = qq == 0 ? ib[0] : qq == 1 ? ib[1] : qq == 2 ? ib[2] : ib[3];
-        const bool on = live && qq < nb;
-        a[st] = on ? Lb[(size_t)sa_ * 49 + rc * 7 + kk] : 0.0;
-        b[st] = on ? (SAME ? a[st] : Lb[(size_t)sb_ * 49 + rc * 7 + kk]) : 0.0;
-      }
-#pragma unroll
-      for (int st = 0; st < 7; st++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], b[st], acc, 0, 0, 0);
-    }
-    // C/D map: col = lane&15, row = (lane>>4) + 4 i
-    if (live) {
-#pragma unroll
-      for (int i = 0; i < 2; i++) {
-        const int row = kl + 4 * i;
-        if (row < 7) stg[row * 7 + rc] = acc[i];
-      }
-    }
-    wave_lds_fence();
-    v -= stg[lane49];
-    wave_lds_fence();
-    return v;
-  }
-#endif
   double *SA = stg, *SB = SAME ? stg : stg + kStage * 49;
   for (int q = q0; q < q1; q += kStage) {
     const int nb = (q1 - q < kStage) ? q1 - q : kStage;
@@ -1860,26 +1402,12 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // clamped row offsets: lanes >= 49 (>= 7) load valid entries and discard them
   const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
   const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
-#if M3S_LLT_TIMING  // experiment: phase timestamps (100 MHz wall clock) into flags[16..]
-  int64_t *tsv = reinterpret_cast<int64_t *>(D.flags + 16);
-  if (tid == 0 && phase != 2) tsv[0] = wall_clock64();
-#define M3S_TS(i) if (tid == 0) tsv[i] = wall_clock64();
-#else
-#define M3S_TS(i)
-#endif
-#if M3S_LLT_ITEMS  // experiment: per-item (start, inputs ready, published) clock stamps into D.dbg
-// stamp 0 carries the wave id in bits 58.. (dynamic dispatch)
-#define M3S_IT(j) if (lane == 0) D.dbg[4 * it + (j)] = (int64_t)clock64() | ((j) == 0 ? (int64_t)wave << 58 : 0);
-#else
-#define M3S_IT(j)
-#endif
   double *scr = scratch[wave];
 
   if (phase == 2) {  // after border_kernel: y and the failure flag from global memory
     for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
     if (tid == 0) fail_s = D.flags[kFlagSplitFail], next_col = 0;
     __syncthreads();
-    M3S_TS(6)
   } else {
   // 0. assembly. LDS factor with room: the per-edge blocks (fin) are staged
   // in LDS with coalesced loads, then summed per slot in edge order (the sums
@@ -1912,7 +1440,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
   if (tid == 0) fail_s = 0, next_item = 0, next_col = 0, next_b0 = 0;
   __syncthreads();
-  M3S_TS(1)
 
   // 1. factorisation + forward substitution as a dataflow over work items:
   // DIAG(k) (diagonal block and W_k = L_kk^-1, then the forward step of y_k),
@@ -1928,10 +1455,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     const int it = wave_ticket(&next_item);
     if (it >= n_disp) break;
     const int item = witems[it];
-#if M3S_LLT_DEBUG
-    if (lane == 0) printf("wave %d takes %d/%d item %d\n", wave, it, n_disp, item);
-#endif
-    M3S_IT(0)
     if (item >= n_tasks) {  // PART: partial sum of the head of a long update list
       const int pi = item - n_tasks, tg = part_tgt[pi];
       const int q0 = part_q0[pi], q1 = part_q1[pi];
@@ -1943,13 +1466,11 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       } else {  // of OFF(t): sum L_ip L_kp^T
         M3S_POLL(q0, q1, flag_set(&sdone[tr_a[q]]) && flag_set(&sdone[tr_b[q]]), (v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, qa, qb, r7, c7, lane49, lane, stg)));
       }
-      M3S_IT(1)
       double *pb = D.parts + (size_t)pi * 56;
       if (act49) pb[lane] = v;
       if (lane < 7) pb[49 + lane] = bp;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&pdone[pi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      M3S_IT(2)
     } else if (item < 0) {  // DIAG(k): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
       const int k = -1 - item;
       const int p0 = split ? dpart_ptr[k] : 0, p1 = split ? dpart_ptr[k + 1] : 0;
@@ -1958,13 +1479,11 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       double v = Lb[(size_t)k * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
-      M3S_IT(1)
       double Lr[7][7], dinv[7];
       const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, Lr, dinv);
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      M3S_IT(3)
       // forward step, off the factorisation's critical path:
       // y_k = L_kk^-1 (b_k - sum_p L_kp y_p)
       double bb = y[k * 7 + lane7];
@@ -1973,7 +1492,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       fwd_solve_store(bb, Lr, dinv, y + (size_t)k * 7, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&ydone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      M3S_IT(2)
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
       const int t2 = item;
       const int dst = task_dst[t2], k = task_col[t2];
@@ -1986,7 +1504,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[tr_a[q]]) && flag_set(&sdone[tr_b[q]]), (v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, qa, qb, r7, c7, lane49, lane, stg)));
       wait_flag(&sdone[k], &fail_s);  // W_k
-      M3S_IT(1)
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -1996,24 +1513,13 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       wave_lds_fence();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      M3S_IT(2)
     }
-#if M3S_LLT_DEBUG
-    if (lane == 0) printf("wave %d done %d\n", wave, it);
-#endif
   }
-#if M3S_LLT_DEBUG
-  if (lane == 0) printf("wave %d at barrier\n", wave);
-#endif
   __syncthreads();
-#if M3S_LLT_DEBUG
-  if (tid == 0) printf("factor done fail %d\n", fail_s);
-#endif
 
   if (phase == 1) {  // hand y and the failure flag to border_kernel / phase 2
     for (int idx = tid; idx < m * 7; idx += 1024) const_cast<double *>(D.rhs)[idx] = y[idx];
     if (tid == 0) D.flags[kFlagSplitFail] = fail_s;
-    M3S_TS(5)
     return;
   }
   }  // phase != 2
@@ -2022,7 +1528,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // c0 whose structure is every later column) factored right-looking,
   // bulk-synchronously, after the dataflow items (which cover columns < c0,
   // including the border blocks L_ik, i >= c0 > k, and all y_p, p < c0).
-  if (phase == 0) { M3S_TS(5) }
   if (D.nc > 0) {
     const int32_t *clq = pl + D.off[28];
     const int nc = clq[0], c0 = clq[1];
@@ -2035,7 +1540,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       border_task<STAGE>(t, nc, c0, pl, D.off, Lb, y, r7, c7, lane49, lane, lane7, act49, stg);
     }
     __syncthreads();
-    if (phase == 0) { M3S_TS(6) }
     // B1: per tail column k: L_kk, W_k, y_k (one wave) | L_ik = A_ik W_k^T,
     // y_i -= L_ik y_k (a wave per row; global factors also copy column k into
     // an LDS panel) | A_ij -= L_ik L_jk^T (kTR x kTC block tiles per wave,
@@ -2043,12 +1547,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     // off-diagonal blocks of the tail are the last slots, column-major.
     const int cbase = S - nc * (nc - 1) / 2;
     double *panel = stg - (size_t)wave * kStageDoubles;  // the stage areas (global factors only)
-#if M3S_LLT_TIMING  // experiment: wave 0's cycles in B1 sub-steps, summed over the tail
-    int64_t bt[7] = {0, 0, 0, 0, 0, 0, 0}, t_0 = clock64();
-#define M3S_BT(i) { const int64_t t_ = clock64(); bt[i] += t_ - t_0; t_0 = t_; }
-#else
-#define M3S_BT(i)
-#endif
     // diagonal block kk: L_kk, W_k, forward step y_k (wave 0)
     auto tail_diag = [&](int kk) {
       const double v = Lb[(size_t)kk * 49 + lane49];
@@ -2069,10 +1567,8 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       const int col0 = cbase + ci * nc - ci * (ci + 1) / 2;  // slot of L_{k+1, k}
 #if !M3S_TAIL_LOOKAHEAD
       if (wave == 0) tail_diag(k);
-      M3S_BT(0)
       __syncthreads();
 #endif
-      M3S_BT(1)
       const int nr = nc - ci - 1;
       for (int rr = wave; rr < nr; rr += NW) {
         const int dst = col0 + rr;
@@ -2095,15 +1591,13 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
         wave_lds_fence();
       }
       if (tid == 0) next_tile = 64;  // trailing tiles 1.. by ticket (tile 0: wave 0)
-      M3S_BT(2)
       __syncthreads();
-      M3S_BT(3)
       const double *Pk = STAGE ? panel : Lb + (size_t)col0 * 49;  // L_{k+1+rr, k} at Pk + 49 rr
       // trailing tiles of kTR block rows x kTC block columns (rr >= cc): each
       // panel row is read from LDS once per tile and used for every block of
       // the tile ((kTR + kTC) * 7 LDS reads per lane for kTR * kTC blocks
       // instead of 14 per block)
-      constexpr int kTR = TAIL ? M3S_TAIL2_TR : M3S_TAIL_TR, kTC = TAIL ? M3S_TAIL2_TC : M3S_TAIL_TC,
+      constexpr int kTR = TAIL ? 2 : M3S_TAIL_TR, kTC = TAIL ? 2 : M3S_TAIL_TC,
                     kTB = kTR * kTC;
       const int nrt = (nr + kTR - 1) / kTR, nct = (nr + kTC - 1) / kTC;
       int ntile = 0;
@@ -2160,21 +1654,12 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
 #if M3S_TAIL_LOOKAHEAD
         if (t == 0) {  // wave 0: block (k+1, k+1) is final (this tile, rr = cc = 0)
           wave_lds_fence();
-          M3S_BT(4)
           tail_diag(k + 1);
-          M3S_BT(0)
         }
 #endif
       }
-      M3S_BT(4)
       __syncthreads();
-      M3S_BT(5)
     }
-#if M3S_LLT_TIMING
-    if (tid == 0)
-      for (int i = 0; i < 6; i++) D.dbg[i] = bt[i];
-#endif
-    M3S_TS(7)
     // B2: back-substitution of the tail, x_k = W_k^T y_k (one wave), then
     // y_j -= L_kj^T x_k for the tail columns j < k (a wave per column)
     for (int ci = nc - 1; ci >= 0; ci--) {
@@ -2204,7 +1689,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     fail_step(7 * m, D.dx_out, D.info, D.flags + kFlagStop, D.delta_thresh);
     return;
   }
-  M3S_TS(2)
 
   // 2. back-substitution L^T x = y in reverse level order (x overwrites y),
   // dataflow: column k waits for x_i of every i in struct(k)
@@ -2215,9 +1699,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     if (t >= m) break;
     const int k = lev_col[m - 1 - t];
     if (k >= m - D.nc) continue;  // dense tail: done above
-#if M3S_LLT_DEBUG
-    if (lane == 0) printf("wave %d backsub t %d k %d\n", wave, t, k);
-#endif
     const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
     double rr = y[k * 7 + lane7];
     M3S_POLL(q0, q1, flag_set(&done2[col_row[q]]), (rr = sub_matvec<STAGE, true>(rr, Lb, col_slot, col_row, qa, qb, y, lane7, lane49, lane, stg)));
@@ -2233,7 +1714,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
   __syncthreads();
 
-  M3S_TS(3)
   // 3. dx = -x in the original variable order, retraction, ||dx||
   float part = 0.0f;
   for (int idx = tid; idx < m * 7; idx += 1024) {
@@ -2257,7 +1737,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     float s2 = 0.0f;
     for (int w2 = 0; w2 < NW; w2++) s2 += nrm[w2];
     D.info[M3S_INFO_ITERS] += 1;
-    M3S_TS(4)
     if (sqrtf(s2) < D.delta_thresh) {
       D.info[M3S_INFO_CONVERGED] = 1;
       D.flags[kFlagStop] = 1;
@@ -2501,7 +1980,6 @@ inline int dense_tail_min() {
 
 struct PlanMeta {
   bool sparse = false;
-  bool pdense = false;  // persistent multi-workgroup dense LLT (pdense_llt_kernel)
   int store = 0;  // sparse_llt_kernel<STORE>
   bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
   size_t lds_bytes = 0;
@@ -2526,12 +2004,6 @@ struct PlanMeta {
 std::mutex g_reg_mu;
 std::unordered_map<const void *, PlanMeta> g_reg;
 
-#ifndef M3S_PACK
-#define M3S_PACK 1  // store target-side planes on the first iteration, read them after
-#endif
-#ifndef M3S_TASKS
-#define M3S_TASKS 1  // XCD-grouped task table
-#endif
 // Task table: the E_loc x chunks (edge, chunk) tasks sorted by (chunk, KF j),
 // cut into 8 contiguous runs, run x dealt to blocks x, x+8, x+16, ... so the
 // edges that stream the same Xj chunk run back to back on one XCD (blocks b
@@ -2585,8 +2057,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.P = P;
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xs, 16) && vec_ok(a->Cs, 16) && vec_ok(a->Q, 16) &&
                    vec_ok(a->idx_ii2jj, 16) && vec_ok(a->valid_match, 4);
-  const char *no_pack = std::getenv("M3S_NO_PACK"), *no_tasks = std::getenv("M3S_NO_TASKS");
-  const bool can_pack = M3S_PACK && vec && !(no_pack && no_pack[0] == '1') &&
+  const bool can_pack = vec &&
                         (a->mode != M3S_MODE_CALIB || (a->width < 65536 && a->height < 32768));
   int64_t blocks = E_loc * L.chunks;
   int pack = 0;
@@ -2598,7 +2069,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
     if (M.range_b != eb || M.range_e != ee) {  // a sharded rank's own edge range
       M.range_b = eb, M.range_e = ee, M.planes_ok = false;
       M.n_blocks = 0;
-      if (M3S_TASKS && !(no_tasks && no_tasks[0] == '1') && (int64_t)M.rj.size() >= ee) {
+      if ((int64_t)M.rj.size() >= ee) {
         // fresh host buffer: an earlier upload from tasks_r may still be queued
         if (!M.tasks_r.empty()) M.tasks_old.push_back(std::move(M.tasks_r));  // freed at the next prepare
         M.tasks_r.clear();
@@ -2719,39 +2190,6 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
   assemble_kernel<<<dim3((unsigned)a->N), dim3(256), 0, st>>>(
       edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, ld, A, stop);
   if ((rc = launch_ok())) return rc;
-  if (meta.pdense) {
-    const int ntr = (int)(n / kPT) + 1, ntc = (int)((n + kPT - 1) / kPT);
-    int32_t *pf = at<int32_t>(ws, Ly.dtile);
-    if (hipMemsetAsync(pf, 0, pd_flag_bytes(ld), st) != hipSuccess) return M3S_ELAUNCH;
-    PDenseArgs P;
-    P.A = A;
-    P.ld = ld;
-    P.n = (int)n;
-    P.ntr = ntr;
-    P.ntc = ntc;
-    P.n_tile_tasks = ntc * ntr - ntc * (ntc - 1) / 2;  // sum over tile columns j of (ntr - j)
-    P.tflag = pf;
-    P.xflag = pf + (size_t)ntr * ntc;
-    P.ctr = P.xflag + ntc;
-    P.x = at<double>(ws, Ly.dx_vec);
-    P.Twc = a->Twc;
-    P.N = a->N;
-    P.dx_out = dx;
-    P.info = a->info;
-    P.flags = flags;
-    P.delta_thresh = a->delta_thresh;
-    const size_t dyn = (size_t)ntr * kPT * (sizeof(double) + sizeof(float));
-    if (dyn > 48 * 1024) {
-      static std::once_flag once;
-      std::call_once(once, [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(pdense_llt_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
-      });
-    }
-    const int T = P.n_tile_tasks + ntc;
-    pdense_llt_kernel<<<dim3((unsigned)std::min(T, kPDGrid)), dim3(kPDThreads), dyn, st>>>(P);
-    return launch_ok();
-  }
   const int np = (int)n + 1;
   if (np <= kMaxSmallNp) {
     const int nbc = (np + 31) / 32;
@@ -2792,26 +2230,6 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
 
 // Per call: zero state, bring ii/jj to the host (the reference's _unique /
 // searchsorted also synchronise), rank them, build and upload the sparse plan.
-// Solver choice. M3S_SOLVER=sparse|pdense overrides. The persistent dense
-// LLT is opt-in: measured on MI355X it is correct and bitwise reproducible
-// but 2-6x slower than the sparse LLT at every size (270 us at 32 KFs, 2.5 ms
-// at 256; DESIGN.md §4 "A/B: persistent dense LLT"), so no graph size takes
-// it by default.
-constexpr int64_t kPDenseMinN = INT64_MAX;
-int solver_override() {
-  const char *e = std::getenv("M3S_SOLVER");
-  if (!e) return 0;
-  if (!strcmp(e, "sparse")) return 1;
-  if (!strcmp(e, "pdense")) return 2;
-  return 0;
-}
-bool want_pdense(int64_t N) {
-  const int o = solver_override();
-  if (o == 1) return false;
-  if (o == 2) return N > 1;
-  return N >= kPDenseMinN;
-}
-
 // Host symbolic plans of recent edge sets (the same factor graph is usually
 // solved many times: every keyframe's local/global optimisation, every bench
 // step). Keyed by (N, HW, E, dense override, remapped ranks).
@@ -2819,11 +2237,16 @@ struct PlanCacheEntry {
   int64_t N = 0, HW = 0, E = 0;
   bool dense = false;
   int tail_min = 0;  // dense_tail_min() the plan was built with
-  int solver = 0;    // solver_override() the plan was built with
   std::vector<int32_t> ri, rj;
   PlanMeta meta;
 };
 std::mutex g_cache_mu;
+// M3S_PLAN_CACHE=0: every solve call runs the host symbolic analysis (cold
+// calls; bench.py times them this way beside the cached figure)
+inline bool plan_cache_enabled() {
+  const char *e = std::getenv("M3S_PLAN_CACHE");
+  return !(e && e[0] == '0');
+}
 std::vector<PlanCacheEntry> g_cache;  // most recent first
 constexpr size_t kPlanCacheSize = 4;
 
@@ -2846,8 +2269,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
                          const std::vector<int32_t> &rj, bool force_dense) {
   PlanMeta meta;
   const int64_t E = a->E;
-  meta.pdense = !force_dense && want_pdense(a->N);
-  if (a->N > 1 && !meta.pdense) {
+  if (a->N > 1) {
     SparsePlan P;
     // split long update lists only when the factor lives in global memory
     // (its products are the slow, staged ones there)
@@ -2901,7 +2323,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
   meta.h_ri = ri;
   // task table of the full edge range (the single-GPU call and world size 1);
   // a sharded rank's first m3s_gn_linearize builds its own
-  if (M3S_TASKS && E > 0) {
+  if (E > 0) {
     build_tasks(meta.rj, 0, E, chunks_for(a->HW, E), meta.tasks);
     meta.n_blocks_full = (int64_t)meta.tasks.size();
   }
@@ -2935,12 +2357,13 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   PlanMeta meta;
   if (!bad) {
     bool hit = false;
-    {
+    const bool use_cache = plan_cache_enabled();
+    if (use_cache) {
       std::lock_guard<std::mutex> g(g_cache_mu);
       for (size_t q = 0; q < g_cache.size(); q++) {
         const PlanCacheEntry &C = g_cache[q];
         if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense &&
-            C.tail_min == dense_tail_min() && C.solver == solver_override() && C.ri == ri && C.rj == rj) {
+            C.tail_min == dense_tail_min() && C.ri == ri && C.rj == rj) {
           meta = C.meta;
           std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
           hit = true;
@@ -2953,9 +2376,8 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       PlanCacheEntry C;
       C.N = a->N, C.HW = a->HW, C.E = E, C.dense = force_dense, C.ri = ri, C.rj = rj, C.meta = meta;
       C.tail_min = dense_tail_min();
-      C.solver = solver_override();
       std::lock_guard<std::mutex> g(g_cache_mu);
-      g_cache.insert(g_cache.begin(), std::move(C));
+      if (use_cache) g_cache.insert(g_cache.begin(), std::move(C));
       if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
     }
   } else {
@@ -3252,6 +2674,15 @@ int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
   if (!edge_sums) return M3S_EINVAL;
   if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
   return gn_solve_impl(a, edge_sums, nullptr, 0, S(stream));
+}
+
+int m3s_gn_release(const m3s_gn_args *a, void *stream) {
+  if (!a || !a->workspace) return M3S_EINVAL;
+  // the entry owns the host buffers of uploads that may still be queued
+  if (hipStreamSynchronize(S(stream)) != hipSuccess) return M3S_ELAUNCH;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  g_reg.erase(a->workspace);
+  return M3S_OK;
 }
 
 size_t m3s_track_workspace_size(int64_t HW) {

@@ -89,6 +89,13 @@ class HipOps:
         self.be._raise(self.be._lib.m3s_gn_solve(ctypes.byref(self.args), self.be._p(es),
                                                  self.stream), "m3s_gn_solve")
 
+    def close(self):
+        """Drop the library's host state of this workspace (m3s_gn_release)."""
+        if self.args is not None:
+            self.be._raise(self.be._lib.m3s_gn_release(ctypes.byref(self.args), self.stream),
+                           "m3s_gn_release")
+            self.args = None
+
 
 class ShardedGN:
     """Per-rank state of one sharded GN problem.
@@ -154,26 +161,29 @@ class ShardedGN:
         return [self.ops.dx]
 
     def solve_timed(self, max_iter: int, delta_thresh: float, stream):
-        """solve() with a HIP event pair on `stream` around every linearize
-        launch (the kernel plus its small per-edge reduce, in the solve's own
-        launch pattern). Returns the per-iteration durations in ms."""
+        """solve() with HIP event pairs on `stream` around every linearize
+        launch (the kernel plus its small per-edge reduce) and every solve
+        launch, in the solve's own launch pattern. Returns the per-iteration
+        durations in ms: (linearize, solve)."""
         self.ops.prepare(delta_thresh)
         evs = []
         for _ in range(int(max_iter)):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record(stream)
             if self.ee > self.eb:
                 self.ops.linearize(self.eb, self.ee, self.es_loc)
-            e1.record(stream)
-            evs.append((e0, e1))
+            e[1].record(stream)
             if self.world > 1:
                 dist.all_gather_into_tensor(self.es_all, self.es_loc, group=self.group)
                 es = self.es_all
             else:
                 es = self.es_loc
+            e[2].record(stream)
             self.ops.solve(es)
+            e[3].record(stream)
+            evs.append(e)
         torch.cuda.synchronize()
-        return [a.elapsed_time(b) for a, b in evs]
+        return [e[0].elapsed_time(e[1]) for e in evs], [e[2].elapsed_time(e[3]) for e in evs]
 
     def linearize_only(self):
         """Timing hook: just the linearize kernel on this rank's slice."""

@@ -116,7 +116,7 @@ class TrackArgs(ctypes.Structure):
 # every symbol include/m3s_gn.h declares
 EXPORTS = (
     "m3s_gn_workspace_size", "m3s_gauss_newton_points", "m3s_gauss_newton_rays",
-    "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve",
+    "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve", "m3s_gn_release",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
     "m3s_fuse_pointmap", "m3s_prep_rays",
@@ -142,6 +142,8 @@ def _load():
     lib.m3s_gn_linearize.argtypes = [P(GnArgs), ctypes.c_int64, ctypes.c_int64, _VP, _VP]
     lib.m3s_gn_solve.restype = ctypes.c_int
     lib.m3s_gn_solve.argtypes = [P(GnArgs), _VP, _VP]
+    lib.m3s_gn_release.restype = ctypes.c_int
+    lib.m3s_gn_release.argtypes = [P(GnArgs), _VP]
     lib.m3s_track_workspace_size.restype = ctypes.c_size_t
     lib.m3s_track_workspace_size.argtypes = [ctypes.c_int64]
     for f in ("m3s_track_rays_sim3", "m3s_track_calib_sim3"):
@@ -315,8 +317,14 @@ def make_gn_args(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, K=None, *
 
 
 def _run_gn(fn_name, a, keep):
-    rc = getattr(_lib, fn_name)(ctypes.byref(a), _stream(keep["Xs"].device))
+    st = _stream(keep["Xs"].device)
+    rc = getattr(_lib, fn_name)(ctypes.byref(a), st)
+    # the per-call workspace goes back to the caching allocator: drop its host
+    # state too (m3s_gn_release; one stream sync, the call's result is needed
+    # by the caller anyway — the reference syncs every iteration)
+    rc_rel = _lib.m3s_gn_release(ctypes.byref(a), st)
     _raise(rc, fn_name)
+    _raise(rc_rel, "m3s_gn_release")
     return [keep["dx"]]
 
 
@@ -508,6 +516,10 @@ def gn_linearize(a, keep, edge_begin, edge_end, edge_sums):
     rc = _lib.m3s_gn_linearize(ctypes.byref(a), int(edge_begin), int(edge_end), _p(edge_sums),
                                _stream(keep["Xs"].device))
     _raise(rc, "m3s_gn_linearize")
+
+
+def gn_release(a, keep):
+    _raise(_lib.m3s_gn_release(ctypes.byref(a), _stream(keep["Xs"].device)), "m3s_gn_release")
 
 
 def gn_solve(a, keep, edge_sums):

@@ -38,6 +38,16 @@
 #include <string.h>
 
 #define NTHR 256 /* the reference's THREADS (gn_kernels.cu:28) */
+/* Accumulator type of the per-edge sums: float is the reference's (thread
+ * sums, blockReduce and the Hs/gs tensors are fp32). Built a second time with
+ * -DORACLE_ACC=double (libgn_oracle_f64.so): the same per-pixel fp32
+ * arithmetic with exact-enough sums, the yardstick that separates the
+ * reference's own fp32 summation noise (x cond(H)) from real differences in
+ * the large-graph parity tests. */
+#ifndef ORACLE_ACC
+#define ORACLE_ACC float
+#endif
+typedef ORACLE_ACC acc_t;
 #define TRI 105  /* 14*15/2 */
 
 enum { MODE_POINTS = 0, MODE_RAYS = 1, MODE_CALIB = 2 };
@@ -286,16 +296,16 @@ static int rows_for_pixel(const params_t *P, const float *Tij, const float *Xi, 
 /* Hs: [4][E][7][7], gs: [2][E][7]; ranks ix/jx index Twc/Xs/Cs. */
 static void edge_blocks(const params_t *P, const float *Twc, const float *Xs, const float *Cs,
                         int HW, int e, int ix, int jx, const int64_t *idx, const uint8_t *valid,
-                        const float *Q, int E, float *Hs, float *gs) {
-  float *acc = (float *)calloc((size_t)NTHR * (TRI + 14), sizeof(float));
+                        const float *Q, int E, acc_t *Hs, acc_t *gs) {
+  acc_t *acc = (acc_t *)calloc((size_t)NTHR * (TRI + 14), sizeof(acc_t));
   float Tij[8];
   relative(Twc + 8 * ix, Twc + 8 * jx, Tij);
   const float *Ti = Twc + 8 * ix;
   const float *Xs_i = Xs + (size_t)ix * HW * 3, *Xs_j = Xs + (size_t)jx * HW * 3;
   const float *Cs_i = Cs + (size_t)ix * HW, *Cs_j = Cs + (size_t)jx * HW;
   for (int k = 0; k < HW; k++) {
-    float *h = acc + (size_t)(k % NTHR) * (TRI + 14);
-    float *vi = h + TRI, *vj = h + TRI + 7;
+    acc_t *h = acc + (size_t)(k % NTHR) * (TRI + 14);
+    acc_t *vi = h + TRI, *vj = h + TRI + 7;
     const size_t ek = (size_t)e * HW + k;
     const int vm = valid[ek] != 0;
     const int64_t id = vm ? idx[ek] : 0;
@@ -318,10 +328,10 @@ static void edge_blocks(const params_t *P, const float *Twc, const float *Xs, co
   /* shared-memory tree, entry by entry (blockReduce) */
   for (int stride = NTHR / 2; stride >= 1; stride >>= 1)
     for (int t = 0; t < stride; t++) {
-      float *a = acc + (size_t)t * (TRI + 14), *b = acc + (size_t)(t + stride) * (TRI + 14);
+      acc_t *a = acc + (size_t)t * (TRI + 14), *b = acc + (size_t)(t + stride) * (TRI + 14);
       for (int x = 0; x < TRI + 14; x++) a[x] += b[x];
     }
-  const float *h = acc, *vi = acc + TRI, *vj = acc + TRI + 7;
+  const acc_t *h = acc, *vi = acc + TRI, *vj = acc + TRI + 7;
   for (int n = 0; n < 7; n++) {
     gs[(size_t)(0 * E + e) * 7 + n] = vi[n];
     gs[(size_t)(1 * E + e) * 7 + n] = vj[n];
@@ -330,7 +340,7 @@ static void edge_blocks(const params_t *P, const float *Twc, const float *Xs, co
   int l = 0;
   for (int n = 0; n < 14; n++)
     for (int m = 0; m <= n; m++, l++) {
-      const float val = h[l];
+      const acc_t val = h[l];
       if (n < 7) {
         HS(0, n, m) = val;
         HS(0, m, n) = val;
@@ -417,10 +427,14 @@ int oracle_edge_blocks(const params_t *P, const float *Twc, const float *Xs, con
       free(ri), free(rj);
       return -1;
     }
+  acc_t *Ha = (acc_t *)calloc((size_t)4 * E * 49 + 1, sizeof(acc_t));
+  acc_t *ga = (acc_t *)calloc((size_t)2 * E * 7 + 1, sizeof(acc_t));
 #pragma omp parallel for schedule(dynamic, 1)
   for (int e = 0; e < E; e++)
-    edge_blocks(P, Twc, Xs, Cs, HW, e, ri[e], rj[e], idx, valid, Q, E, Hs, gs);
-  free(ri), free(rj);
+    edge_blocks(P, Twc, Xs, Cs, HW, e, ri[e], rj[e], idx, valid, Q, E, Ha, ga);
+  for (size_t k = 0; k < (size_t)4 * E * 49; k++) Hs[k] = (float)Ha[k];
+  for (size_t k = 0; k < (size_t)2 * E * 7; k++) gs[k] = (float)ga[k];
+  free(Ha), free(ga), free(ri), free(rj);
   return 0;
 }
 
@@ -442,8 +456,8 @@ int oracle_gn(const params_t *P, float *Twc, const float *Xs, const float *Cs, i
       free(ri), free(rj);
       return -1;
     }
-  float *Hs = (float *)calloc((size_t)4 * E * 49 + 1, sizeof(float));
-  float *gs = (float *)calloc((size_t)2 * E * 7 + 1, sizeof(float));
+  acc_t *Hs = (acc_t *)calloc((size_t)4 * E * 49 + 1, sizeof(acc_t));
+  acc_t *gs = (acc_t *)calloc((size_t)2 * E * 7 + 1, sizeof(acc_t));
   double *A = (double *)malloc(sizeof(double) * ((size_t)n * n + 1));
   double *b = (double *)malloc(sizeof(double) * ((size_t)n + 1));
   int it = 0;

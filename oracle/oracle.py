@@ -18,6 +18,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libgn_oracle.so")
+LIB_F64_PATH = os.path.join(HERE, "libgn_oracle_f64.so")  # fp64 per-edge sums (yardstick)
 
 MODE_POINTS, MODE_RAYS, MODE_CALIB = 0, 1, 2
 
@@ -40,19 +41,20 @@ class Params(ctypes.Structure):
     ]
 
 
-_lib = None
+_libs = {}
 
 
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(f64=False):
+    path = LIB_F64_PATH if f64 else LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        _lib = ctypes.CDLL(LIB_PATH)
+        _lib = ctypes.CDLL(path)
+        _libs[path] = _lib
         P = ctypes.c_void_p
         _lib.oracle_gn.restype = ctypes.c_int
         _lib.oracle_gn.argtypes = [
@@ -67,7 +69,7 @@ def lib():
         for f in ("oracle_retract", "oracle_adjT_inv", "oracle_relative"):
             getattr(_lib, f).restype = None
             getattr(_lib, f).argtypes = [P, P, P] if f != "oracle_retract" else [P, P]
-    return _lib
+    return _libs[path]
 
 
 def _c(a, dtype):
@@ -108,12 +110,13 @@ def _inputs(Twc, Xs, Cs, ii, jj, idx, valid, Q):
     return Twc, Xs, Cs, ii, jj, idx, valid, Q, N, HW, E
 
 
-def gn(params, Twc, Xs, Cs, ii, jj, idx, valid, Q, max_iter, delta_thresh):
-    """Returns (Twc_out [N,8], dx [N-1,7], iters, solve_failed)."""
+def gn(params, Twc, Xs, Cs, ii, jj, idx, valid, Q, max_iter, delta_thresh, f64=False):
+    """Returns (Twc_out [N,8], dx [N-1,7], iters, solve_failed). f64: the
+    fp64-accumulator build (not the reference's arithmetic; a yardstick)."""
     Twc, Xs, Cs, ii, jj, idx, valid, Q, N, HW, E = _inputs(Twc, Xs, Cs, ii, jj, idx, valid, Q)
     dx = np.zeros((max(N - 1, 0), 7), np.float32)
     failed = ctypes.c_int(0)
-    it = lib().oracle_gn(
+    it = lib(f64).oracle_gn(
         ctypes.byref(params), _ptr(Twc), _ptr(Xs), _ptr(Cs), N, HW, _ptr(ii), _ptr(jj), E,
         _ptr(idx), _ptr(valid), _ptr(Q), int(max_iter), float(delta_thresh), _ptr(dx),
         ctypes.byref(failed),

@@ -99,13 +99,61 @@ class OracleOps:
             self.stop = True
 
 
+class LocalFormOracleOps(OracleOps):
+    """CPU stand-in with the HIP path's payload: per edge the 36 fp64 values of
+    m3s_gn_linearize (include/m3s_gn.h) — L's upper triangle (28, row-major),
+    l (7), cost (1) in the frame of the residual — and a solve that maps them
+    through M = Adj(T_i)^-T exactly as the device finalize does (H_jj = M L M^T,
+    g_j = M l; Hs[0] = Hs[3] = H_jj, Hs[1] = Hs[2] = -H_jj, gs[0] = -g_j,
+    gs[1] = g_j). L and l come from the oracle's reference blocks
+    (L = M^-1 Hs[3] M^-T, l = M^-1 gs[1])."""
+
+    stride = 36
+
+    def linearize(self, eb, ee, es_loc):
+        T = self.Twc.numpy()
+        iu = np.triu_indices(7)
+        for k, e in enumerate(range(eb, ee)):
+            a, b = int(self.ri[e]), int(self.rj[e])
+            lo, hi = min(a, b), max(a, b)
+            sel = [lo, hi] if lo != hi else [lo]
+            Hs, gs = self.orc.edge_blocks(
+                self.params, T[sel], self.Xs[sel], self.Cs[sel],
+                np.array([self.ii[e]]), np.array([self.jj[e]]), self.idx[k:k + 1],
+                self.valid[k:k + 1], self.Q[k:k + 1])
+            Mi = np.linalg.inv(self.orc.adjT_inv_matrix(T[a]).astype(np.float64))
+            L = Mi @ Hs[3, 0].astype(np.float64) @ Mi.T
+            l = Mi @ gs[1, 0].astype(np.float64)
+            es_loc[k] = torch.from_numpy(np.concatenate([L[iu], l, [0.0]]))
+
+    def solve(self, es):
+        if self.stop:
+            return
+        N = self.Twc.shape[0]
+        T = self.Twc.numpy()
+        P = es.numpy()
+        iu = np.triu_indices(7)
+        Hs = np.zeros((len(self.ri), 4, 7, 7))
+        gs = np.zeros((len(self.ri), 2, 7))
+        for e in range(len(self.ri)):
+            L = np.zeros((7, 7))
+            L[iu] = P[e, :28]
+            L = L + L.T - np.diag(np.diag(L))
+            M = self.orc.adjT_inv_matrix(T[int(self.ri[e])]).astype(np.float64)
+            Hjj, gj = M @ L @ M.T, M @ P[e, 28:35]
+            Hs[e] = (Hjj, -Hjj, -Hjj, Hjj)
+            gs[e] = (-gj, gj)
+        full = np.concatenate([Hs.reshape(len(self.ri), -1), gs.reshape(len(self.ri), -1)], 1)
+        super().solve(torch.from_numpy(full))
+
+
 def _graph():
     from mast3r_slam_amd import synthetic
 
     return synthetic.make_graph(N_KF, H, W, seed=41)
 
 
-def _rank_main(rank, world, port, out_dir):
+def _rank_main(rank, world, port, out_dir, local_form=False):
     _paths()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -114,8 +162,8 @@ def _rank_main(rank, world, port, out_dir):
         E = g.n_edges
         eb, ee, _ = edge_slice(E, rank, world)
         Twc = g.T_init.data.clone()
-        ops = OracleOps(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj[eb:ee], g.valid_match[eb:ee],
-                        g.Q[eb:ee])
+        cls = LocalFormOracleOps if local_form else OracleOps
+        ops = cls(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj[eb:ee], g.valid_match[eb:ee], g.Q[eb:ee])
         solver = ShardedGN(1, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj[eb:ee],
                            g.valid_match[eb:ee], g.Q[eb:ee], E, sigma_a=SIG[0], sigma_b=SIG[1],
                            ops=ops)
@@ -133,11 +181,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_gn_matches_single_process_oracle(world, tmp_path):
+@pytest.mark.parametrize("world,local_form", [(2, False), (3, False), (2, True), (4, True)])
+def test_sharded_gn_matches_single_process_oracle(world, local_form, tmp_path):
+    """local_form: the 36-double per-edge payload of the HIP path
+    (m3s_gn_linearize) travels through the gloo all-gather."""
     from oracle import oracle as orc
 
-    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path), local_form), nprocs=world, join=True)
     Ts = [np.load(tmp_path / f"T_{r}.npy") for r in range(world)]
     for r in range(1, world):
         assert np.array_equal(Ts[0], Ts[r]), f"rank {r} poses differ from rank 0"

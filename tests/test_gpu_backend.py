@@ -289,7 +289,6 @@ def test_sparse_llt_matches_dense_llt(be, N, tail, monkeypatch):
     from mast3r_slam_amd import synthetic
 
     monkeypatch.setenv("M3S_DENSE_TAIL_MIN", tail)
-    monkeypatch.setenv("M3S_SOLVER", "sparse")  # pin the sparse LLT whatever the default policy
     g = synthetic.make_graph(N, 24, 32, seed=90 + N)
     T_s, dx_s, info_s = run_gpu(be, "rays", g, 3, 0.0)
     monkeypatch.setenv("M3S_DENSE", "1")
@@ -308,7 +307,6 @@ def test_border_split_is_bitwise_identical(be, monkeypatch):
     from mast3r_slam_amd import synthetic
 
     monkeypatch.setenv("M3S_DENSE_TAIL_MIN", "8")
-    monkeypatch.setenv("M3S_SOLVER", "sparse")
     g = synthetic.make_graph(140, 24, 32, seed=77)
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     monkeypatch.setenv("M3S_BORDER_SPLIT", "0")
@@ -316,49 +314,3 @@ def test_border_split_is_bitwise_identical(be, monkeypatch):
     assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
     np.testing.assert_array_equal(T_a, T_b)
     np.testing.assert_array_equal(dx_a, dx_b)
-
-
-@pytest.mark.parametrize("N", [2, 6, 33, 70, 140, 260])
-def test_persistent_dense_llt_matches_dense_llt(be, N, monkeypatch):
-    """Persistent multi-workgroup dense LLT (pdense_llt_kernel: 32x32 fp64
-    tiles, MFMA updates, dataflow back-substitution; M3S_SOLVER=pdense, the
-    opt-in) against the single-workgroup dense paths
-    (M3S_DENSE=1) on identical inputs."""
-    from mast3r_slam_amd import synthetic
-
-    g = synthetic.make_graph(N, 24, 32, seed=190 + N)
-    monkeypatch.setenv("M3S_SOLVER", "pdense")
-    T_p, dx_p, info_p = run_gpu(be, "rays", g, 3, 0.0)
-    T_p2, dx_p2, _ = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.setenv("M3S_DENSE", "1")
-    T_d, dx_d, info_d = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.delenv("M3S_DENSE")
-    assert info_p[be.INFO_ITERS] == info_d[be.INFO_ITERS] == 3
-    assert info_p[be.INFO_SOLVE_FAIL] == info_d[be.INFO_SOLVE_FAIL] == 0
-    np.testing.assert_array_equal(T_p, T_p2)  # bitwise reproducible (sharded ranks rely on it)
-    np.testing.assert_array_equal(dx_p, dx_p2)
-    np.testing.assert_allclose(dx_p, dx_d, atol=1e-6 + 1e-5 * np.abs(dx_d).max())
-    np.testing.assert_allclose(T_p, T_d, atol=1e-5)
-
-
-def test_persistent_dense_llt_one_step_matches_oracle(be, monkeypatch):
-    from mast3r_slam_amd import synthetic
-
-    monkeypatch.setenv("M3S_SOLVER", "pdense")
-    g = synthetic.make_graph(100, 24, 32, seed=301)
-    _, dx_gpu, info = run_gpu(be, "rays", g, 1, 0.0)
-    _, dx_ref, it, failed = run_oracle("rays", g, 1, 0.0)
-    assert info[be.INFO_SOLVE_FAIL] == failed == 0
-    np.testing.assert_allclose(dx_gpu, dx_ref, atol=1e-6 + 1e-4 * np.abs(dx_ref).max())
-
-
-def test_persistent_dense_llt_singular_zero_dx(be, monkeypatch):
-    from mast3r_slam_amd import synthetic
-
-    monkeypatch.setenv("M3S_SOLVER", "pdense")
-    g = synthetic.make_graph(40, 12, 16, seed=77)
-    valid = torch.zeros_like(g.valid_match)
-    T_gpu, dx, info = run_gpu(be, "rays", g, 4, 0.0, valid=valid)
-    assert info[be.INFO_SOLVE_FAIL] == 4 and info[be.INFO_ITERS] == 4
-    assert np.all(dx == 0)
-    np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())

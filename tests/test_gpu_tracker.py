@@ -30,7 +30,8 @@ def pose_tol(taus):
     return 1e-5 + 1e-4 * float(np.linalg.norm(np.asarray(taus, np.float64), axis=-1).sum())
 
 
-def run_gpu(be, d, max_iters=None, sync_every=5):
+def run_gpu(be, d, max_iters=None, sync_every=5, cfg=None):
+    CFG = tro.TRACKING_CFG if cfg is None else cfg
     t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k])).to(DEV)  # noqa: E731
     mi = int(d["max_iters"]) if max_iters is None else max_iters
     if int(d["calib"]):
@@ -69,30 +70,38 @@ def test_tracker_cholesky_failure_reported(be, golden_dir):
     assert info[1] == 1  # the reference raises -> track() reports failure
 
 
-@pytest.mark.parametrize("calib", [False, True])
-def test_tracker_c1_shape_matches_oracle(be, calib):
-    """C1 shape (512x384), natural termination, vs the numpy restatement."""
+@pytest.mark.parametrize("calib,H,W,fixed", [(False, 384, 512, False), (True, 384, 512, False),
+                                              (False, 512, 512, False), (True, 512, 512, False),
+                                              (False, 512, 512, True)])
+def test_tracker_c1_c2_shapes_match_oracle(be, calib, H, W, fixed):
+    """C1 (512x384) and C2 (512x512) shapes vs the numpy restatement: natural
+    termination, and (fixed) the bench's 10 iterations with early exit off."""
     from mast3r_slam_amd import synthetic
 
-    p = synthetic.make_pair(384, 512, seed=1001)
+    p = synthetic.make_pair(H, W, seed=1001 if H == 384 else 1002)
+    CFG = dict(tro.TRACKING_CFG)
+    if fixed:
+        CFG.update(max_iters=10, rel_error=0.0, delta_norm=0.0)
     Xf, Xk = p.Xf.numpy(), p.Xk.numpy()
     rec = []
     if calib:
         K = p.K.numpy()
-        Xf = tro.constrain_points_to_ray((384, 512), Xf, K)
-        Xk = tro.constrain_points_to_ray((384, 512), Xk, K)
-        meas, vm = tro.calib_meas(Xk, (384, 512), CFG["depth_eps"])
+        Xf = tro.constrain_points_to_ray((H, W), Xf, K)
+        Xk = tro.constrain_points_to_ray((H, W), Xk, K)
+        meas, vm = tro.calib_meas(Xk, (H, W), CFG["depth_eps"])
         T_f, T_r, it = tro.track_calib(Xf, Xk, p.T_WCf_init.data.numpy(), p.T_WCk.data.numpy(),
-                                       p.Qk.numpy(), p.valid.numpy(), meas, vm, K, (384, 512),
+                                       p.Qk.numpy(), p.valid.numpy(), meas, vm, K, (H, W),
                                        dict(CFG), rec)
     else:
         T_f, T_r, it = tro.track_rays(Xf, Xk, p.T_WCf_init.data.numpy(), p.T_WCk.data.numpy(),
                                       p.Qk.numpy(), p.valid.numpy(), dict(CFG), rec)
     d = dict(calib=int(calib), Xf=Xf, Xk=Xk, T_WCf_init=p.T_WCf_init.data.numpy(),
              T_WCk=p.T_WCk.data.numpy(), Qk=p.Qk.numpy(), valid=p.valid.numpy(), K=p.K.numpy(),
-             H=384, W=512, max_iters=CFG["max_iters"])
-    T_WCf, T_CkCf, info = run_gpu(be, d)
-    assert info[0] == it
+             H=H, W=W, max_iters=CFG["max_iters"])
+    T_WCf, T_CkCf, info = run_gpu(be, d, cfg=CFG)
+    assert info[0] == it and info[1] == 0
+    if fixed:
+        assert it == 10
     tol = pose_tol([r["tau"][0] for r in rec])
     np.testing.assert_allclose(T_WCf[0], T_f[0], atol=tol)
 

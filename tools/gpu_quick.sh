@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box: parity tests, sparse-LLT phase timing, bench (no CPU leg). Any failure ends the script.
+# GPU-box: parity tests, bench (no CPU leg). Any failure ends the script.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
@@ -7,9 +7,5 @@ mkdir -p $OUT
 cd $R
 echo "torch import"; timeout -k 10 300 python -c "import torch; print(torch.cuda.is_available())" && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
-if [ -f variants/lib_T.so ]; then
-  M3S_LIB=$R/variants/lib_T.so NS=${NS:-32,64,128,256} timeout -k 10 300 python tools/llt_timing.py > $OUT/llt_t.txt 2>&1 || { echo "llt timing failed"; tail -20 $OUT/llt_t.txt; exit 1; }
-  cat $OUT/llt_t.txt
-fi
 timeout -k 10 600 python bench.py --no-cpu > $OUT/bench_q.json 2> $OUT/bench_q.err || { echo "bench failed"; tail -30 $OUT/bench_q.err; exit 1; }
 cat $OUT/bench_q.json

@@ -158,15 +158,15 @@ const char *m3s_version(void);
  * edge ranks (ri, rj) (pose rank 0 fixed); split > 0 cuts update lists longer
  * than split into PART items (at most max_parts, widening split to fit), as
  * the solver does for factors that live in global memory. Writes the
- * flattened int32 plan to out (if cap suffices) and meta[0..32] = {m, S,
- * levels, 29 section offsets in the order of m3s_symbolic.h, n_parts}.
+ * flattened int32 plan to out (if cap suffices) and meta[0..34] = {m, S,
+ * levels, 31 section offsets in the order of m3s_symbolic.h, n_parts}.
  * Returns the plan length in int32 words. */
 int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t split,
                               int32_t max_parts, int32_t *out, int64_t cap, int32_t *meta);
 
 /* Diagnostic: byte offsets of the workspace sections for (N, HW, E), in the
  * order flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk,
- * Dinv, tasks, planes, total (offs[14]). Returns the total. */
+ * Dinv, tail, tasks, planes, total (offs[15]). Returns the total. */
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs);
 
 #ifdef __cplusplus

@@ -80,9 +80,18 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
   return (ch + kBlockPix - 1) / kBlockPix * kBlockPix;
 }
 
+// tail_llt_kernel (dense top of the elimination tree on the f64 MFMA): tile
+// rows (n + 1 <= 16 kTailMaxT) and its scratch (dense bordered tail, L tiles,
+// W_k); see the kernel
+constexpr int kTailMaxT = 32;
+inline size_t tail_scratch_doubles() {
+  const size_t nmax = 16 * kTailMaxT;
+  return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 + (size_t)kTailMaxT * 256;
+}
+
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      tasks, planes, total;
+      colsync, tail, tasks, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -130,6 +139,10 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 7 * (size_t)(m + 1), 256);
   L.parts = off;  // split update partials, at most slot_cap of them
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
+  L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets (epoch-tagged, zeroed per call)
+  off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16), 256);
+  L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
+  off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
   // target-side planes of every edge (5 planes = rays, the widest mode)
@@ -1024,6 +1037,9 @@ struct SparseDev {
   int32_t *info;
   int32_t *flags;
   float delta_thresh;
+  int tail_done;  // phase 2: the dense tail was solved by tail_llt_kernel (x_tail in rhs)
+  double *tail_A;  // border_kernel: also write the bordered tail blocks densely here (or null)
+  int tail_ld;
   int phase;  // global factors with a dense tail: 0 whole solve, 1 up to the
               // tail border, 2 from the tail factor (border_kernel between)
 };
@@ -1143,8 +1159,31 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #define M3S_TAIL_LOOKAHEAD 1
 #endif
 
+// Cross-workgroup hand-off of doubles (column-task kernels): write-through
+// (sc1) stores drained before the flag, sc1 loads (L2 / fabric served, never a
+// stale L1 line) after the flag (MI355X_MICROARCH.md, inter-workgroup
+// visibility, R1 / R2 forms).
+__device__ __forceinline__ double ld_sc1(const double *p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool SC1>
+__device__ __forceinline__ double ld_blk(const double *p) {
+  if (SC1) return ld_sc1(p);
+  return *p;
+}
+template <bool SC1>
+__device__ __forceinline__ void st_blk(double *p, double v) {
+  if (SC1) st_sc1(p, v);
+  else *p = v;
+}
+
 // v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
-template <bool STAGE, bool SAME>
+template <bool STAGE, bool SAME, bool SC1 = false>
 __device__ __forceinline__ double sub_products(double v, const double *Lb, const int32_t *sa,
                                                const int32_t *sb, int q0, int q1, int r7, int c7,
                                                int lane49, int lane, double *stg) {
@@ -1178,8 +1217,8 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
 #pragma unroll
     for (int bq = 0; bq < kStage; bq++) {
       if (bq < nb) {
-        va[bq] = Lb[(size_t)sa[q + bq] * 49 + lane49];
-        if (!SAME) vb[bq] = Lb[(size_t)sb[q + bq] * 49 + lane49];
+        va[bq] = ld_blk<SC1>(Lb + (size_t)sa[q + bq] * 49 + lane49);
+        if (!SAME) vb[bq] = ld_blk<SC1>(Lb + (size_t)sb[q + bq] * 49 + lane49);
       }
     }
     if (lane < 49) {
@@ -1204,7 +1243,7 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
 
 // Rows (lanes 0..6): acc -= sum_q op(A_q) y_{p_q}, op(A) = A (TRANS false:
 // row l7 of A) or A^T (TRANS: column `lane` of A). y lives in LDS.
-template <bool STAGE, bool TRANS>
+template <bool STAGE, bool TRANS, bool SC1 = false>
 __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const int32_t *slot,
                                              const int32_t *vidx, int q0, int q1, const double *y,
                                              int lane7, int lane49, int lane, double *stg) {
@@ -1221,19 +1260,27 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
   }
   for (int q = q0; q < q1; q += kStage) {
     const int nb = (q1 - q < kStage) ? q1 - q : kStage;
-    double va[kStage];
+    double va[kStage], vy[kStage];
 #pragma unroll
     for (int bq = 0; bq < kStage; bq++)
-      if (bq < nb) va[bq] = Lb[(size_t)slot[q + bq] * 49 + lane49];
+      if (bq < nb) {
+        va[bq] = ld_blk<SC1>(Lb + (size_t)slot[q + bq] * 49 + lane49);
+        if (SC1) vy[bq] = ld_sc1(y + (size_t)vidx[q + bq] * 7 + lane7);  // y of other workgroups
+      }
     if (lane < 49) {
 #pragma unroll
       for (int bq = 0; bq < kStage; bq++)
         if (bq < nb) stg[bq * 49 + lane] = va[bq];
     }
+    if (SC1 && lane < 7) {
+#pragma unroll
+      for (int bq = 0; bq < kStage; bq++)
+        if (bq < nb) stg[kStage * 49 + bq * 7 + lane] = vy[bq];
+    }
     wave_lds_fence();
     for (int bq = 0; bq < nb; bq++) {
       const double *A = stg + bq * 49;
-      const double *yv = y + (size_t)vidx[q + bq] * 7;
+      const double *yv = SC1 ? stg + kStage * 49 + bq * 7 : y + (size_t)vidx[q + bq] * 7;
       double t0 = 0.0;
 #pragma unroll
       for (int mm = 0; mm < 7; mm++) t0 += (TRANS ? A[mm * 7 + lane7] : A[lane7 * 7 + mm]) * yv[mm];
@@ -1250,8 +1297,9 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
 // updates -> L_kk (row-major, upper part 0) into Lb[k], W_k = L_kk^-1
 // (row-major) into Di[k]; Lr (strictly lower L_kk) and dinv = 1 / diag, wave-
 // uniform, for the forward step. Returns true on a non-positive pivot.
+template <bool SC1 = false>
 __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double *Di, double *scr, int lane,
-                                            int l7, double (&Lr)[7][7], double (&dinv)[7]) {
+                                            int l7, double (&Lr)[7][7], double (&dinv)[7], double *Wl = nullptr) {
   // entry layout -> row layout through the wave's scratch
   if (lane < 49) scr[lane] = v;
   wave_lds_fence();
@@ -1291,14 +1339,16 @@ __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double 
   if (lane < 7) {
 #pragma unroll
     for (int qq = 0; qq < 7; qq++) {
-      Lb[(size_t)k * 49 + lane * 7 + qq] = (qq <= lane) ? a[qq] : 0.0;  // row `lane` of L_kk
-      Di[(size_t)k * 49 + qq * 7 + lane] = w[qq];                       // column `lane` of W
+      st_blk<SC1>(Lb + (size_t)k * 49 + lane * 7 + qq, (qq <= lane) ? a[qq] : 0.0);  // row `lane` of L_kk
+      st_blk<SC1>(Di + (size_t)k * 49 + qq * 7 + lane, w[qq]);                       // column `lane` of W
+      if (Wl) Wl[qq * 7 + lane] = w[qq];
     }
   }
   return bad;
 }
 
 // y_k = L_kk^-1 b (lane r < 7 holds b_r), stored to yk_out[0..7)
+template <bool SC1 = false>
 __device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7][7], const double (&dinv)[7],
                                                 double *yk_out, int lane) {
   double yk[7];
@@ -1313,7 +1363,7 @@ __device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7]
     double yo = 0.0;
 #pragma unroll
     for (int qq = 0; qq < 7; qq++) yo = (qq == lane) ? yk[qq] : yo;
-    yk_out[lane] = yo;
+    st_blk<SC1>(yk_out + lane, yo);
   }
 }
 
@@ -1324,7 +1374,7 @@ __device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7]
 template <bool STAGE>
 __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t *pl, const int *off, double *Lb,
                                             double *y, int r7, int c7, int lane49, int lane, int lane7, bool act49,
-                                            double *stg) {
+                                            double *stg, double *Ad = nullptr, int ld = 0) {
   const int32_t *dtr_ptr = pl + off[6], *dtr_slot = pl + off[7], *dtr_p = pl + off[8], *task_dst = pl + off[10],
                 *task_tr_ptr = pl + off[12], *tr_a = pl + off[13], *tr_b = pl + off[14];
   const int32_t *clq = pl + off[28];
@@ -1340,12 +1390,17 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
     bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
     if (act49) Lb[(size_t)k * 49 + lane] = v;
     if (lane < 7) y[k * 7 + lane] = bb;
+    if (Ad && act49) Ad[(size_t)(7 * ci + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
   } else {
     const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
     const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
     double v = Lb[(size_t)dst * 49 + lane49];
     v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
     if (act49) Lb[(size_t)dst * 49 + lane] = v;
+    if (Ad && act49) {  // the block and its transpose (tail_llt_kernel reads whole 16x16 tiles)
+      Ad[(size_t)(7 * ri + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
+      Ad[(size_t)(7 * ci + c7 / 7) * ld + 7 * ri + r7 / 7] = v;
+    }
   }
 }
 
@@ -1528,7 +1583,10 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // c0 whose structure is every later column) factored right-looking,
   // bulk-synchronously, after the dataflow items (which cover columns < c0,
   // including the border blocks L_ik, i >= c0 > k, and all y_p, p < c0).
-  if (D.nc > 0) {
+  if (D.nc > 0 && D.tail_done) {  // tail_llt_kernel solved the dense tail: y holds x there
+    for (int q = tid; q < D.nc; q += 1024) done2[m - D.nc + q] = 1;
+    __syncthreads();
+  } else if (D.nc > 0) {
     const int32_t *clq = pl + D.off[28];
     const int nc = clq[0], c0 = clq[1];
     const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
@@ -1742,6 +1800,493 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       D.flags[kFlagStop] = 1;
     }
   }
+}
+
+// ------------------------------------- column tasks over many workgroups --
+// Large graphs (factor in global memory): the sparse columns of the
+// elimination tree below the dense tail are factored as column tasks spread
+// over the chip instead of as dataflow items on one workgroup's 16 waves. A
+// task is column k: DIAG (D_k - sum_p L_kp L_kp^T -> L_kk, W_k = L_kk^-1, the
+// forward step y_k) on wave 0, then its OFF blocks L_ik = (A_ik - sum_p L_ip
+// L_kp^T) W_k^T on all 4 waves. Column k reads exactly the columns p with
+// L_kp != 0 (its dtr list), all earlier in the level-order dispatch list, so
+// a workgroup waits only for tasks running workgroups drew before it
+// (progress does not depend on co-residency). Hand-off: sc1 stores drained
+// before the column's flag, sc1 loads after polling it. Flags and tickets
+// carry an epoch (solve launch count since m3s_gn_prepare zeroed them):
+// nothing is reset between launches. col_backsub_kernel runs the tasks in
+// reverse (x_k = W_k^T (y_k - sum_i L_ik^T x_i)) and the workgroup that
+// finishes the last column writes dx, retracts and tests ||dx||.
+// (Eigen SimplicialLLT factor + solve, gn_kernels.cu:132-153, with the
+// reference's dx = 0 on failure and pose_retr_kernel :415-453.)
+struct ColArgs {
+  const int32_t *plan;
+  int off[kPlanSections];
+  int m, c0, ncols, epoch;  // ncols = c0 sparse columns (corder)
+  double *L, *Dinv, *y;     // factor slots, W_k, RHS [m][7] (x after the back-substitution)
+  int32_t *done, *done2;    // [m] epoch flags: column factored / x_k final
+  int32_t *ctr;             // [0] factor ticket, [1] back-substitution ticket, [2] columns finished
+  int32_t *flags;
+  int32_t *info;
+  float *Twc, *dx_out;
+  int64_t N;
+  float delta_thresh;
+};
+constexpr int kColSpins = 1 << 20;  // bounded waits: a plan bug becomes a solve failure, never a hang
+__device__ __forceinline__ void set_fail(int32_t *flags) {
+  __hip_atomic_store(flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// whole-wave global ticket: every lane adds 1 (folded into one add of 64)
+__device__ __forceinline__ int wave_gticket(int32_t *ctr) {
+  const int o = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane(o) >> 6;
+}
+
+// wave-uniform wait until flag[idx[q]] == want for every q in [q0, q1) with
+// idx[q] < lim (lanes poll 64 at a time, sc1 loads); false on timeout
+__device__ __forceinline__ bool wait_flags(const int32_t *flag, const int32_t *idx, int q0, int q1, int lim, int want,
+                                           int lane) {
+  int spins = 0;
+  for (int qb = q0; qb < q1; qb += 64) {
+    const int q = qb + lane;
+    const int i = q < q1 ? idx[q] : -1;
+    for (;;) {
+      const bool ok = i < 0 || i >= lim ||
+                      __hip_atomic_load(flag + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want;
+      if (__ballot(!ok) == 0) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kColSpins) return false;
+    }
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
+  if (C.flags[kFlagStop]) return;
+  __shared__ int tk_s;
+  __shared__ double Wsh[49];
+  __shared__ double scratch[4][64];
+  __shared__ __attribute__((aligned(16))) double stage[4][kStageDoubles];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int32_t *pl = C.plan;
+  const int32_t *col_ptr = pl + C.off[1], *dtr_ptr = pl + C.off[6], *dtr_slot = pl + C.off[7],
+                *dtr_p = pl + C.off[8], *task_dst = pl + C.off[10], *task_tr_ptr = pl + C.off[12],
+                *tr_a = pl + C.off[13], *tr_b = pl + C.off[14], *corder = pl + C.off[29], *ctask0 = pl + C.off[30];
+  const int r = lane / 7, c = lane % 7;
+  const bool act49 = lane < 49;
+  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
+  const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
+  double *stg = stage[wave], *scr = scratch[wave];
+  const int base = C.epoch * (C.ncols + (int)gridDim.x);  // tickets drawn by earlier launches
+  double *L = C.L;
+  for (;;) {
+    if (wave == 0) {
+      const int t = wave_gticket(C.ctr + 0) - base;
+      if (lane == 0) tk_s = t;
+    }
+    __syncthreads();
+    const int t = tk_s;
+    __syncthreads();
+    if (t >= C.ncols) break;
+    const int k = corder[t];
+    const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
+    if (wave == 0) {
+      if (!wait_flags(C.done, dtr_p, q0, q1, C.m, C.epoch + 1, lane) && lane == 0) set_fail(C.flags);
+      // DIAG(k): the assembled D_k (previous launch: plain load) minus the
+      // updates from the columns p (this launch: sc1)
+      double v = L[(size_t)k * 49 + lane49];
+      v = sub_products<true, true, true>(v, L, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+      double Lr[7][7], dinv[7];
+      if (diag_factor<true>(v, k, L, C.Dinv, scr, lane, l7, Lr, dinv, Wsh) && lane == 0) set_fail(C.flags);
+      double bb = C.y[(size_t)k * 7 + lane7];
+      bb = sub_matvec<true, false, true>(bb, L, dtr_slot, dtr_p, q0, q1, C.y, lane7, lane49, lane, stg);
+      fwd_solve_store<true>(bb, Lr, dinv, C.y + (size_t)k * 7, lane);
+    }
+    __syncthreads();  // W_k in LDS; the dependencies are final for every wave
+    // OFF(i, k) for the |struct(k)| tasks of column k, one per wave
+    const int tc0 = ctask0[k], ntask = col_ptr[k + 1] - col_ptr[k];
+    for (int tt = wave; tt < ntask; tt += 4) {
+      const int t2 = tc0 + tt, dst = task_dst[t2];
+      double v = L[(size_t)dst * 49 + lane49];
+      v = sub_products<true, false, true>(v, L, tr_a, tr_b, task_tr_ptr[t2], task_tr_ptr[t2 + 1], r7, c7, lane49,
+                                          lane, stg);
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      double x = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * Wsh[c7 + mm];
+      if (act49) st_sc1(L + (size_t)dst * 49 + lane, x);
+      wave_lds_fence();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every sc1 store of column k has left
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(C.done + k, C.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// dx = -x (original order), retraction, ||dx|| test (one wave; x in y, sc1)
+__device__ void col_finish(const ColArgs &C, int lane) {
+  __shared__ float dxs[7 * 512];
+  const int32_t *perm = C.plan + C.off[0];
+  const int m = C.m;
+  const bool failed =
+      __hip_atomic_load(C.flags + kFlagSplitFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (failed) {
+    for (int k = lane; k < 7 * m; k += 64) C.dx_out[k] = 0.0f;
+    if (lane == 0) {
+      C.flags[kFlagSplitFail] = 0;
+      C.info[M3S_INFO_ITERS] += 1;
+      C.info[M3S_INFO_SOLVE_FAIL] += 1;
+      if (0.0f < C.delta_thresh) {
+        C.info[M3S_INFO_CONVERGED] = 1;
+        C.flags[kFlagStop] = 1;
+      }
+    }
+    return;
+  }
+  float part = 0.0f;
+  for (int idx = lane; idx < 7 * m; idx += 64) {
+    const int vn = idx / 7, q = idx - 7 * vn;
+    const int vo = perm[vn];
+    const float v = -(float)ld_sc1(C.y + idx);
+    C.dx_out[vo * 7 + q] = v;
+    dxs[vo * 7 + q] = v;
+    part += v * v;
+  }
+  part = wave_sum(part);
+  wave_lds_fence();
+  for (int p = lane; p < m; p += 64) {
+    const Sim3f T = load_sim3(C.Twc + 8 * (size_t)(p + 1));
+    float xi[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
+    store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, T));
+  }
+  if (lane == 0) {
+    C.info[M3S_INFO_ITERS] += 1;
+    if (sqrtf(part) < C.delta_thresh) {
+      C.info[M3S_INFO_CONVERGED] = 1;
+      C.flags[kFlagStop] = 1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
+  if (C.flags[kFlagStop]) return;
+  __shared__ __attribute__((aligned(16))) double stage[kStageDoubles];
+  const int lane = threadIdx.x;
+  const int32_t *pl = C.plan;
+  const int32_t *col_ptr = pl + C.off[1], *col_row = pl + C.off[2], *col_slot = pl + C.off[3],
+                *corder = pl + C.off[29];
+  const int lane7 = lane < 7 ? lane : 0;
+  const int lane49 = lane < 49 ? lane : 0;
+  const int base = C.epoch * (C.ncols + (int)gridDim.x);
+  if (C.ncols == 0) {  // no sparse columns: the tail kernel solved everything
+    if (blockIdx.x == 0) col_finish(C, lane);
+    return;
+  }
+  for (;;) {
+    const int t = wave_gticket(C.ctr + 1) - base;
+    if (t >= C.ncols) break;
+    const int k = corder[C.ncols - 1 - t];
+    const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
+    if (!wait_flags(C.done2, col_row, q0, q1, C.c0, C.epoch + 1, lane) && lane == 0) set_fail(C.flags);
+    double rr = C.y[(size_t)k * 7 + lane7];
+    rr = sub_matvec<true, true, true>(rr, C.L, col_slot, col_row, q0, q1, C.y, lane7, lane49, lane, stage);
+    double xk = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) xk += C.Dinv[(size_t)k * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
+    if (lane < 7) st_sc1(C.y + (size_t)k * 7 + lane, xk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(C.done2 + k, C.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the workgroup that finishes the last column finishes the step
+    const int fin = wave_gticket(C.ctr + 2);
+    if (fin - C.epoch * C.ncols == C.ncols - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      col_finish(C, lane);
+    }
+  }
+}
+
+// ------------------------------------------- dense tail on the f64 MFMA --
+// The top clique of the elimination tree (nc block columns, n = 7 nc scalar
+// columns; SparsePlan::nc) after its border updates is a dense SPD system:
+// a chain of n dependent pivots. sparse_llt_kernel factored it with 7x7 block
+// products on one CU's dependent global-memory round trips (B1/B2, ~440 us at
+// 256 KFs). Here one workgroup of 4 waves (one per SIMD) factors it
+// left-looking over 16x16 fp64 tiles on v_mfma_f64_16x16x4f64, per tile
+// column k:
+//   update  A(I,k) -= sum_{j<k} L(I,j) L(k,j)^T for I >= k, accumulated in
+//           registers (wave w owns the rows I = k + w (mod 4)); the finished
+//           L tiles stream from L2 (written once, read by later columns);
+//   diag    wave 0: A(k,k) -> L_kk (register Cholesky, readlane broadcasts),
+//           W_k = L_kk^-1 into LDS (and global, for the back-substitution);
+//   panel   L(I,k)^T = W_k A(I,k)^T on the MFMA, stored to L2.
+// The RHS y is row n of the augmented matrix, so row n of the factor is
+// y' = L^-1 y; then L^T x = y' by tile columns from the bottom. Every sum
+// runs in a fixed order: bitwise reproducible (the sharded ranks rely on it).
+// Replaces the dense-tail part of SimplicialLLT (gn_kernels.cu:132-153).
+//
+// Layouts. An accumulator tile holds A(I,k)^T in the MFMA C layout: lane l,
+// register r = A(I,k)[l & 15][(l >> 4) + 4 r], which is also the operand
+// order q = r of a product X . A(I,k)^T. Finished tiles are stored in that
+// order, [tile][lane][4] (32 B per lane): every MFMA operand is one load.
+constexpr int kTailNW = 4;     // waves (one per SIMD)
+constexpr int kTailRows = (kTailMaxT + kTailNW - 1) / kTailNW;  // tile rows per wave and column
+
+struct TailArgs {
+  const double *Ad;  // bordered tail, dense symmetric [n][ld] (border_kernel writes it)
+  int ld;
+  double *rhs;       // y [m][7] in; x of the tail columns out (same place)
+  double *Lg;        // finished L tiles, [tile (I,J) = I (I + 1) / 2 + J][64][4]
+  double *Wg;        // [TC][16][16]: W_k of every tile column
+  int32_t *flags;
+  int nc, c0;        // tail columns, first tail column
+};
+
+// augmented tail matrix entry (i, j): padding columns are identity (and the
+// unused (n, n)), padding rows zero, row n the RHS y of the tail columns
+__device__ __forceinline__ double tail_entry(const TailArgs &A, int n, int i, int j) {
+  const bool pad = j >= n || i > n;
+  const double *src = (i == n) ? A.rhs + 7 * A.c0 + j : A.Ad + (size_t)i * A.ld + j;
+  const double v = pad ? 0.0 : *src;
+  return (j >= n && i == j) ? 1.0 : v;
+}
+
+// Diagonal tile from Dg (one wave): L_kk (Cholesky by rows, lane r < 16 holds
+// row r, pivots broadcast by readlane), W_k = L_kk^-1 -> Wk, and for the tile
+// that holds the RHS row, y' of its columns -> yv_k. Columns >= jv (padding,
+// the RHS row's own column) are identity. Returns true on a non-positive
+// pivot (computed on with pivot 1; the step becomes dx = 0).
+#ifdef M3S_TAIL_STAMPS
+__device__ int64_t *g_tail_stamp;
+#define M3S_DSTAMP(i) if (lane == 0 && g_tail_stamp) g_tail_stamp[i] = wall_clock64();
+#else
+#define M3S_DSTAMP(i)
+#endif
+__device__ __forceinline__ bool tail_diag(const double (*Dg)[17], double (*Wk)[17], double *yv_k, int jv, int rhs_row,
+                                          int lane) {
+  const int lr = lane & 15;
+  M3S_DSTAMP(110)
+  double a[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) a[c] = Dg[lr][c];
+  double dinv[16];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    if (j < jv) {
+      double d = readlane_d(a[j], j);
+      bad |= !(d > 0.0);
+      d = d > 0.0 ? d : 1.0;
+      const double inv = rsqrt_nr(d);
+      dinv[j] = inv;
+      a[j] = (lane > j) ? a[j] * inv : ((lane == j) ? d * inv : 0.0);
+#pragma unroll
+      for (int c = j + 1; c < 16; c++) {
+        const double lcj = readlane_d(a[j], c);
+        if (lane >= c) a[c] -= a[j] * lcj;
+      }
+    } else {
+      dinv[j] = 1.0;
+      a[j] = (lane == j) ? 1.0 : 0.0;
+    }
+  }
+  M3S_DSTAMP(111)
+  if (lane == rhs_row) {
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (j < jv) yv_k[j] = a[j];
+  }
+  // W = L^-1: lane c computes column c
+  double w[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    double s2 = (r == lane) ? 1.0 : 0.0;
+    if (r < jv) {
+#pragma unroll
+      for (int mm = 0; mm < r; mm++) s2 -= readlane_d(a[mm], r) * w[mm];
+      s2 *= dinv[r];
+    }
+    w[r] = s2;
+  }
+  M3S_DSTAMP(112)
+  if (lane < 16) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) Wk[r][lane] = w[r];
+  }
+  M3S_DSTAMP(113)
+  return bad;
+}
+
+__device__ __forceinline__ int tail_tile(int I, int J) { return I * (I + 1) / 2 + J; }
+
+// one finished tile's operand registers (32 B per lane, L2)
+__device__ __forceinline__ f64x4 tail_load(const double *Lg, int t, int lane) {
+  const f64x4 *p = reinterpret_cast<const f64x4 *>(Lg + (size_t)t * 256) + lane;
+  return __builtin_nontemporal_load(p);
+}
+
+__global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
+  if (A.flags[kFlagStop]) return;
+  __shared__ double Wk[16][17];  // W_k of the current step
+  __shared__ double Dg[16][17];  // diagonal tile staging
+  __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
+  __shared__ int fail_s;
+  const int n = 7 * A.nc;
+  const int TC = (n + 15) / 16, TR = (n + 16) / 16;  // tile columns; tile rows incl. the RHS row n
+  const int In = n / 16, rn = n - 16 * In;             // RHS row: tile row, local row
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  double *Lg = A.Lg, *Wg = A.Wg;
+  if (tid == 0) fail_s = 0;
+  for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) yv[q] = 0.0, xv[q] = 0.0;
+  __syncthreads();
+#ifdef M3S_TAIL_STAMPS
+  int64_t *stamp = reinterpret_cast<int64_t *>(Wg + (size_t)kTailMaxT * 256);
+  if (tid == 0) g_tail_stamp = stamp;
+#define M3S_STAMP(i) if (tid == 0) stamp[i] = wall_clock64();
+#else
+#define M3S_STAMP(i)
+#endif
+  M3S_STAMP(0)
+  for (int k = 0; k < TC; k++) {
+    // column k: wave w holds the rows I = k + w + 4u (u < kTailRows)
+    f64x4 acc[kTailRows];
+#pragma unroll
+    for (int u = 0; u < kTailRows; u++) {
+      const int I = k + wave + kTailNW * u;
+      f64x4 v = {0.0, 0.0, 0.0, 0.0};
+      if (I < TR) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) v[r] = tail_entry(A, n, 16 * I + lr, 16 * k + lk + 4 * r);
+      }
+      acc[u] = v;
+    }
+    // A(I,k)^T -= L(k,j) L(I,j)^T, j ascending; the operands of j + 2 are
+    // in flight while j's products run (3-deep register ring)
+    f64x4 rk[3], ri[3][kTailRows];
+#define M3S_TAIL_ISSUE(j_, b_)                                                           \
+  do {                                                                                   \
+    rk[b_] = tail_load(Lg, tail_tile(k, (j_)), lane);                                    \
+    for (int u = 0; u < kTailRows; u++) {                                                \
+      const int I = k + wave + kTailNW * u;                                              \
+      if (I < TR) ri[b_][u] = tail_load(Lg, tail_tile(I, (j_)), lane);                   \
+    }                                                                                    \
+  } while (0)
+#define M3S_TAIL_UPD(b_)                                                                 \
+  do {                                                                                   \
+    for (int u = 0; u < kTailRows; u++) {                                                \
+      const int I = k + wave + kTailNW * u;                                              \
+      if (I < TR) {                                                                      \
+        for (int q = 0; q < 4; q++)                                                      \
+          acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-rk[b_][q], ri[b_][u][q], acc[u], 0, 0, 0); \
+      }                                                                                  \
+    }                                                                                    \
+  } while (0)
+    if (k > 0) M3S_TAIL_ISSUE(0, 0);
+    if (k > 1) M3S_TAIL_ISSUE(1, 1);
+    for (int j = 0; j < k; j += 3) {
+      if (j + 2 < k) M3S_TAIL_ISSUE(j + 2, 2);
+      M3S_TAIL_UPD(0);
+      if (j + 1 >= k) break;
+      if (j + 3 < k) M3S_TAIL_ISSUE(j + 3, 0);
+      M3S_TAIL_UPD(1);
+      if (j + 2 >= k) break;
+      if (j + 4 < k) M3S_TAIL_ISSUE(j + 4, 1);
+      M3S_TAIL_UPD(2);
+    }
+#undef M3S_TAIL_ISSUE
+#undef M3S_TAIL_UPD
+    M3S_STAMP(1 + 3 * k)
+    if (wave == 0) {  // diag: tile (k, k) is wave 0's u = 0
+#pragma unroll
+      for (int r = 0; r < 4; r++) Dg[lr][lk + 4 * r] = acc[0][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (tail_diag(Dg, Wk, yv + 16 * k, min(16, n - 16 * k), In == k ? rn : -1, lane) && lane == 0) fail_s = 1;
+      if (lane < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) Wg[(size_t)k * 256 + r * 16 + lane] = Wk[r][lane];
+      }
+    }
+    M3S_STAMP(2 + 3 * k)
+    __syncthreads();  // W_k
+    // panel: L(I,k)^T = W_k A(I,k)^T for I > k, stored in operand order
+#pragma unroll
+    for (int u = 0; u < kTailRows; u++) {
+      const int I = k + wave + kTailNW * u;
+      if (I < TR && I > k) {
+        f64x4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; q++) d = __builtin_amdgcn_mfma_f64_16x16x4f64(Wk[lr][4 * q + lk], acc[u][q], d, 0, 0, 0);
+        reinterpret_cast<f64x4 *>(Lg + (size_t)tail_tile(I, k) * 256)[lane] = d;
+        if (I == In && lr == rn) {  // y' of this column from the RHS row
+#pragma unroll
+          for (int r = 0; r < 4; r++) yv[16 * k + lk + 4 * r] = d[r];
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L(., k) in L2 before any wave loads it
+    __syncthreads();
+    M3S_STAMP(3 + 3 * k)
+  }
+  // back-substitution L^T x = y', tile columns from the bottom; yv
+  // accumulates the updates of each column in decreasing K (fixed order).
+  // Thread (J, c) (two per thread: 16 (K - 1) <= 496 pairs) sums column c of
+  // tile (K, J), L(K,J)[r][c] at lane 16 (c % 4) + r, register c / 4; the next
+  // row's tiles and W are loaded while this row runs.
+  constexpr int kBP = (16 * kTailMaxT + 64 * kTailNW - 1) / (64 * kTailNW);  // pairs per thread
+  double lb[kBP][16], wb[16];
+  auto bs_load = [&](int K) {
+#pragma unroll
+    for (int pp = 0; pp < kBP; pp++) {
+      const int q = tid + 64 * kTailNW * pp, J = q >> 4, c = q & 15;
+      if (J < K) {
+        const double *T = Lg + (size_t)tail_tile(K, J) * 256 + (c >> 2);
+#pragma unroll
+        for (int r = 0; r < 16; r++) lb[pp][r] = __builtin_nontemporal_load(T + 4 * (16 * (c & 3) + r));
+      }
+    }
+    if (wave == 0 && lane < 16) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) wb[i] = Wg[(size_t)K * 256 + i * 16 + lane];
+    }
+  };
+  if (TC > 0) bs_load(TC - 1);
+  for (int K = TC - 1; K >= 0; K--) {
+    const int jv = min(16, n - 16 * K);
+    if (wave == 0 && lane < 16) {
+      double x = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; i++) x += wb[i] * yv[16 * K + i];
+      xv[16 * K + lane] = lane < jv ? x : 0.0;
+    }
+    __syncthreads();
+    double u[kBP];
+#pragma unroll
+    for (int pp = 0; pp < kBP; pp++) {
+      u[pp] = 0.0;
+      const int q = tid + 64 * kTailNW * pp, J = q >> 4;
+      if (J < K) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) u[pp] += lb[pp][r] * xv[16 * K + r];
+      }
+    }
+    if (K > 0) bs_load(K - 1);
+#pragma unroll
+    for (int pp = 0; pp < kBP; pp++) {
+      const int q = tid + 64 * kTailNW * pp, J = q >> 4, c = q & 15;
+      if (J < K) yv[16 * J + c] -= u[pp];
+    }
+    __syncthreads();
+  }
+  M3S_STAMP(100)
+  for (int j = tid; j < n; j += 64 * kTailNW) A.rhs[7 * A.c0 + j] = xv[j];
+  if (tid == 0 && fail_s) A.flags[kFlagSplitFail] = 1;
+#undef M3S_STAMP
 }
 
 // ------------------------------------------------- small dense Cholesky --
@@ -1965,7 +2510,17 @@ __global__ void __launch_bounds__(64 * kBorderWaves) border_kernel(SparseDev D) 
   double *stg = smem + (size_t)wave * kStageDoubles;
   double *y = const_cast<double *>(D.rhs);
   for (int t = blockIdx.x * kBorderWaves + wave; t < nt0; t += gridDim.x * kBorderWaves)
-    border_task<true>(t, nc, c0, pl, D.off, D.L, y, r7, c7, lane49, lane, lane7, act49, stg);
+    border_task<true>(t, nc, c0, pl, D.off, D.L, y, r7, c7, lane49, lane, lane7, act49, stg, D.tail_A, D.tail_ld);
+}
+
+inline bool cols_path() {  // M3S_COLS=0: large graphs on sparse_llt_kernel's one workgroup (A/B)
+  const char *e = std::getenv("M3S_COLS");
+  return !(e && e[0] == '0');
+}
+
+inline bool tail_mfma() {  // M3S_TAIL_MFMA=0: the dense tail in sparse_llt_kernel (A/B)
+  const char *e = std::getenv("M3S_TAIL_MFMA");
+  return !(e && e[0] == '0');
 }
 
 inline bool border_split() {  // M3S_BORDER_SPLIT=0: tail border inside the one-workgroup kernel (A/B)
@@ -1979,6 +2534,7 @@ inline int dense_tail_min() {
 }
 
 struct PlanMeta {
+  int epoch = 0;  // solve launches since m3s_gn_prepare (column-task flags / tickets)
   bool sparse = false;
   int store = 0;  // sparse_llt_kernel<STORE>
   bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
@@ -2113,6 +2669,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     auto it = g_reg.find(ws);
     if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
     meta = it->second;
+    it->second.epoch++;
   }
   int rc;
   float *dx = a->dx_out;
@@ -2126,6 +2683,9 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     const PlanImage &I = meta.img;
     SparseDev D;
     D.phase = 0;
+    D.tail_done = 0;
+    D.tail_A = nullptr;
+    D.tail_ld = 0;
     D.plan = at<int32_t>(ws, Ly.plan);
     D.plan_len = meta.plan_len;
     const int64_t offs[kPlanSections] = {
@@ -2134,7 +2694,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         I.off_task_dst, I.off_task_col,     I.off_task_tr_ptr, I.off_tr_a,  I.off_tr_b,
         I.off_asm_ptr,  I.off_asm_edge,     I.off_g_ptr,    I.off_g_edge,   I.off_ctask_ptr,
         I.off_items,    I.off_wave_ptr,     I.off_witems,
-        I.off_part_q0,  I.off_part_q1,      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr, I.off_clq};
+        I.off_part_q0,  I.off_part_q1,      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr, I.off_clq,
+        I.off_corder,   I.off_ctask0};
     for (int q = 0; q < kPlanSections; q++) D.off[q] = (int)offs[q];
     D.n_items = meta.n_items;
     D.n_tasks = meta.n_tasks;
@@ -2163,16 +2724,82 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
     D.info = a->info;
     D.flags = flags;
     D.delta_thresh = a->delta_thresh;
-    if (meta.store == 1)
+    if (meta.store == 0 && cols_path() && meta.m <= 512 && (meta.nc == 0 || 7 * meta.nc + 1 <= 16 * kTailMaxT)) {
+      // column tasks over the chip -> tail border -> dense tail on the MFMA
+      // -> column back-substitution + step
+      ColArgs C;
+      C.plan = D.plan;
+      for (int q = 0; q < kPlanSections; q++) C.off[q] = D.off[q];
+      C.m = meta.m;
+      C.c0 = meta.m - meta.nc;
+      C.ncols = C.c0;
+      C.epoch = meta.epoch;
+      C.L = D.L;
+      C.Dinv = D.Dinv;
+      C.y = const_cast<double *>(D.rhs);
+      int32_t *cs = at<int32_t>(ws, Ly.colsync);
+      C.done = cs;
+      C.done2 = cs + (meta.m + 1);
+      C.ctr = cs + 2 * (meta.m + 1);
+      C.flags = flags;
+      C.info = a->info;
+      C.Twc = a->Twc;
+      C.dx_out = dx;
+      C.N = a->N;
+      C.delta_thresh = a->delta_thresh;
+      const int g1 = std::max(1, std::min(C.ncols, 256));
+      col_factor_kernel<<<g1, 256, 0, st>>>(C);
+      if (meta.nc > 0) {
+        double *tail = at<double>(ws, Ly.tail);
+        const int tld = 16 * kTailMaxT;
+        D.tail_A = tail;
+        D.tail_ld = tld;
+        const int nt0 = meta.nc * (meta.nc + 1) / 2;
+        border_kernel<<<(nt0 + kBorderWaves - 1) / kBorderWaves, 64 * kBorderWaves,
+                        kBorderWaves * kStageDoubles * sizeof(double), st>>>(D);
+        TailArgs T;
+        T.Ad = tail;
+        T.ld = tld;
+        T.rhs = C.y;
+        T.Lg = tail + (size_t)tld * tld;
+        T.Wg = T.Lg + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256;
+        T.flags = flags;
+        T.nc = meta.nc;
+        T.c0 = C.c0;
+        tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
+      }
+      const int g4 = std::max(1, std::min(C.ncols, 256));
+      col_backsub_kernel<<<g4, 64, 0, st>>>(C);
+    } else if (meta.store == 1)
       sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.store == 2)
       sparse_llt_kernel<2><<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.nc > 0 && border_split()) {
+      // the dense tail on the f64 MFMA when it fits (tail_llt_kernel), else
+      // in phase 2 of the one-workgroup kernel
+      const bool mfma_tail = 7 * meta.nc + 1 <= 16 * kTailMaxT && tail_mfma();
+      double *tail = at<double>(ws, Ly.tail);
+      const int tld = 16 * kTailMaxT;
+      D.tail_A = mfma_tail ? tail : nullptr;
+      D.tail_ld = tld;
       D.phase = 1;
       sparse_llt_kernel<0><<<1, 1024, meta.lds_bytes, st>>>(D);
       const int nt0 = meta.nc * (meta.nc + 1) / 2;
       border_kernel<<<(nt0 + kBorderWaves - 1) / kBorderWaves, 64 * kBorderWaves,
                       kBorderWaves * kStageDoubles * sizeof(double), st>>>(D);
+      if (mfma_tail) {
+        TailArgs T;
+        T.Ad = tail;
+        T.ld = tld;
+        T.rhs = const_cast<double *>(D.rhs);
+        T.Lg = tail + (size_t)tld * tld;
+        T.Wg = T.Lg + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256;
+        T.flags = flags;
+        T.nc = meta.nc;
+        T.c0 = meta.m - meta.nc;
+        tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
+        D.tail_done = 1;
+      }
       D.phase = 2;
       sparse_llt_kernel<0, true><<<1, 1024, meta.lds_bytes, st>>>(D);
     } else
@@ -2405,6 +3032,8 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   bool ok = true;
   ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.flags), M.h_flags, sizeof M.h_flags, hipMemcpyHostToDevice, st) == hipSuccess;
   ok &= hipMemsetAsync(at<uint32_t>(ws, Ly.edge_cnt), 0, edge_cnt_bytes(E), st) == hipSuccess;
+  ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
+  M.epoch = 0;
   ok &= hipMemcpyAsync(a->info, M.h_info, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
   if (E > 0) {
     ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_i), M.h_ri.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
@@ -2708,7 +3337,7 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
       I.off_task_dst, I.off_task_col, I.off_task_tr_ptr, I.off_tr_a,     I.off_tr_b,
       I.off_asm_ptr,  I.off_asm_edge, I.off_g_ptr,       I.off_g_edge,   I.off_ctask_ptr,
       I.off_items,    I.off_wave_ptr, I.off_witems,    I.off_part_q0,  I.off_part_q1,
-      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr, I.off_clq};
+      I.off_part_tgt, I.off_dpart_ptr, I.off_opart_ptr, I.off_clq, I.off_corder, I.off_ctask0};
   if (meta) {
     meta[0] = P.m, meta[1] = P.S, meta[2] = P.levels;
     for (int k = 0; k < kPlanSections; k++) meta[3 + k] = (int32_t)offs[k];
@@ -2721,9 +3350,9 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
 
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs) {
   const Layout L = gn_layout(N, HW, E);
-  const size_t o[14] = {L.flags, L.rank_i, L.rank_j, L.first, L.partials, L.edge_sums, L.A,
-                        L.fin,   L.plan,   L.Lblk,   L.Dinv,  L.tasks,    L.planes, L.total};
-  if (offs) std::copy(o, o + 14, offs);
+  const size_t o[15] = {L.flags, L.rank_i, L.rank_j, L.first, L.partials, L.edge_sums, L.A, L.fin,
+                        L.plan,  L.Lblk,   L.Dinv,   L.tail,  L.tasks,    L.planes,    L.total};
+  if (offs) std::copy(o, o + 15, offs);
   return L.total;
 }
 

@@ -377,6 +377,13 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     }
     P.task_lev_ptr.push_back((int32_t)P.task_dst.size());
   }
+  // column tasks: sparse columns in level order; first OFF task per column
+  P.ctask0.assign(m, 0);
+  for (int pos = 0; pos < m; pos++) {
+    const int k = P.lev_col[pos];
+    P.ctask0[k] = P.ctask_ptr[pos];
+    if (k < c0) P.corder.push_back(k);
+  }
   // the kernel addresses tail blocks arithmetically: off-diagonal slots of
   // the tail columns are the last nc (nc - 1) / 2 slots, column-major
   for (int ci = 0; ci < nc; ci++)
@@ -499,6 +506,8 @@ void flatten_plan(const SparsePlan &P, PlanImage &img) {
   img.off_dpart_ptr = put(P.dpart_ptr);
   img.off_opart_ptr = put(P.opart_ptr);
   img.off_clq = put(P.clq);
+  img.off_corder = put(P.corder);
+  img.off_ctask0 = put(P.ctask0);
 }
 
 }  // namespace m3s

@@ -58,6 +58,10 @@ struct SparsePlan {
   // update list (dtr list for ri == ci, tr list otherwise). nc = 0: none.
   int nc = 0;
   std::vector<int32_t> clq;
+  // Column tasks (multi-workgroup factorisation, col_factor_kernel): the
+  // sparse columns (< m - nc) in level order (a topological order), and the
+  // first OFF task of every column (its |struct(k)| tasks are contiguous).
+  std::vector<int32_t> corder, ctask0;
 };
 
 // ranks of (ii, jj) in sorted-unique(cat(ii, jj)); returns the unique count
@@ -78,9 +82,9 @@ struct PlanImage {
       off_dtr_slot, off_dtr_p, off_task_lev_ptr, off_task_dst, off_task_col, off_task_tr_ptr,
       off_tr_a, off_tr_b, off_asm_ptr, off_asm_edge, off_g_ptr, off_g_edge, off_ctask_ptr,
       off_items, off_wave_ptr, off_witems, off_part_q0, off_part_q1, off_part_tgt, off_dpart_ptr,
-      off_opart_ptr, off_clq;
+      off_opart_ptr, off_clq, off_corder, off_ctask0;
 };
-constexpr int kPlanSections = 29;
+constexpr int kPlanSections = 31;
 constexpr int kLltWaves = 16;  // waves of sparse_llt_kernel (1024 threads)
 void flatten_plan(const SparsePlan &P, PlanImage &img);
 

@@ -177,16 +177,16 @@ def version() -> str:
 PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col", "dtr_ptr",
                  "dtr_slot", "dtr_p", "task_lev_ptr", "task_dst", "task_col", "task_tr_ptr", "tr_a",
                  "tr_b", "asm_ptr", "asm_edge", "g_ptr", "g_edge", "ctask_ptr", "items", "wave_ptr", "witems",
-                 "part_q0", "part_q1", "part_tgt", "dpart_ptr", "opart_ptr", "clq")
+                 "part_q0", "part_q1", "part_tgt", "dpart_ptr", "opart_ptr", "clq", "corder", "ctask0")
 
 
 LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
-                   "plan", "Lblk", "Dinv", "tasks", "planes", "total")
+                   "plan", "Lblk", "Dinv", "tail", "tasks", "planes", "total")
 
 
 def workspace_layout(N, HW, E):
     """Byte offsets of the GN workspace sections (diagnostics/tests)."""
-    offs = (ctypes.c_size_t * 14)()
+    offs = (ctypes.c_size_t * len(LAYOUT_SECTIONS))()
     _lib.m3s_gn_layout_debug(int(N), int(HW), int(E), offs)
     return dict(zip(LAYOUT_SECTIONS, list(offs)))
 
@@ -221,7 +221,8 @@ def sparse_plan(N, ri, rj, split=0, max_parts=0):
             "asm_ptr": S + 1, "g_ptr": m + 1, "ctask_ptr": m + 1, "clq": 2 + nc + nc * nc,
             "items": n_items, "wave_ptr": 2, "witems": n_items,
             "part_q0": NP, "part_q1": NP, "part_tgt": NP,
-            "dpart_ptr": m + 1 if sp else 0, "opart_ptr": T + 1 if sp else 0}
+            "dpart_ptr": m + 1 if sp else 0, "opart_ptr": T + 1 if sp else 0,
+            "corder": m - nc, "ctask0": m}
     for name, ln in lens.items():
         plan[name] = plan[name][:ln]
     nnz = int(plan["col_ptr"][m])

@@ -1,21 +1,22 @@
 #!/bin/bash
-# GPU-box: the default bench line (with the CPU leg), then single-GPU bench
-# lines at 64 / 128 / 256 keyframes (the graph sizes of the N-GPU weak-scaling
-# runs, solved on one GPU). Any failure ends the script.
+# GPU-box: single-GPU bench lines at the weak-scaling graph sizes (64 / 128 /
+# 256 keyframes = the graphs of the 2 / 4 / 8-GPU runs, solved on one GPU),
+# MODE=calib|rays. Prints GN it/s, ms/step and the per-launch linearize and
+# solve times. Any failure ends the script.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
+TAG=${TAG:-sweep}
 mkdir -p $OUT
 cd $R
-timeout -k 10 300 python bench.py > $OUT/bench_full.json 2> $OUT/bench_full.err || { echo "bench failed"; tail -5 $OUT/bench_full.err; exit 1; }
-cat $OUT/bench_full.json
 for n in ${NS:-64 128 256}; do
-  timeout -k 10 240 python bench.py --kf-per-gpu $n --steps 3 --warmup 1 --no-cpu --no-tracker > $OUT/bench_n$n.json 2> $OUT/bench_n$n.err || { echo "bench n=$n failed"; tail -5 $OUT/bench_n$n.err; exit 1; }
-  python - "$OUT/bench_n$n.json" <<'EOF'
+  timeout -k 10 240 python bench.py --kf-per-gpu $n --steps 3 --warmup 1 --cold-steps 2 --no-cpu --no-tracker --mode ${MODE:-calib} ${BENCH_ARGS:-} > $OUT/${TAG}_n$n.json 2> $OUT/${TAG}_n$n.err || { echo "bench n=$n failed"; tail -5 $OUT/${TAG}_n$n.err; exit 1; }
+  python - "$OUT/${TAG}_n$n.json" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
-c = d["config"]
-print(c["keyframes"], "KF", c["directed_edges"], "edges:", d["value"], "pair-it/s,", d["gn_iters_per_s"], "GN it/s,",
-      d["ms_per_step"], "ms/step, linearize", d["roofline"]["avg_launch_ms"], "ms")
-EOF
+c, r = d["config"], d["roofline"]
+print(c["keyframes"], "KF", c["directed_edges"], "edges:", d["gn_iters_per_s"], "GN it/s,", d["ms_per_step"],
+      "ms/step (cold", d["cold"]["ms_per_step"], "), linearize", r["avg_launch_ms"], "ms, gather",
+      r["gather_kernel"]["avg_launch_ms"], "ms, solve", r["solve"]["avg_ms"], "ms")
+PY
 done

@@ -400,25 +400,45 @@ def copy_leg(dev, nbytes=1 << 30, reps=10):
 
 
 def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
-    """configs[1]: single-keyframe tracking GN at 512x512 (replicas only)."""
+    """configs[1]: single-keyframe tracking GN at 512x512 (replicas only).
+    The default path is the persistent one-launch tracker; the launch-per-
+    iteration path (M3S_TRACK_PERSISTENT=0) is timed beside it."""
     p = synthetic.make_pair(H, W, seed=1002, device=dev)
     a = (p.Xf.contiguous(), p.Xk.contiguous(), p.T_WCf_init.data.contiguous(), p.T_WCk.data.contiguous(),
          p.Qk.contiguous(), p.valid.contiguous())
     call = lambda: be.track_rays_sim3(*a, 0.003, 10.0, 1.345, iters, 0.0, 0.0, sync_every=0)  # noqa: E731
-    for _ in range(3):
-        call()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        out = call()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    assert int(out[2][0]) == iters
+
+    def timed():
+        for _ in range(3):
+            call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = call()
+        torch.cuda.synchronize()
+        assert int(out[2][0]) == iters
+        return time.perf_counter() - t0
+
+    dt = timed()
+    old = os.environ.get("M3S_TRACK_PERSISTENT")
+    os.environ["M3S_TRACK_PERSISTENT"] = "0"
+    try:
+        dt_l = timed()
+    finally:
+        if old is None:
+            del os.environ["M3S_TRACK_PERSISTENT"]
+        else:
+            os.environ["M3S_TRACK_PERSISTENT"] = old
     return {"workload": "C2: 1 frame->keyframe pair, rays+dist Sim3 GN, %dx%d, %d fixed iterations"
                         % (H, W, iters),
             "gn_iters_per_s": round(reps * iters / dt, 1), "ms_per_solve": round(dt / reps * 1e3, 4),
-            "bytes_per_iter": 45 * H * W,
-            "hbm_frac": round(45 * H * W * reps * iters / dt / 1e9 / HBM_PEAK_GBS, 4)}
+            "path": "persistent (one launch per solve; pixel inputs register-resident after iteration 1)",
+            "bytes_per_solve": 45 * H * W,
+            "bound": "latency: one grid-wide arrival + all-partials read per iteration",
+            "launch_per_iter": {"gn_iters_per_s": round(reps * iters / dt_l, 1),
+                                "ms_per_solve": round(dt_l / reps * 1e3, 4),
+                                "note": "M3S_TRACK_PERSISTENT=0: one linearize launch per iteration, "
+                                        "45 B per pixel re-read each time"}}
 
 
 def matching_leg(be, synthetic, dev, H, W, reps=20):

@@ -632,6 +632,162 @@ __device__ __forceinline__ void pixel_contrib(ACC &acc, const ResidualParams &P,
   }
 }
 
+// ------------------------------------- pixel-pair packed accumulation --
+// Two PIXELS per lane in the halves of a float2: every per-pixel operation
+// (the Sim(3) transform, the residuals, the Jacobian entries, the Huber
+// weights and all 36 normal-equation sums) is one v_pk_* instruction for
+// both pixels; only the transcendentals (v_sqrt / v_rcp / v_log) stay
+// scalar. Entries no row of the model touches stay compile-time zeros and
+// take no registers (rays 33, calib 32 live sums). Same per-pixel products as
+// pixel_contrib; the fp32 sums are per half, then combined in fold().
+struct AccumPP {
+  f32x2 s[kNP];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int k = 0; k < kNP; k++) s[k] = f32x2{0.0f, 0.0f};
+  }
+  __device__ __forceinline__ void fold(float *acc) const {
+#pragma unroll
+    for (int k = 0; k < kNP; k++) acc[k] += s[k].x + s[k].y;
+  }
+  // one residual row (non-zero columns M, a[p] = the p-th entry) of both pixels
+  template <unsigned M, int K>
+  __device__ __forceinline__ void add(const f32x2 (&a)[K], f32x2 w, f32x2 e) {
+    f32x2 wa[K];
+#pragma unroll
+    for (int p = 0; p < K; p++) wa[p] = w * a[p];
+#pragma unroll
+    for (int p = 0; p < K; p++)
+#pragma unroll
+      for (int q = p; q < K; q++) {
+        const int t = kL + tri(nth_col(M, p), nth_col(M, q));
+        s[t] = __builtin_elementwise_fma(wa[p], a[q], s[t]);
+      }
+    const f32x2 we = w * e;
+#pragma unroll
+    for (int p = 0; p < K; p++) s[kG + nth_col(M, p)] = __builtin_elementwise_fma(we, a[p], s[kG + nth_col(M, p)]);
+    s[kCost] = __builtin_elementwise_fma(we, e, s[kCost]);
+  }
+};
+
+// keeps the scheduler from hoisting the next row's products over this row's
+// sums (register pressure of the pixel-pair kernels)
+#ifndef M3S_ROWBAR
+#define M3S_ROWBAR 1
+#endif
+#if M3S_ROWBAR
+#define M3S_ROW_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define M3S_ROW_BARRIER()
+#endif
+__device__ __forceinline__ f32x2 splat2(float v) { return f32x2{v, v}; }
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 rcp2(f32x2 x) { return f32x2{frcp(x.x), frcp(x.y)}; }
+__device__ __forceinline__ f32x2 sqrt2(f32x2 x) { return f32x2{fsqrt(x.x), fsqrt(x.y)}; }
+__device__ __forceinline__ f32x2 abs2(f32x2 x) { return f32x2{fabsf(x.x), fabsf(x.y)}; }
+__device__ __forceinline__ f32x2 min2(f32x2 a, f32x2 b) { return f32x2{fminf(a.x, b.x), fminf(a.y, b.y)}; }
+__device__ __forceinline__ f32x2 sel2(bool cx, bool cy, f32x2 a, f32x2 b) {
+  return f32x2{cx ? a.x : b.x, cy ? a.y : b.y};
+}
+
+// Y = T X for two points (same FMA order per element as act(Sim3Mat))
+__device__ __forceinline__ void act2(const Sim3Mat &M, const f32x2 (&X)[3], f32x2 (&Y)[3]) {
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+    Y[r] = fma2(splat2(M.m[3 * r]), X[0],
+                fma2(splat2(M.m[3 * r + 1]), X[1], fma2(splat2(M.m[3 * r + 2]), X[2], splat2(M.t[r]))));
+}
+
+// pixel_contrib for two pixels: in[k] = plane k of both, Y = T_ij Xj of both
+template <int MODE, int NPL>
+__device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParams &P, const f32x2 (&in)[NPL],
+                                               const f32x2 (&Y)[3]) {
+  if constexpr (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
+    const f32x2 nj2 = fma2(Y[0], Y[0], fma2(Y[1], Y[1], Y[2] * Y[2]));
+    const f32x2 nj = sqrt2(nj2);
+    const f32x2 inj = rcp2(nj);
+    const f32x2 rx = Y[0] * inj, ry = Y[1] * inj, rz = Y[2] * inj;
+    const f32x2 e0 = rx - in[0], e1 = ry - in[1], e2 = rz - in[2], e3 = nj - in[3];
+    const f32x2 swr = in[4] * P.inv_sig_a, swd = in[4] * P.inv_sig_b;
+    const f32x2 kr = swr * swr, kd = swd * swd;
+    const f32x2 hk = splat2(P.huber_k);
+    // huber(sw e) sw^2 = min(1, k / |sw e|) sw^2
+    const f32x2 w0 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e0))) * kr;
+    const f32x2 w1 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e1))) * kr;
+    const f32x2 w2 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e2))) * kr;
+    const f32x2 w3 = min2(splat2(1.0f), hk * rcp2(abs2(swd * e3))) * kd;
+    // d r / d P = (I - r r^T) / |P|
+    const f32x2 rxi = rx * inj, ryi = ry * inj, rzi = rz * inj;
+    const f32x2 dxx = inj - rx * rxi, dyy = inj - ry * ryi, dzz = inj - rz * rzi;
+    const f32x2 dxy = -(ry * rxi), dxz = -(rz * rxi), dyz = -(rz * ryi);
+    const f32x2 ax[5] = {dxx, dxy, dxz, rz, -ry};  // kRayX: tau0 tau1 tau2 phi1 phi2
+    const f32x2 ay[5] = {dxy, dyy, dyz, -rz, rx};  // kRayY: tau0 tau1 tau2 phi0 phi2
+    const f32x2 az[5] = {dxz, dyz, dzz, ry, -rx};  // kRayZ: tau0 tau1 tau2 phi0 phi1
+    const f32x2 ad[4] = {rx, ry, rz, nj};          // kRayD: tau0 tau1 tau2 sigma
+    acc.add<kRayX, 5>(ax, w0, e0);
+    M3S_ROW_BARRIER();
+    acc.add<kRayY, 5>(ay, w1, e1);
+    M3S_ROW_BARRIER();
+    acc.add<kRayZ, 5>(az, w2, e2);
+    M3S_ROW_BARRIER();
+    acc.add<kRayD, 4>(ad, w3, e3);
+    M3S_ROW_BARRIER();
+  } else if constexpr (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
+    // focal-normalised u / v rows as in pixel_contrib
+    const bool vzx = Y[2].x > P.z_eps, vzy = Y[2].y > P.z_eps;
+    const f32x2 zr = rcp2(Y[2]);
+    const f32x2 lj = f32x2{flog(Y[2].x), flog(Y[2].y)};
+    const f32x2 zero2 = splat2(0.0f);
+    const f32x2 zinv = sel2(vzx, vzy, zr, zero2);
+    const f32x2 e2 = sel2(vzx, vzy, lj - in[2], zero2);
+    const int ux = __float_as_int(in[0].x), uy = __float_as_int(in[0].y);
+    const f32x2 tu = {(float)(ux & 0xffff), (float)(uy & 0xffff)};
+    const f32x2 tv = {(float)(ux >> 16), (float)(uy >> 16)};
+    const f32x2 x = Y[0] * zinv, y = Y[1] * zinv;
+    const f32x2 u = fma2(splat2(P.fx), x, splat2(P.cx)), v = fma2(splat2(P.fy), y, splat2(P.cy));
+    const float ulim = (float)P.width - 1.0f - P.border, vlim = (float)P.height - 1.0f - P.border;
+    const bool gx = (u.x > P.border) && (u.x < ulim) && (v.x > P.border) && (v.x < vlim) && vzx;
+    const bool gy = (u.y > P.border) && (u.y < ulim) && (v.y > P.border) && (v.y < vlim) && vzy;
+    const f32x2 sq = sel2(gx, gy, in[1], zero2);
+    const f32x2 etu = (u - tu) * (1.0f / P.fx), etv = (v - tv) * (1.0f / P.fy);
+    const f32x2 swu = sq * (P.inv_sig_a * P.fx), swv = sq * (P.inv_sig_a * P.fy);
+    const f32x2 hk = splat2(P.huber_k);
+    const f32x2 Wu = min2(swu * swu, (swu * hk) * rcp2(abs2(etu)));
+    const f32x2 Wv = min2(swv * swv, (swv * hk) * rcp2(abs2(etv)));
+    const f32x2 swz = sq * P.inv_sig_b;
+    const f32x2 Wz = min2(swz * swz, (swz * hk) * rcp2(abs2(e2)));
+    const f32x2 xyp = x * y;
+    const f32x2 one = splat2(1.0f);
+    const f32x2 au[5] = {zinv, -(x * zinv), -xyp, fma2(x, x, one), -y};  // kCalU: 0 2 3 4 5
+    const f32x2 av[5] = {zinv, -(y * zinv), -fma2(y, y, one), xyp, x};  // kCalV: 1 2 3 4 5
+    const f32x2 az[4] = {zinv, y, -x, one};                              // kCalZ: 2 3 4 6
+    acc.add<kCalU, 5>(au, Wu, etu);
+    M3S_ROW_BARRIER();
+    acc.add<kCalV, 5>(av, Wv, etv);
+    M3S_ROW_BARRIER();
+    acc.add<kCalZ, 4>(az, Wz, e2);
+    M3S_ROW_BARRIER();
+  } else {  // 3D point (point_align_kernel :564-674)
+    const f32x2 e0 = Y[0] - in[0], e1 = Y[1] - in[1], e2 = Y[2] - in[2];
+    const f32x2 sw = in[3] * P.inv_sig_a;
+    const f32x2 k2 = sw * sw;
+    const f32x2 hk = splat2(P.huber_k);
+    const f32x2 w0 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e0))) * k2;
+    const f32x2 w1 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e1))) * k2;
+    const f32x2 w2 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e2))) * k2;
+    const f32x2 one = splat2(1.0f);
+    const f32x2 ax[4] = {one, Y[2], -Y[1], Y[0]};  // kPtX: 0 4 5 6
+    const f32x2 ay[4] = {one, -Y[2], Y[0], Y[1]};  // kPtY: 1 3 5 6
+    const f32x2 az[4] = {one, Y[1], -Y[0], Y[2]};  // kPtZ: 2 3 4 6
+    acc.add<kPtX, 4>(ax, w0, e0);
+    M3S_ROW_BARRIER();
+    acc.add<kPtY, 4>(ay, w1, e1);
+    M3S_ROW_BARRIER();
+    acc.add<kPtZ, 4>(az, w2, e2);
+    M3S_ROW_BARRIER();
+  }
+}
+
 // wave64 butterfly sum
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

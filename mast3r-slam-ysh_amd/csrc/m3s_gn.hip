@@ -50,6 +50,12 @@ typedef long long i64x2 __attribute__((ext_vector_type(2)));
 
 namespace {
 
+#ifndef M3S_PP  // packed linearize: two pixels per float2 (AccumPP) instead of row pairs
+#define M3S_PP 1
+#endif
+#ifndef M3S_PP_LDS  // PP: operands read from the LDS slot per pixel pair
+#define M3S_PP_LDS 1
+#endif
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
@@ -539,8 +545,15 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
 // keyframe, which the task table places on one XCD back to back). No gathers.
 // calib / points fit 128 VGPRs (4 waves per SIMD); rays keeps 84 accumulator
 // VGPRs and is left unbounded (164, 3 waves)
+#ifndef M3S_PK_WAVES  // packed linearize: minimum waves per SIMD (register bound 512 / w)
+#define M3S_PK_WAVES (M3S_PP ? 3 : 4)
+#endif
+#ifndef M3S_PK_WAVES_RAYS
+#define M3S_PK_WAVES_RAYS (M3S_PP ? 3 : 1)
+#endif
 template <int MODE>
-__global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_kernel(LinArgs A) {
+__global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_PK_WAVES)
+    linearize_packed_kernel(LinArgs A) {
   if (*A.stop) return;
   const int64_t b = block_task(A);
   if (b < 0) return;
@@ -555,7 +568,11 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
   constexpr int NPL = PixIn<MODE>::kPlanes;
   const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
 
+#if M3S_PP
+  AccumPP acc;
+#else
   Accum<MODE> acc;
+#endif
   acc.zero();
   const int64_t p_begin = c * A.chunk_pix;
   const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
@@ -567,6 +584,32 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
     xv[0] = xj4[0], xv[1] = xj4[1], xv[2] = xj4[2];
   };
   float sink = 0.0f;  // 0 experiment only
+#if M3S_PP
+  // pixel pairs (0, 1) and (2, 3) in the halves of float2 registers; Xj of the
+  // 4 pixels arrives interleaved: x0 y0 z0 x1 | y1 z1 x2 y2 | z2 x3 y3 z3
+  auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
+    {
+      const f32x2 X[3] = {{xv[0].x, xv[0].w}, {xv[0].y, xv[1].x}, {xv[0].z, xv[1].y}};
+      f32x2 in[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].x, pv[k].y};
+      f32x2 Y[3];
+      act2(Tm, X, Y);
+      pixel_contrib2<MODE, NPL>(acc, A.P, in, Y);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const f32x2 X[3] = {{xv[1].z, xv[2].y}, {xv[1].w, xv[2].z}, {xv[2].x, xv[2].w}};
+      f32x2 in[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].z, pv[k].w};
+      f32x2 Y[3];
+      act2(Tm, X, Y);
+      pixel_contrib2<MODE, NPL>(acc, A.P, in, Y);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#else
   auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
     const float Xj[4][3] = {{xv[0].x, xv[0].y, xv[0].z}, {xv[0].w, xv[1].x, xv[1].y},
                             {xv[1].z, xv[1].w, xv[2].x}, {xv[2].y, xv[2].z, xv[2].w}};
@@ -582,6 +625,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
       if ((s + 1) % 1 == 0) __builtin_amdgcn_sched_barrier(0);
     }
   };
+#endif
   // Prefetch one trip ahead through LDS with no VGPR cost: each wave's next
   // trip (NPL plane vectors + 3 Xj vectors, 16 B per lane each) is loaded by
   // global_load_lds_dwordx4 into the wave's own LDS slot while the wave
@@ -605,6 +649,35 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
   if (p0 < p_end) issue(p0);
   for (; p0 < p_end; p0 += kBlockPix) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if M3S_PP && M3S_PP_LDS
+    // each pixel pair's operands are read from the LDS slot just before its
+    // math (8-B reads: 2 NPL + 6 VGPRs live instead of 4 (NPL + 3)); the slot
+    // is refilled once the second pair's operands are in registers
+    const float *sl = reinterpret_cast<const float *>(&stage[wv][0][ln]);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      f32x2 in[NPL], X[3];
+#pragma unroll
+      for (int k = 0; k < NPL; k++) in[k] = *reinterpret_cast<const f32x2 *>(sl + 256 * k + 2 * h);
+      // Xj of pixels 2h, 2h + 1: floats 6h .. 6h + 5 of the lane's 12
+      const float *xs = sl + 256 * NPL;
+      float xf[6];
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const int f = 6 * h + q;
+        xf[q] = xs[256 * (f >> 2) + (f & 3)];
+      }
+      X[0] = f32x2{xf[0], xf[3]}, X[1] = f32x2{xf[1], xf[4]}, X[2] = f32x2{xf[2], xf[5]};
+      if (h == 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
+        if (p0 + kBlockPix < p_end) issue(p0 + kBlockPix);
+      }
+      f32x2 Y[3];
+      act2(Tm, X, Y);
+      pixel_contrib2<MODE, NPL>(acc, A.P, in, Y);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
     f32x4 pv[NPL], xv[3];
 #pragma unroll
     for (int k = 0; k < NPL; k++) pv[k] = stage[wv][k][ln];
@@ -613,6 +686,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? 1 : 4) linearize_packed_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
     if (p0 + kBlockPix < p_end) issue(p0 + kBlockPix);
     do_trip(pv, xv);
+#endif
   }
   float sums[kNP];
 #pragma unroll
@@ -1170,6 +1244,11 @@ __device__ __forceinline__ double ld_sc1(const double *p) {
 __device__ __forceinline__ void st_sc1(double *p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-B write-through store (global_store_dwordx4 ... sc1); the caller drains
+// it with an explicit s_waitcnt vmcnt(0) before signalling
+__device__ __forceinline__ void st_sc1_x4(float *p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 template <bool SC1>
 __device__ __forceinline__ double ld_blk(const double *p) {
@@ -3082,10 +3161,11 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
 // --------------------------------------------------------------- tracker --
 
 constexpr size_t kTrackStateOff = 0;
-inline size_t track_partials_off() { return 256; }
 
+struct TrackSync;
 __global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackState *st, int32_t *info,
-                                  float *T_WCf_out, float *T_CkCf_out) {
+                                  float *T_WCf_out, float *T_CkCf_out, uint32_t *sync_words, int n_sync) {
+  for (int k = threadIdx.x; k < n_sync; k += blockDim.x) sync_words[k] = 0u;
   if (threadIdx.x != 0) return;
   const Sim3f Tk = load_sim3(T_WCk), Tf = load_sim3(T_WCf);
   const Sim3f R = compose(inverse(Tk), Tf);
@@ -3097,6 +3177,69 @@ __global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackS
   for (int k = 0; k < 8; k++) info[k] = 0;
   store_sim3(T_CkCf_out, R);
   store_sim3(T_WCf_out, Tf);
+}
+
+// One tracker GN update from the reduced sums s (kL / kG / kCost layout):
+// 7x7 fp64 Cholesky of H (one thread, fully unrolled; 1/L_kk by rsqrt + 2
+// Newton steps, no IEEE sqrt / division sequences on the serial chain),
+// tau = -H^-1 g (tracker.py:156-171: g = sum w e J with e = pred - meas), the
+// retraction T <- Exp(tau) T, and check_convergence (nonlinear_optimizer.py:
+// 5-25; rel is NaN on the first step, old_cost = inf). T and old_cost are
+// updated in place unless the Cholesky fails.
+constexpr int kTrackContinue = 0, kTrackConverged = 1, kTrackFailed = 2;
+__device__ __forceinline__ int track_update(const double *s, Sim3f &T, double &old_cost, float rel_error,
+                                            float delta_norm) {
+  double H[7][7], L[7][7], g[7], y[7], x[7];
+  for (int a = 0; a < 7; a++)
+    for (int c = 0; c < 7; c++) H[a][c] = s[kL + tri(a < c ? a : c, a < c ? c : a)];
+  for (int a = 0; a < 7; a++) g[a] = s[kG + a];
+  const double cost = 0.5 * s[kCost];
+  double dinv[7];
+#pragma unroll
+  for (int a = 0; a < 7; a++)
+#pragma unroll
+    for (int c = 0; c < 7; c++) L[a][c] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    double d = H[k][k];
+#pragma unroll
+    for (int p = 0; p < k; p++) d -= L[k][p] * L[k][p];
+    if (!(d > 0.0)) return kTrackFailed;
+    dinv[k] = rsqrt_nr(d);
+    L[k][k] = d * dinv[k];
+#pragma unroll
+    for (int i = k + 1; i < 7; i++) {
+      double v = H[i][k];
+#pragma unroll
+      for (int p = 0; p < k; p++) v -= L[i][p] * L[k][p];
+      L[i][k] = v * dinv[k];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    double v = -g[i];
+#pragma unroll
+    for (int p = 0; p < i; p++) v -= L[i][p] * y[p];
+    y[i] = v * dinv[i];
+  }
+#pragma unroll
+  for (int i = 6; i >= 0; i--) {
+    double v = y[i];
+#pragma unroll
+    for (int p = i + 1; p < 7; p++) v -= L[p][i] * x[p];
+    x[i] = v * dinv[i];
+  }
+  float tau[7];
+  float n2 = 0.0f;
+  for (int k = 0; k < 7; k++) {
+    tau[k] = (float)x[k];
+    n2 += tau[k] * tau[k];
+  }
+  T = retract(tau, T);
+  const float cost_f = (float)cost;  // the reference's cost is a python float of an fp32 .item()
+  const double rel = fabs((old_cost - (double)cost_f) / old_cost);  // NaN on the first step
+  old_cost = (double)cost_f;
+  return (rel < (double)rel_error || sqrtf(n2) < delta_norm) ? kTrackConverged : kTrackContinue;
 }
 
 // reduce chunk partials, 7x7 fp64 Cholesky, tau = -H^-1 g, retraction,
@@ -3140,73 +3283,261 @@ __device__ void track_solve_block(const LinArgs &A) {
   }
   __syncthreads();
   if (t != 0) return;
-  double H[7][7], L[7][7], g[7], y[7], x[7];
-  for (int a = 0; a < 7; a++)
-    for (int c = 0; c < 7; c++) H[a][c] = s[kL + tri(a < c ? a : c, a < c ? c : a)];
-  for (int a = 0; a < 7; a++) g[a] = s[kG + a];
-  const double cost = 0.5 * s[kCost];
-  // one thread, fully unrolled; 1/L_kk by rsqrt + 2 Newton steps (no IEEE
-  // sqrt / division sequences on the serial chain)
-  double dinv[7];
-#pragma unroll
-  for (int a = 0; a < 7; a++)
-#pragma unroll
-    for (int c = 0; c < 7; c++) L[a][c] = 0.0;
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    double d = H[k][k];
-#pragma unroll
-    for (int p = 0; p < k; p++) d -= L[k][p] * L[k][p];
-    if (!(d > 0.0)) {  // torch.linalg.cholesky raises -> tracking failure
-      info[M3S_INFO_SOLVE_FAIL] = 1;
-      info[M3S_INFO_ITERS] += 1;
-      st->done = 1;
-      return;
-    }
-    dinv[k] = rsqrt_nr(d);
-    L[k][k] = d * dinv[k];
-#pragma unroll
-    for (int i = k + 1; i < 7; i++) {
-      double v = H[i][k];
-#pragma unroll
-      for (int p = 0; p < k; p++) v -= L[i][p] * L[k][p];
-      L[i][k] = v * dinv[k];
-    }
-  }
-  // tau = H^-1 (-g): kernel g = sum w e J with e = pred - meas  (tracker.py:165-169)
-#pragma unroll
-  for (int i = 0; i < 7; i++) {
-    double v = -g[i];
-#pragma unroll
-    for (int p = 0; p < i; p++) v -= L[i][p] * y[p];
-    y[i] = v * dinv[i];
-  }
-#pragma unroll
-  for (int i = 6; i >= 0; i--) {
-    double v = y[i];
-#pragma unroll
-    for (int p = i + 1; p < 7; p++) v -= L[p][i] * x[p];
-    x[i] = v * dinv[i];
-  }
-  float tau[7];
-  float n2 = 0.0f;
-  for (int k = 0; k < 7; k++) {
-    tau[k] = (float)x[k];
-    n2 += tau[k] * tau[k];
-  }
-  const Sim3f Tn = retract(tau, load_sim3(st->T_rel));
-  store_sim3(st->T_rel, Tn);
-  store_sim3(T_CkCf_out, Tn);
-  store_sim3(T_WCf_out, compose(load_sim3(st->T_WCk), Tn));
+  Sim3f T = load_sim3(st->T_rel);
+  double old = st->old_cost;
+  const int r = track_update(s, T, old, rel_error, delta_norm);
   info[M3S_INFO_ITERS] += 1;
-  const float cost_f = (float)cost;  // the reference's cost is a python float of an fp32 .item()
-  const double old = st->old_cost;
-  const double rel = fabs((old - (double)cost_f) / old);  // NaN on the first step (old = inf)
-  if (rel < (double)rel_error || sqrtf(n2) < delta_norm) {
+  if (r == kTrackFailed) {  // torch.linalg.cholesky raises -> tracking failure
+    info[M3S_INFO_SOLVE_FAIL] = 1;
+    st->done = 1;
+    return;
+  }
+  store_sim3(st->T_rel, T);
+  store_sim3(T_CkCf_out, T);
+  store_sim3(T_WCf_out, compose(load_sim3(st->T_WCk), T));
+  if (r == kTrackConverged) {
     st->done = 1;
     info[M3S_INFO_CONVERGED] = 1;
   }
-  st->old_cost = (double)cost_f;
+  st->old_cost = old;
+}
+
+// ------------------------------------------------ persistent tracker GN --
+// All iterations of one frame -> keyframe solve in ONE launch (tracker.py:
+// 173-266). G <= 256 workgroups, one per CU, each owning PPL pixels per lane.
+// A lane loads its pixels' inputs once (target-side PixIn from Xk / Q / valid
+// and the source point Xf) and keeps them in registers across iterations, so
+// iterations 2.. read nothing from HBM. Per iteration:
+//   1. each workgroup accumulates its pixels (the packed Accum of the backend
+//      kernels) and stores its 36-float partial, write-through (sc1), into the
+//      iteration's slot (double-buffered by iteration parity);
+//   2. arrival: one lane per workgroup adds 1 to counter shard b % 8 (8
+//      counters on lines of their own: 32 arrivals per word instead of 256);
+//      wave 0 polls all shards (sc1 loads) until every workgroup has arrived;
+//   3. EVERY workgroup reads all G partials (sc1 loads) and sums them in fp64
+//      in a fixed order, then its thread 0 runs the same 7x7 update
+//      (track_update): identical inputs and order give identical poses and
+//      convergence decisions in every workgroup, so nothing is broadcast and
+//      all workgroups leave the loop together.
+// Slot reuse is safe: a workgroup writes slot it % 2 for iteration it only
+// after every workgroup arrived at it - 1, i.e. finished reading slot it - 2.
+// Waits are bounded (a timeout ends the solve with info[SOLVE_FAIL] = 2).
+// Hand-off form: MI355X_MICROARCH.md inter-workgroup table, row 1 (sc1 stores
+// drained by the storing wave, agent atomic add by one lane of it, sc1 poll,
+// sc1 loads after a workgroup barrier).
+constexpr int kTrkThreads = 512;
+constexpr int kTrkMaxBlocks = 256;
+constexpr int kTrkShards = 8;
+constexpr int kTrkSpins = 1 << 22;
+struct TrackSync {
+  uint32_t ctr[kTrkShards][32];  // arrival counters, one 128-B line each
+  uint32_t top[32];              // arrivals of the shards' last workgroups
+  uint32_t gen[32];              // iterations published by the reducer
+  float rec[32];                 // the published pose (8) and status
+  double old_cost[16];           // the published cost (check_convergence)
+  double shard_sum[kTrkShards][kNP];  // level-1 sums (fp64)
+};
+inline size_t track_sync_off() { return 128; }  // after TrackState (<= 128 B)
+inline size_t track_part_off() { return track_sync_off() + sizeof(TrackSync); }
+static_assert(sizeof(TrackState) <= 128, "TrackState must fit before the sync lines");
+
+#ifdef M3S_TRK_STAMPS  // phase stamps of workgroups 0 and G - 1 (tools/trk_stamps.py)
+__device__ int64_t g_trk_stamp[2][16][8];
+#define M3S_TSTAMP(ph)                                                                     \
+  if (t == 0 && (b == 0 || b == G - 1) && it < 16) g_trk_stamp[b == 0 ? 0 : 1][it][ph] = wall_clock64();
+#else
+#define M3S_TSTAMP(ph)
+#endif
+template <int MODE, int PPL>
+__global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A, int max_iters, TrackSync *sync) {
+  const int G = (int)gridDim.x, b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+  constexpr int NW = kTrkThreads / 64;
+  __shared__ float redf[NW][kNP];
+  __shared__ double redd[NW][kNP];
+  __shared__ double s_sum[kNP];
+  __shared__ float T_s[8];
+  __shared__ int state_s;  // kTrackContinue / kTrackConverged / kTrackFailed / 3 = barrier timeout
+  __shared__ __attribute__((aligned(16))) float blk_s[kNP];
+  TrackState *st = A.track;
+  const int64_t HW = A.HW;
+  PixIn<MODE> in[PPL];
+  float Xf[PPL][3];
+  bool live[PPL];
+#pragma unroll
+  for (int s = 0; s < PPL; s++) {
+    const int64_t p = ((int64_t)b * PPL + s) * kTrkThreads + t;
+    live[s] = p < HW;
+    const int64_t pc = live[s] ? p : 0;
+    in[s] = gather_pixel<MODE, true>(A, A.Xs, nullptr, pc, A.valid[pc] != 0, 0, A.Q[pc], 0.0f);
+    Xf[s][0] = A.Xsrc[3 * pc], Xf[s][1] = A.Xsrc[3 * pc + 1], Xf[s][2] = A.Xsrc[3 * pc + 2];
+  }
+  Sim3f T = load_sim3(st->T_rel);
+  const Sim3f Tk = load_sim3(st->T_WCk);
+  int it = 0, status = kTrackContinue;
+  for (; it < max_iters; it++) {
+    M3S_TSTAMP(0)
+    const Sim3Mat Tm = sim3_matrix(T);
+    Accum<MODE> acc;
+    acc.zero();
+#pragma unroll
+    for (int s = 0; s < PPL; s++) {
+      if (live[s]) {
+        float Y[3];
+        act(Tm, Xf[s], Y);
+        pixel_contrib<MODE>(acc, A.P, in[s], Y);
+      }
+    }
+    float v[kNP];
+#pragma unroll
+    for (int k = 0; k < kNP; k++) v[k] = 0.0f;
+    acc.fold(v);
+    M3S_TSTAMP(1)
+    {
+      int idx;
+      bool ok;
+      const float x = xreduce36(v, lane, idx, ok);
+      if (ok) redf[wv][idx] = x;
+    }
+    __syncthreads();
+    float *slot = A.partials;
+    if (wv == 0) {
+      // block partial -> LDS -> 9 x 16-B write-through stores
+      if (lane < kNP) {
+        float x = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NW; w++) x += redf[w][lane];
+        blk_s[lane] = x;
+      }
+      wave_lds_fence();
+      if (lane < kNP / 4) st_sc1_x4(slot + (size_t)b * kNP + 4 * lane, reinterpret_cast<const f32x4 *>(blk_s)[lane]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has left this wave
+      M3S_TSTAMP(2)
+      // level 1: the last arriver of shard s = b % 8 (told by the value its
+      // add returned) sums the shard's partials (blocks s, s + 8, ..., lane j
+      // = block s + 8 j: a fixed order) into shard_sum[s] in fp64
+      const int sh = b % kTrkShards;
+      const uint32_t n_sh = (uint32_t)(G - sh + kTrkShards - 1) / kTrkShards;
+      const uint32_t n_top = (uint32_t)(G < kTrkShards ? G : kTrkShards);
+      uint32_t o = 0;
+      if (lane == 0) o = __hip_atomic_fetch_add(&sync->ctr[sh][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      o = __builtin_amdgcn_readfirstlane(o);
+      bool top_last = false;
+      if (o == n_sh * (uint32_t)(it + 1) - 1) {
+        double a[kNP];
+#pragma unroll
+        for (int k = 0; k < kNP; k++) a[k] = 0.0;
+        if (lane < (int)n_sh) {
+          const unsigned long long *src =
+              reinterpret_cast<const unsigned long long *>(slot + (size_t)(sh + kTrkShards * lane) * kNP);
+          unsigned long long w2[kNP / 2];
+#pragma unroll
+          for (int k = 0; k < kNP / 2; k++) w2[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int k = 0; k < kNP / 2; k++) {
+            a[2 * k] = (double)__uint_as_float((uint32_t)(w2[k] & 0xffffffffull));
+            a[2 * k + 1] = (double)__uint_as_float((uint32_t)(w2[k] >> 32));
+          }
+        }
+        int idx;
+        bool ok;
+        const double x = xreduce36(a, lane, idx, ok);
+        if (ok) st_sc1(&sync->shard_sum[sh][idx], x);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // level 2: the last shard reducer sums the shard sums in shard order
+        uint32_t o2 = 0;
+        if (lane == 0) o2 = __hip_atomic_fetch_add(&sync->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        o2 = __builtin_amdgcn_readfirstlane(o2);
+        top_last = o2 == n_top * (uint32_t)(it + 1) - 1;
+      }
+      if (top_last) {
+        M3S_TSTAMP(3)
+        if (lane < kNP) {
+          double v[kTrkShards];
+#pragma unroll
+          for (int j = 0; j < kTrkShards; j++) v[j] = j < (int)n_top ? ld_sc1(&sync->shard_sum[j][lane]) : 0.0;
+          double x = 0.0;
+#pragma unroll
+          for (int j = 0; j < kTrkShards; j++) x += v[j];
+          s_sum[lane] = x;
+        }
+        wave_lds_fence();
+        M3S_TSTAMP(4)
+        if (lane == 0) {
+          // the previous reducer's cost (published with its record; inf first)
+          double oc = it == 0 ? __builtin_inf() : ld_sc1(&sync->old_cost[0]);
+          Sim3f Tn = T;
+          const int r = track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
+          if (r == kTrackFailed) Tn = T;
+          float rec[9];
+          store_sim3(rec, Tn);
+          rec[8] = __int_as_float(r);
+#pragma unroll
+          for (int k = 0; k < 8; k++) T_s[k] = rec[k];
+          state_s = r;
+#pragma unroll
+          for (int k = 0; k < 9; k++) store_sc1(&sync->rec[k], rec[k]);
+          st_sc1(&sync->old_cost[0], oc);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(&sync->gen[0], (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else if (lane == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(&sync->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)(it + 1)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kTrkSpins) break;
+        }
+        M3S_TSTAMP(4)
+        if (spins > kTrkSpins) {
+          state_s = 3;
+        } else {
+          float rec[9];
+#pragma unroll
+          for (int k = 0; k < 9; k++)
+            rec[k] = __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t *>(&sync->rec[k]), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+          for (int k = 0; k < 8; k++) T_s[k] = rec[k];
+          state_s = __float_as_int(rec[8]);
+        }
+      }
+    }
+    M3S_TSTAMP(5)
+    __syncthreads();
+    status = state_s;
+    if (status == 3 || status == kTrackFailed) break;
+    T = load_sim3(T_s);
+    if (status == kTrackConverged) break;
+  }
+  if (b == 0 && t == 0) {  // outputs: the last successful pose, the iteration count, the status
+    A.info[M3S_INFO_ITERS] = it < max_iters ? it + 1 : max_iters;
+    if (status == kTrackFailed) A.info[M3S_INFO_SOLVE_FAIL] = 1;
+    if (status == 3) A.info[M3S_INFO_SOLVE_FAIL] = 2;
+    if (status == kTrackConverged) A.info[M3S_INFO_CONVERGED] = 1;
+    store_sim3(st->T_rel, T);
+    store_sim3(A.T_CkCf_out, T);
+    store_sim3(A.T_WCf_out, compose(Tk, T));
+  }
+}
+
+// pixels per lane of the persistent tracker (1, 2, 4) so that the grid fits
+// one workgroup per CU; 0: too large (one launch per iteration instead)
+int track_ppl(int64_t HW) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  const int64_t G = std::min<int64_t>(cus, kTrkMaxBlocks);
+  for (int ppl : {1, 2, 4})
+    if (HW <= G * kTrkThreads * ppl) return ppl;
+  return 0;
+}
+// M3S_TRACK_PERSISTENT=0: one launch per iteration (A/B of the persistent kernel)
+bool track_persistent_enabled() {
+  const char *e = std::getenv("M3S_TRACK_PERSISTENT");
+  return !(e && e[0] == '0');
 }
 
 int track_impl(const m3s_track_args *a, int mode, void *stream) {
@@ -3229,8 +3560,10 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   int rc;
   if (mode == M3S_MODE_CALIB && (rc = read_K(a->K, P, st))) return rc;
   TrackState *ts = at<TrackState>(a->workspace, kTrackStateOff);
-  float *partials = at<float>(a->workspace, track_partials_off());
-  track_init_kernel<<<1, 64, 0, st>>>(a->T_WCf, a->T_WCk, ts, a->info, a->T_WCf_out, a->T_CkCf_out);
+  TrackSync *sync = at<TrackSync>(a->workspace, track_sync_off());
+  float *partials = at<float>(a->workspace, track_part_off());
+  track_init_kernel<<<1, 64, 0, st>>>(a->T_WCf, a->T_WCk, ts, a->info, a->T_WCf_out, a->T_CkCf_out,
+                                      reinterpret_cast<uint32_t *>(sync), (int)(sizeof(TrackSync) / 4));
   if ((rc = launch_ok())) return rc;
   LinArgs L;
   memset(&L, 0, sizeof L);
@@ -3252,6 +3585,22 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   L.rel_error = a->rel_error, L.delta_norm = a->delta_norm;
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xf, 16) && vec_ok(a->Xk, 16) && vec_ok(a->Qk, 16) &&
                    vec_ok(a->valid, 4);
+  // persistent: every iteration in one launch (one workgroup per CU)
+  const int ppl = track_ppl(a->HW);
+  if (ppl > 0 && track_persistent_enabled()) {
+    if (a->max_iters < 1) return M3S_OK;
+    const int G = (int)((a->HW + (int64_t)kTrkThreads * ppl - 1) / ((int64_t)kTrkThreads * ppl));
+    if (mode == M3S_MODE_RAYS) {
+      if (ppl == 1) track_persistent_kernel<M3S_MODE_RAYS, 1><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+      else if (ppl == 2) track_persistent_kernel<M3S_MODE_RAYS, 2><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+      else track_persistent_kernel<M3S_MODE_RAYS, 4><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+    } else {
+      if (ppl == 1) track_persistent_kernel<M3S_MODE_CALIB, 1><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+      else if (ppl == 2) track_persistent_kernel<M3S_MODE_CALIB, 2><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+      else track_persistent_kernel<M3S_MODE_CALIB, 4><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+    }
+    return launch_ok();
+  }
   for (int it = 0; it < a->max_iters; it++) {
     if ((rc = dispatch_linearize<true>(mode, L, L.chunks, vec, 0, st))) return rc;
     if (a->sync_every > 0 && (it + 1) % a->sync_every == 0 && it + 1 < a->max_iters) {
@@ -3316,7 +3665,8 @@ int m3s_gn_release(const m3s_gn_args *a, void *stream) {
 
 size_t m3s_track_workspace_size(int64_t HW) {
   const int64_t chunks = chunks_for(HW, 1);
-  return track_partials_off() + align_up(sizeof(float) * kNP * (size_t)(chunks + 1), 256);
+  const size_t parts = std::max<size_t>((size_t)(chunks + 1), 2 * (size_t)kTrkMaxBlocks);
+  return track_part_off() + align_up(sizeof(float) * kNP * parts, 256);
 }
 
 int m3s_track_rays_sim3(const m3s_track_args *a, void *stream) { return track_impl(a, M3S_MODE_RAYS, stream); }
@@ -3346,6 +3696,18 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
   const int64_t n = (int64_t)I.data.size();
   if (out && cap >= n) std::copy(I.data.begin(), I.data.end(), out);
   return n;
+}
+
+// phase stamps of the last persistent tracker launch (M3S_TRK_STAMPS builds
+// only; returns 0 otherwise): [2 workgroups][16 iterations][8 phases]
+int m3s_track_stamps_debug(int64_t *out) {
+#ifdef M3S_TRK_STAMPS
+  if (hipDeviceSynchronize() != hipSuccess) return M3S_ELAUNCH;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trk_stamp), sizeof(g_trk_stamp)) == hipSuccess ? 1 : M3S_ELAUNCH;
+#else
+  (void)out;
+  return 0;
+#endif
 }
 
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs) {

@@ -119,18 +119,18 @@ EXPORTS = (
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve", "m3s_gn_release",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
-    "m3s_fuse_pointmap", "m3s_prep_rays",
+    "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_track_stamps_debug",
 )
 FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2}
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    if not os.path.exists(path):
         raise ImportError(
-            f"mast3r_slam_backends: {LIB_PATH} is missing; build it with "
+            f"mast3r_slam_backends: {path} is missing; build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)"
         )
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     P = ctypes.POINTER
     lib.m3s_gn_workspace_size.restype = ctypes.c_size_t
     lib.m3s_gn_workspace_size.argtypes = [ctypes.c_int64] * 3
@@ -162,6 +162,8 @@ def _load():
     lib.m3s_iter_proj.argtypes = [P(IterProjArgs), _VP]
     lib.m3s_refine_matches.restype = ctypes.c_int
     lib.m3s_refine_matches.argtypes = [P(RefineArgs), _VP]
+    lib.m3s_track_stamps_debug.restype = ctypes.c_int
+    lib.m3s_track_stamps_debug.argtypes = [_VP]
     lib.m3s_gn_layout_debug.restype = ctypes.c_size_t
     lib.m3s_gn_layout_debug.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP]
     return lib

@@ -168,10 +168,11 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
  * order flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk,
  * Dinv, tail, tasks, planes, total (offs[15]). Returns the total. */
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs);
-/* phase stamps of the last persistent tracker launch ([2][16][8] wall-clock
- * ticks of workgroups 0 and G-1), 1 in builds with -DM3S_TRK_STAMPS, else 0
- * (tools/trk_stamps.py) */
-int m3s_track_stamps_debug(int64_t *out);
+/* instrumented builds only: which = 0 persistent-tracker phase stamps
+ * [2][16][8] (-DM3S_TRK_STAMPS), 1 column-task stamps [2][512][4]
+ * (-DM3S_COL_STAMPS); wall-clock ticks. 1 if present, 0 otherwise
+ * (tools/trk_stamps.py, tools/col_stamps.py) */
+int m3s_debug_stamps(int which, int64_t *out);
 
 #ifdef __cplusplus
 }

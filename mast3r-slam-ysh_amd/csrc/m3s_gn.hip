@@ -145,8 +145,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 7 * (size_t)(m + 1), 256);
   L.parts = off;  // split update partials, at most slot_cap of them
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
-  L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets (epoch-tagged, zeroed per call)
-  off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16), 256);
+  L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap] (epoch-tagged, zeroed per call)
+  off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16 + L.slot_cap), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
   off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
   L.tasks = off;
@@ -1450,7 +1450,7 @@ __device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7]
 // lower triangle): the updates from the sparse columns p < c0, and for a
 // diagonal block also the tail RHS. Tasks are independent (used in
 // sparse_llt_kernel and, spread over the chip, by border_kernel).
-template <bool STAGE>
+template <bool STAGE, bool SC1 = false>
 __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t *pl, const int *off, double *Lb,
                                             double *y, int r7, int c7, int lane49, int lane, int lane7, bool act49,
                                             double *stg, double *Ad = nullptr, int ld = 0) {
@@ -1464,9 +1464,9 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
   if (ri == ci) {
     const int q0 = dtr_ptr[k], q1 = bend[ci * nc + ci];
     double v = Lb[(size_t)k * 49 + lane49];
-    v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+    v = sub_products<STAGE, true, SC1>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
     double bb = y[k * 7 + lane7];
-    bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
+    bb = sub_matvec<STAGE, false, SC1>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
     if (act49) Lb[(size_t)k * 49 + lane] = v;
     if (lane < 7) y[k * 7 + lane] = bb;
     if (Ad && act49) Ad[(size_t)(7 * ci + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
@@ -1474,7 +1474,7 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
     const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
     const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
     double v = Lb[(size_t)dst * 49 + lane49];
-    v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+    v = sub_products<STAGE, false, SC1>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
     if (act49) Lb[(size_t)dst * 49 + lane] = v;
     if (Ad && act49) {  // the block and its transpose (tail_llt_kernel reads whole 16x16 tiles)
       Ad[(size_t)(7 * ri + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
@@ -1912,6 +1912,17 @@ struct ColArgs {
   float delta_thresh;
 };
 constexpr int kColSpins = 1 << 20;  // bounded waits: a plan bug becomes a solve failure, never a hang
+#ifdef M3S_COL_STAMPS  // per-column wall-clock stamps (tools/col_stamps.py)
+__device__ int64_t g_col_stamp[2][512][4];
+#define M3S_CSTAMP(ph, k, i)                                \
+  do {                                                      \
+    if ((k) < 512) g_col_stamp[ph][k][i] = wall_clock64(); \
+  } while (0)
+#else
+#define M3S_CSTAMP(ph, k, i) \
+  do {                       \
+  } while (0)
+#endif
 __device__ __forceinline__ void set_fail(int32_t *flags) {
   __hip_atomic_store(flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1970,8 +1981,10 @@ __global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
     if (t >= C.ncols) break;
     const int k = corder[t];
     const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
+    if (tid == 0) M3S_CSTAMP(0, k, 0);
     if (wave == 0) {
       if (!wait_flags(C.done, dtr_p, q0, q1, C.m, C.epoch + 1, lane) && lane == 0) set_fail(C.flags);
+      if (lane == 0) M3S_CSTAMP(0, k, 1);
       // DIAG(k): the assembled D_k (previous launch: plain load) minus the
       // updates from the columns p (this launch: sc1)
       double v = L[(size_t)k * 49 + lane49];
@@ -1983,6 +1996,7 @@ __global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
       fwd_solve_store<true>(bb, Lr, dinv, C.y + (size_t)k * 7, lane);
     }
     __syncthreads();  // W_k in LDS; the dependencies are final for every wave
+    if (tid == 0) M3S_CSTAMP(0, k, 2);
     // OFF(i, k) for the |struct(k)| tasks of column k, one per wave
     const int tc0 = ctask0[k], ntask = col_ptr[k + 1] - col_ptr[k];
     for (int tt = wave; tt < ntask; tt += 4) {
@@ -2001,6 +2015,118 @@ __global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every sc1 store of column k has left
     __syncthreads();
     if (tid == 0) __hip_atomic_store(C.done + k, C.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) M3S_CSTAMP(0, k, 3);
+  }
+}
+
+// ------------------------------------ wave-level dataflow factorisation --
+// Large graphs: every block of the sparse columns' factor is its own work
+// item on one wave, dispatched over the whole chip from one ticket counter in
+// a topological order (level order; DIAG(k) before the OFF tasks of column k;
+// the dense-tail border tasks last):
+//   DIAG(k)    D_k - sum_p L_kp L_kp^T -> L_kk, W_k = L_kk^-1, y_k; waits for
+//              the slots L_kp of its update list (dtr);
+//   OFF(t)     L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T; waits for DIAG(k) and
+//              the slots of its update list (tr_a / tr_b);
+//   BORDER(b)  one dense-tail block minus its updates from the sparse columns
+//              (and the tail RHS), written to the factor and densely for
+//              tail_llt_kernel; waits for the slots of its update prefix.
+// Every block slot has an epoch flag (diagonal slots = DIAG done, which also
+// covers y_k); a finished block is published with write-through (sc1) stores
+// drained before the flag, and read with sc1 loads. A wave waits only for
+// items with smaller tickets (all dispatched to running waves earlier), so
+// progress does not depend on residency. The columns' OFF tasks no longer
+// queue behind one workgroup's 4 waves: the top of the elimination tree (33
+// OFF blocks in one column at 256 KFs) runs its blocks side by side.
+// (SimplicialLLT's factor, gn_kernels.cu:132-153.)
+struct DfArgs {
+  const int32_t *plan;
+  int off[kPlanSections];
+  const int32_t *items;  // dispatch list: -1-k DIAG(k), t < n_tasks OFF(t), n_tasks + b BORDER(b)
+  int n_items, n_tasks, m, c0, nc, epoch;
+  double *L, *Dinv, *y;
+  int32_t *sdone;  // [S] slot epoch flags
+  int32_t *ctr;    // ticket counter
+  int32_t *flags;
+  double *tail_A;
+  int tail_ld;
+};
+constexpr int kDfWaves = 4;
+
+__global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
+  if (D.flags[kFlagStop]) return;
+  __shared__ __attribute__((aligned(16))) double stage[kDfWaves][kStageDoubles];
+  __shared__ double scratch[kDfWaves][64];
+  __shared__ double Wsh[kDfWaves][49];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int32_t *pl = D.plan;
+  const int32_t *dtr_ptr = pl + D.off[6], *dtr_slot = pl + D.off[7], *dtr_p = pl + D.off[8],
+                *task_dst = pl + D.off[10], *task_col = pl + D.off[11], *task_tr_ptr = pl + D.off[12],
+                *tr_a = pl + D.off[13], *tr_b = pl + D.off[14];
+  const int32_t *clq = pl + D.off[28];
+  const int r = lane / 7, c = lane % 7;
+  const bool act49 = lane < 49;
+  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
+  const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
+  double *stg = stage[wave], *scr = scratch[wave], *W = Wsh[wave];
+  const int want = D.epoch + 1;
+  const int base = D.epoch * (D.n_items + (int)gridDim.x * kDfWaves);  // tickets of earlier launches
+  double *L = D.L;
+  const int BIG = 1 << 30;
+  for (;;) {
+    const int t = wave_gticket(D.ctr) - base;
+    if (t >= D.n_items) break;
+    const int code = D.items[t];
+    if (code < 0) {  // DIAG(k)
+      const int k = -1 - code;
+      const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
+      if (!wait_flags(D.sdone, dtr_slot, q0, q1, BIG, want, lane) && lane == 0) set_fail(D.flags);
+      double v = L[(size_t)k * 49 + lane49];  // assembled by the previous launch
+      v = sub_products<true, true, true>(v, L, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+      double Lr[7][7], dinv[7];
+      if (diag_factor<true>(v, k, L, D.Dinv, scr, lane, l7, Lr, dinv) && lane == 0) set_fail(D.flags);
+      double bb = D.y[(size_t)k * 7 + lane7];
+      bb = sub_matvec<true, false, true>(bb, L, dtr_slot, dtr_p, q0, q1, D.y, lane7, lane49, lane, stg);
+      fwd_solve_store<true>(bb, Lr, dinv, D.y + (size_t)k * 7, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(D.sdone + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (code < D.n_tasks) {  // OFF(t)
+      const int dst = task_dst[code], k = task_col[code];
+      const int q0 = task_tr_ptr[code], q1 = task_tr_ptr[code + 1];
+      bool ok = wait_flags(D.sdone, task_col, code, code + 1, BIG, want, lane);  // DIAG(k)
+      ok &= wait_flags(D.sdone, tr_a, q0, q1, BIG, want, lane);
+      ok &= wait_flags(D.sdone, tr_b, q0, q1, BIG, want, lane);
+      if (!ok && lane == 0) set_fail(D.flags);
+      if (act49) W[lane] = ld_sc1(D.Dinv + (size_t)k * 49 + lane);
+      double v = L[(size_t)dst * 49 + lane49];
+      v = sub_products<true, false, true>(v, L, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      double x = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * W[c7 + mm];
+      if (act49) st_sc1(L + (size_t)dst * 49 + lane, x);
+      wave_lds_fence();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(D.sdone + dst, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {  // BORDER(b): waits for its update prefix, then border_task (sc1 reads)
+      const int bt = code - D.n_tasks, nc = D.nc;
+      const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
+      int ci = 0, rem = bt;
+      while (rem >= nc - ci) rem -= nc - ci, ci++;
+      const int ri = ci + rem, k = D.c0 + ci;
+      bool ok;
+      if (ri == ci) {
+        ok = wait_flags(D.sdone, dtr_slot, dtr_ptr[k], bend[ci * nc + ci], BIG, want, lane);
+      } else {
+        const int task = ct0[ci] + ri - ci - 1;
+        const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
+        ok = wait_flags(D.sdone, tr_a, q0, q1, BIG, want, lane) && wait_flags(D.sdone, tr_b, q0, q1, BIG, want, lane);
+      }
+      if (!ok && lane == 0) set_fail(D.flags);
+      border_task<true, true>(bt, nc, D.c0, pl, D.off, L, D.y, r7, c7, lane49, lane, lane7, act49, stg, D.tail_A,
+                              D.tail_ld);
+    }
   }
 }
 
@@ -2070,7 +2196,9 @@ __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
     if (t >= C.ncols) break;
     const int k = corder[C.ncols - 1 - t];
     const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
+    if (lane == 0) M3S_CSTAMP(1, k, 0);
     if (!wait_flags(C.done2, col_row, q0, q1, C.c0, C.epoch + 1, lane) && lane == 0) set_fail(C.flags);
+    if (lane == 0) M3S_CSTAMP(1, k, 1);
     double rr = C.y[(size_t)k * 7 + lane7];
     rr = sub_matvec<true, true, true>(rr, C.L, col_slot, col_row, q0, q1, C.y, lane7, lane49, lane, stage);
     double xk = 0.0;
@@ -2079,6 +2207,7 @@ __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
     if (lane < 7) st_sc1(C.y + (size_t)k * 7 + lane, xk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(C.done2 + k, C.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) M3S_CSTAMP(1, k, 2);
     // the workgroup that finishes the last column finishes the step
     const int fin = wave_gticket(C.ctr + 2);
     if (fin - C.epoch * C.ncols == C.ncols - 1) {
@@ -2597,6 +2726,11 @@ inline bool cols_path() {  // M3S_COLS=0: large graphs on sparse_llt_kernel's on
   return !(e && e[0] == '0');
 }
 
+inline bool df_path() {  // M3S_DF=0: column tasks + border_kernel instead of the block dataflow (A/B)
+  const char *e = std::getenv("M3S_DF");
+  return !(e && e[0] == '0');
+}
+
 inline bool tail_mfma() {  // M3S_TAIL_MFMA=0: the dense tail in sparse_llt_kernel (A/B)
   const char *e = std::getenv("M3S_TAIL_MFMA");
   return !(e && e[0] == '0');
@@ -2619,6 +2753,7 @@ struct PlanMeta {
   bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
   size_t lds_bytes = 0;
   int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0, nc = 0;
+  int off_dfitems = 0, n_dfitems = 0;  // df_factor_kernel dispatch list (appended to the plan image)
   PlanImage img;  // offsets (data vector cleared after upload)
   // linearize state of this solve call: edge ranks, the task table of the
   // edge range last linearized (host copy stays alive for the async upload)
@@ -2826,16 +2961,41 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       C.dx_out = dx;
       C.N = a->N;
       C.delta_thresh = a->delta_thresh;
-      const int g1 = std::max(1, std::min(C.ncols, 256));
-      col_factor_kernel<<<g1, 256, 0, st>>>(C);
+      double *tail = at<double>(ws, Ly.tail);
+      const int tld = 16 * kTailMaxT;
+      if (df_path()) {
+        // every block of the sparse columns and the tail border: one wave-level dataflow
+        DfArgs F;
+        F.plan = D.plan;
+        for (int q = 0; q < kPlanSections; q++) F.off[q] = D.off[q];
+        F.items = D.plan + meta.off_dfitems;
+        F.n_items = meta.n_dfitems;
+        F.n_tasks = meta.n_tasks;
+        F.m = meta.m;
+        F.c0 = C.c0;
+        F.nc = meta.nc;
+        F.epoch = meta.epoch;
+        F.L = D.L;
+        F.Dinv = D.Dinv;
+        F.y = C.y;
+        F.sdone = cs + 2 * (meta.m + 1) + 16;
+        F.ctr = C.ctr + 3;
+        F.flags = flags;
+        F.tail_A = tail;
+        F.tail_ld = tld;
+        const int nw = std::max(1, std::min(F.n_items, 1024));
+        df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
+      } else {
+        const int g1 = std::max(1, std::min(C.ncols, 256));
+        col_factor_kernel<<<g1, 256, 0, st>>>(C);
+      }
       if (meta.nc > 0) {
-        double *tail = at<double>(ws, Ly.tail);
-        const int tld = 16 * kTailMaxT;
         D.tail_A = tail;
         D.tail_ld = tld;
         const int nt0 = meta.nc * (meta.nc + 1) / 2;
-        border_kernel<<<(nt0 + kBorderWaves - 1) / kBorderWaves, 64 * kBorderWaves,
-                        kBorderWaves * kStageDoubles * sizeof(double), st>>>(D);
+        if (!df_path())
+          border_kernel<<<(nt0 + kBorderWaves - 1) / kBorderWaves, 64 * kBorderWaves,
+                          kBorderWaves * kStageDoubles * sizeof(double), st>>>(D);
         TailArgs T;
         T.Ad = tail;
         T.ld = tld;
@@ -2984,6 +3144,15 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1, dense_tail_min());
     PlanImage img;
     flatten_plan(P, img);
+    // df_factor_kernel's dispatch list: the sparse columns in level order,
+    // DIAG(k) then the OFF tasks of column k, then the dense-tail border tasks
+    meta.off_dfitems = (int)img.data.size();
+    for (int32_t k : P.corder) {
+      img.data.push_back(-1 - k);
+      for (int q = 0; q < P.col_ptr[k + 1] - P.col_ptr[k]; q++) img.data.push_back(P.ctask0[k] + q);
+    }
+    for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
+    meta.n_dfitems = (int)img.data.size() - meta.off_dfitems;
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
     if (fits && !force_dense) {
       meta.sparse = true;
@@ -3698,16 +3867,23 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
   return n;
 }
 
-// phase stamps of the last persistent tracker launch (M3S_TRK_STAMPS builds
-// only; returns 0 otherwise): [2 workgroups][16 iterations][8 phases]
-int m3s_track_stamps_debug(int64_t *out) {
-#ifdef M3S_TRK_STAMPS
+// Instrumented builds only (tools/trk_stamps.py, tools/col_stamps.py):
+// which = 0: persistent tracker phase stamps [2][16][8] (-DM3S_TRK_STAMPS);
+// which = 1: column-task stamps [2][512][4] (-DM3S_COL_STAMPS). Wall-clock
+// ticks (100 MHz). Returns 1, or 0 when the build has no such stamps.
+int m3s_debug_stamps(int which, int64_t *out) {
   if (hipDeviceSynchronize() != hipSuccess) return M3S_ELAUNCH;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trk_stamp), sizeof(g_trk_stamp)) == hipSuccess ? 1 : M3S_ELAUNCH;
-#else
+#ifdef M3S_TRK_STAMPS
+  if (which == 0)
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trk_stamp), sizeof(g_trk_stamp)) == hipSuccess ? 1 : M3S_ELAUNCH;
+#endif
+#ifdef M3S_COL_STAMPS
+  if (which == 1)
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_col_stamp), sizeof(g_col_stamp)) == hipSuccess ? 1 : M3S_ELAUNCH;
+#endif
+  (void)which;
   (void)out;
   return 0;
-#endif
 }
 
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs) {

@@ -119,7 +119,7 @@ EXPORTS = (
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve", "m3s_gn_release",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
-    "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_track_stamps_debug",
+    "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_debug_stamps",
 )
 FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2}
 
@@ -162,8 +162,8 @@ def _load(path=LIB_PATH):
     lib.m3s_iter_proj.argtypes = [P(IterProjArgs), _VP]
     lib.m3s_refine_matches.restype = ctypes.c_int
     lib.m3s_refine_matches.argtypes = [P(RefineArgs), _VP]
-    lib.m3s_track_stamps_debug.restype = ctypes.c_int
-    lib.m3s_track_stamps_debug.argtypes = [_VP]
+    lib.m3s_debug_stamps.restype = ctypes.c_int
+    lib.m3s_debug_stamps.argtypes = [ctypes.c_int, _VP]
     lib.m3s_gn_layout_debug.restype = ctypes.c_size_t
     lib.m3s_gn_layout_debug.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP]
     return lib

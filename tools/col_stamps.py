@@ -1,0 +1,73 @@
+"""Per-column timing of the large-graph solve (library built with
+-DM3S_COL_STAMPS [-DM3S_TAIL_STAMPS], tools/mkvar.sh): one stepwise GN
+iteration of an N-keyframe rays graph (64x64 pixels: the solve does not depend
+on the image size), then per elimination-tree level of the sparse columns the
+spread of (ticket -> dependencies ready -> DIAG done -> column published) in
+us from the first column's ticket, and the back-substitution likewise.
+
+usage: N=256 python tools/col_stamps.py variants/lib_colst.so"""
+import os
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mast3r-slam-ysh_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mast3r_slam_backends as be  # noqa: E402
+
+be._lib = be._load(os.path.abspath(sys.argv[1]))
+from mast3r_slam_amd import synthetic  # noqa: E402
+from mast3r_slam_amd.distributed import HipOps  # noqa: E402
+
+N = int(os.environ.get("N", "256"))
+dev = torch.device("cuda:0")
+g = synthetic.make_graph(N, 64, 64, seed=1003, device=dev)
+Twc = g.T_init.data.clone().contiguous()
+E = g.n_edges
+ops = HipOps(be.MODE_RAYS, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q, E, None,
+             sigma_a=0.003, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5)
+es = torch.zeros(E, 36, dtype=torch.float64, device=dev)
+for rep in range(3):
+    ops.prepare(0.0)
+    ops.linearize(0, E, es)
+    torch.cuda.synchronize()
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record()
+    ops.solve(es)
+    s1.record()
+    torch.cuda.synchronize()
+print(f"N={N}: solve {s0.elapsed_time(s1) * 1e3:.1f} us (HIP events, last rep)")
+st = np.zeros((2, 512, 4), np.int64)
+assert be._lib.m3s_debug_stamps(1, st.ctypes.data_as(__import__("ctypes").c_void_p)) == 1
+ri = np.unique(np.concatenate([g.ii.cpu().numpy(), g.jj.cpu().numpy()]), return_inverse=True)[1].reshape(2, -1)
+p = be.sparse_plan(N, ri[0], ri[1], split=32)
+m, nc = p["m"], p["nc"]
+c0 = m - nc
+cols = np.arange(c0)
+parent = np.full(m, -1)
+for k in range(m):
+    rows = p["col_row"][p["col_ptr"][k]:p["col_ptr"][k + 1]]
+    if len(rows):
+        parent[k] = rows.min()
+lev = np.zeros(m, int)
+for k in range(m):
+    if parent[k] >= 0:
+        lev[parent[k]] = max(lev[parent[k]], lev[k] + 1)
+F = st[0, :c0]
+t0 = F[:, 0].min()
+us = lambda x: (x - t0) / 100.0  # noqa: E731
+print(f"sparse columns {c0}, tail columns {nc}; factor: first ticket -> last publish {us(F[:, 3].max()):.1f} us")
+print("level  cols   ticket(min/max)   ready(max)   diag(max)   publish(min/max)   per-column ready->publish (mean)")
+for L in range(lev[:c0].max() + 1):
+    ks = cols[lev[:c0] == L]
+    if not len(ks):
+        continue
+    f = F[ks]
+    print(f"{L:5d} {len(ks):5d}   {us(f[:, 0].min()):7.1f}/{us(f[:, 0].max()):7.1f}   {us(f[:, 1].max()):9.1f}"
+          f"   {us(f[:, 2].max()):9.1f}   {us(f[:, 3].min()):7.1f}/{us(f[:, 3].max()):7.1f}"
+          f"   {((f[:, 3] - f[:, 1]) / 100.0).mean():8.2f}")
+B = st[1, :c0]
+tb = B[:, 0].min()
+print(f"back-substitution: first ticket -> last x {((B[:, 2].max() - tb) / 100.0):.1f} us; per column ready->done "
+      f"mean {((B[:, 2] - B[:, 1]) / 100.0).mean():.2f} us; wait (ticket->ready) max {((B[:, 1] - B[:, 0]) / 100.0).max():.1f} us")

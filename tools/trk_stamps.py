@@ -29,7 +29,7 @@ for _ in range(5):
     be.track_rays_sim3(*a, 0.003, 10.0, 1.345, 10, 0.0, 0.0, sync_every=0)
 torch.cuda.synchronize()
 st = np.zeros((2, 16, 8), np.int64)
-assert lib.m3s_track_stamps_debug(st.ctypes.data_as(ctypes.c_void_p)) == 1
+assert lib.m3s_debug_stamps(0, st.ctypes.data_as(ctypes.c_void_p)) == 1
 t0 = st[0, 0, 0]
 for w in range(2):
     print("workgroup", "0" if w == 0 else "G-1")

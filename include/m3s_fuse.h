@@ -27,6 +27,8 @@ extern "C" {
 #define M3S_FILTER_WEIGHTED_POINTMAP 0 /* frame.py:73-76 (config default) */
 #define M3S_FILTER_INDEP_CONF 1        /* frame.py:68-72                  */
 #define M3S_FILTER_RECENT 2            /* frame.py:59-62: overwrite       */
+#define M3S_FILTER_WEIGHTED_SPHERICAL 3 /* frame.py:78-100: confidence-weighted
+                                           mean of (r, phi, theta)          */
 
 typedef struct m3s_fuse_args {
   float *X_canon;      /* [HW, 3] keyframe canonical pointmap, updated in place */

@@ -12,6 +12,7 @@
  *   Cs         float  [N, HW]     (the reference's [N, HW, 1]) average conf
  *   ii, jj     int64  [E]         global keyframe ids of each directed edge
  *   idx_ii2jj  int64  [E, HW]     pixel of KF ii matched to pixel k of KF jj
+ *                                 (int32 when idx_i32 = 1)
  *   valid_match uint8 [E, HW]     (torch.bool, [E, HW, 1] in the reference)
  *   Q          float  [E, HW]     match quality
  *   K          float  [3, 3]      calib only
@@ -79,6 +80,10 @@ typedef struct m3s_gn_args {
   int32_t *info;  /* [8] int32 device */
   void *workspace;
   size_t workspace_bytes;
+  /* 0: idx_ii2jj is the reference's int64 [E, HW]; 1: it holds int32 (the
+   * device edge store of mast3r_slam_amd.factor_graph: 4 B less per edge
+   * pixel on the first GN iteration's reads) */
+  int idx_i32;
 } m3s_gn_args;
 
 /* Bytes of scratch the GN entry points need for this problem size. */
@@ -169,7 +174,7 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
  * Dinv, tail, tasks, planes, total (offs[15]). Returns the total. */
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs);
 /* instrumented builds only: which = 0 persistent-tracker phase stamps
- * [2][16][8] (-DM3S_TRK_STAMPS), 1 column-task stamps [2][512][4]
+ * [2][16][8] (-DM3S_TRK_STAMPS), 1 column-task stamps [4][2048][4]
  * (-DM3S_COL_STAMPS); wall-clock ticks. 1 if present, 0 otherwise
  * (tools/trk_stamps.py, tools/col_stamps.py) */
 int m3s_debug_stamps(int which, int64_t *out);

@@ -49,6 +49,27 @@ __global__ void __launch_bounds__(kFuseThreads) fuse_pointmap_kernel(m3s_fuse_ar
       xc[0] = x[0], xc[1] = x[1], xc[2] = x[2];
       A.C[p] = cn;
     }
+  } else if (A.mode == M3S_FILTER_WEIGHTED_SPHERICAL) {  // frame.py:78-100
+    // cartesian_to_spherical: r = ||P||, phi = atan2(y, x), theta = acos(z / r)
+    float so[3], sn[3];
+    {
+      const float r = sqrtf(xc[0] * xc[0] + xc[1] * xc[1] + xc[2] * xc[2]);
+      so[0] = r, so[1] = atan2f(xc[1], xc[0]), so[2] = acosf(xc[2] / r);
+    }
+    {
+      const float r = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+      sn[0] = r, sn[1] = atan2f(x[1], x[0]), sn[2] = acosf(x[2] / r);
+    }
+    const float den = co + cn;
+    float sp[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) sp[k] = ((co * so[k]) + (cn * sn[k])) / den;
+    // spherical_to_cartesian
+    const float st = sinf(sp[2]);
+    xc[0] = sp[0] * st * cosf(sp[1]);
+    xc[1] = sp[0] * st * sinf(sp[1]);
+    xc[2] = sp[0] * cosf(sp[2]);
+    A.C[p] = co + cn;
   } else {  // recent (frame.py:59-62)
     xc[0] = x[0], xc[1] = x[1], xc[2] = x[2];
     A.C[p] = cn;
@@ -108,7 +129,7 @@ extern "C" {
 
 int m3s_fuse_pointmap(const m3s_fuse_args *a, void *stream) {
   if (!a || !a->X_canon || !a->C || !a->X_new || !a->C_new || a->HW < 0) return M3S_EINVAL;
-  if (a->mode < 0 || a->mode > M3S_FILTER_RECENT) return M3S_EINVAL;
+  if (a->mode < 0 || a->mode > M3S_FILTER_WEIGHTED_SPHERICAL) return M3S_EINVAL;
   if (a->HW == 0) return M3S_OK;
   const unsigned blocks = (unsigned)((a->HW + kFuseThreads - 1) / kFuseThreads);
   fuse_pointmap_kernel<<<blocks, kFuseThreads, 0, static_cast<hipStream_t>(stream)>>>(*a);

@@ -90,9 +90,9 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 // rows (n + 1 <= 16 kTailMaxT) and its scratch (dense bordered tail, L tiles,
 // W_k); see the kernel
 constexpr int kTailMaxT = 32;
-inline size_t tail_scratch_doubles() {
+inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cyc_kernel)
   const size_t nmax = 16 * kTailMaxT;
-  return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 + (size_t)kTailMaxT * 256;
+  return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2 + (size_t)kTailMaxT * 256 + nmax;
 }
 
 struct Layout {
@@ -146,7 +146,7 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   L.parts = off;  // split update partials, at most slot_cap of them
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap] (epoch-tagged, zeroed per call)
-  off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16 + L.slot_cap), 256);
+  off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
   off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
   L.tasks = off;
@@ -183,6 +183,7 @@ struct LinArgs {
   const float *Cs;
   const float *Xsrc;       // tracker: Xf (source points); backend: unused
   const int64_t *idx;
+  int idx32;  // idx holds int32 (m3s_gn_args.idx_i32)
   const uint8_t *valid;
   const float *Q;
   const int32_t *rank_i;
@@ -467,6 +468,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   // edge data (idx/valid/Q) is addressed relative to the launch's edge slice
   const size_t eoff = TRACK ? 0 : (size_t)e_loc * HW;
   const int64_t *__restrict__ idx = TRACK ? nullptr : A.idx + eoff;
+  const int32_t *__restrict__ idx32 = TRACK ? nullptr : reinterpret_cast<const int32_t *>(A.idx) + eoff;
   const uint8_t *__restrict__ valid = A.valid + eoff;
   const float *__restrict__ Qe = A.Q + eoff;
   constexpr int NPL = PixIn<MODE>::kPlanes;
@@ -487,9 +489,15 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
       const f32x4 q4 = ld_stream(reinterpret_cast<const f32x4 *>(Qe + p0));
       int64_t ids[4] = {0, 0, 0, 0};
       if (!TRACK) {
-        const i64x2 i01 = ld_stream(reinterpret_cast<const i64x2 *>(idx + p0));
-        const i64x2 i23 = ld_stream(reinterpret_cast<const i64x2 *>(idx + p0 + 2));
-        ids[0] = i01.x, ids[1] = i01.y, ids[2] = i23.x, ids[3] = i23.y;
+        if (A.idx32) {  // uniform branch: 16 B of int32 ids
+          typedef int i32x4 __attribute__((ext_vector_type(4)));
+          const i32x4 i4 = ld_stream(reinterpret_cast<const i32x4 *>(idx32 + p0));
+          ids[0] = i4.x, ids[1] = i4.y, ids[2] = i4.z, ids[3] = i4.w;
+        } else {
+          const i64x2 i01 = ld_stream(reinterpret_cast<const i64x2 *>(idx + p0));
+          const i64x2 i23 = ld_stream(reinterpret_cast<const i64x2 *>(idx + p0 + 2));
+          ids[0] = i01.x, ids[1] = i01.y, ids[2] = i23.x, ids[3] = i23.y;
+        }
       }
       const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * p0);
       const f32x4 xa = xj4[0], xb = xj4[1], xc = xj4[2];
@@ -518,7 +526,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   } else {
     for (int64_t p = p_begin + threadIdx.x; p < p_end; p += kThreads) {
       const bool vm = valid[p] != 0;
-      const int64_t id = TRACK ? p : idx[p];
+      const int64_t id = TRACK ? p : (A.idx32 ? (int64_t)idx32[p] : idx[p]);
       const float Xj[3] = {Xs_j[3 * p], Xs_j[3 * p + 1], Xs_j[3 * p + 2]};
       const float cj = TRACK ? 0.0f : Cs_j[p];
       const PixIn<MODE> in = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p, vm, id, Qe[p], cj);
@@ -1262,10 +1270,26 @@ __device__ __forceinline__ void st_blk(double *p, double v) {
 }
 
 // v -= sum_q A_q(r,:) . B_q(c,:)   (A_q = L[sa[q]], B_q = L[sb[q]], or B = A if SAME)
+// Wait until flag[idx] == want on every active lane (idx per lane), with
+// relaxed agent-scope (sc1) loads; bounded like wait_flags. false on timeout.
+__device__ __forceinline__ bool wait_lanes(const int32_t *flag, int idx, bool active, int want) {
+  int spins = 0;
+  for (;;) {
+    const bool ok = !active || __hip_atomic_load(flag + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want;
+    if (__ballot(!ok) == 0) return true;
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1 << 20)) return false;
+  }
+}
+
+// wflag (staged sc1 path only): wait for each batch's blocks (flag[slot] ==
+// want) just before loading them, so the sums of the blocks that are ready
+// early run while the later ones are still being produced; *ok &= no timeout
 template <bool STAGE, bool SAME, bool SC1 = false>
 __device__ __forceinline__ double sub_products(double v, const double *Lb, const int32_t *sa,
                                                const int32_t *sb, int q0, int q1, int r7, int c7,
-                                               int lane49, int lane, double *stg) {
+                                               int lane49, int lane, double *stg, const int32_t *wflag = nullptr,
+                                               int want = 0, bool *ok = nullptr) {
   if (!STAGE) {
     int q = q0;
     for (; q + 1 < q1; q += 2) {
@@ -1290,14 +1314,33 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
     return v;
   }
   double *SA = stg, *SB = SAME ? stg : stg + kStage * 49;
+  // the list's slot indices, 64 at a time, one per lane (one load round
+  // trip; then wave-uniform readlanes), so the block loads of a batch all
+  // issue at once instead of each waiting behind its own index load
+  int my_a = 0, my_b = 0;
   for (int q = q0; q < q1; q += kStage) {
+    if (((q - q0) & 63) == 0) {
+      my_a = q + lane < q1 ? sa[q + lane] : 0;
+      if (!SAME) my_b = q + lane < q1 ? sb[q + lane] : 0;
+    }
     const int nb = (q1 - q < kStage) ? q1 - q : kStage;
+    if (wflag) {
+      const int rel = lane - ((q - q0) & 63);
+      const bool act = rel >= 0 && rel < nb;
+      bool w = wait_lanes(wflag, my_a, act, want);
+      if (!SAME) w &= wait_lanes(wflag, my_b, act, want);
+      if (!w) *ok = false;
+    }
     double va[kStage], vb[kStage];
 #pragma unroll
     for (int bq = 0; bq < kStage; bq++) {
       if (bq < nb) {
-        va[bq] = ld_blk<SC1>(Lb + (size_t)sa[q + bq] * 49 + lane49);
-        if (!SAME) vb[bq] = ld_blk<SC1>(Lb + (size_t)sb[q + bq] * 49 + lane49);
+        const int ia = __builtin_amdgcn_readlane(my_a, ((q - q0) & 63) + bq);
+        va[bq] = ld_blk<SC1>(Lb + (size_t)ia * 49 + lane49);
+        if (!SAME) {
+          const int ib = __builtin_amdgcn_readlane(my_b, ((q - q0) & 63) + bq);
+          vb[bq] = ld_blk<SC1>(Lb + (size_t)ib * 49 + lane49);
+        }
       }
     }
     if (lane < 49) {
@@ -1337,14 +1380,20 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
     }
     return acc;
   }
+  int my_s = 0, my_v = 0;  // list indices per lane, 64 at a time (see sub_products)
   for (int q = q0; q < q1; q += kStage) {
+    if (((q - q0) & 63) == 0) {
+      my_s = q + lane < q1 ? slot[q + lane] : 0;
+      my_v = q + lane < q1 ? vidx[q + lane] : 0;
+    }
     const int nb = (q1 - q < kStage) ? q1 - q : kStage;
     double va[kStage], vy[kStage];
 #pragma unroll
     for (int bq = 0; bq < kStage; bq++)
       if (bq < nb) {
-        va[bq] = ld_blk<SC1>(Lb + (size_t)slot[q + bq] * 49 + lane49);
-        if (SC1) vy[bq] = ld_sc1(y + (size_t)vidx[q + bq] * 7 + lane7);  // y of other workgroups
+        const int is = __builtin_amdgcn_readlane(my_s, ((q - q0) & 63) + bq);
+        va[bq] = ld_blk<SC1>(Lb + (size_t)is * 49 + lane49);
+        if (SC1) vy[bq] = ld_sc1(y + (size_t)__builtin_amdgcn_readlane(my_v, ((q - q0) & 63) + bq) * 7 + lane7);
       }
     if (lane < 49) {
 #pragma unroll
@@ -1368,6 +1417,61 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
     wave_lds_fence();
   }
   return acc;
+}
+
+// DIAG(k)'s two update sums in one staged pass over its list (the blocks
+// L_kp are loaded once for both): v -= sum_q L_q(r,:) . L_q(c,:) (entry
+// layout) and bb -= sum_q L_q(l7,:) . y_{p_q} (row layout); per-block sums in
+// sub_products / sub_matvec order (bitwise the same results). sc1 loads.
+__device__ __forceinline__ void diag_updates_sc1(double &v, double &bb, const double *Lb, const int32_t *slot,
+                                                 const int32_t *vidx, int q0, int q1, const double *y, int r7,
+                                                 int c7, int lane7, int lane49, int lane, double *stg,
+                                                 const int32_t *wflag, int want, bool *ok) {
+  int my_s = 0, my_v = 0;  // list indices per lane, 64 at a time (see sub_products)
+  for (int q = q0; q < q1; q += kStage) {
+    if (((q - q0) & 63) == 0) {
+      my_s = q + lane < q1 ? slot[q + lane] : 0;
+      my_v = q + lane < q1 ? vidx[q + lane] : 0;
+    }
+    const int nb = (q1 - q < kStage) ? q1 - q : kStage;
+    {  // this batch's blocks L_kp (y_p is stored before L_kp can exist)
+      const int rel = lane - ((q - q0) & 63);
+      if (!wait_lanes(wflag, my_s, rel >= 0 && rel < nb, want)) *ok = false;
+    }
+    double va[kStage], vy[kStage];
+#pragma unroll
+    for (int bq = 0; bq < kStage; bq++)
+      if (bq < nb) {
+        const int is = __builtin_amdgcn_readlane(my_s, ((q - q0) & 63) + bq);
+        const int iv = __builtin_amdgcn_readlane(my_v, ((q - q0) & 63) + bq);
+        va[bq] = ld_sc1(Lb + (size_t)is * 49 + lane49);
+        vy[bq] = ld_sc1(y + (size_t)iv * 7 + lane7);
+      }
+    if (lane < 49) {
+#pragma unroll
+      for (int bq = 0; bq < kStage; bq++)
+        if (bq < nb) stg[bq * 49 + lane] = va[bq];
+    }
+    if (lane < 7) {
+#pragma unroll
+      for (int bq = 0; bq < kStage; bq++)
+        if (bq < nb) stg[kStage * 49 + bq * 7 + lane] = vy[bq];
+    }
+    wave_lds_fence();
+    for (int bq = 0; bq < nb; bq++) {
+      const double *A = stg + bq * 49;
+      double s0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) s0 += A[r7 + mm] * A[c7 + mm];
+      v -= s0;
+      const double *yv = stg + kStage * 49 + bq * 7;
+      double t0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) t0 += A[lane7 * 7 + mm] * yv[mm];
+      bb -= t0;
+    }
+    wave_lds_fence();
+  }
 }
 
 // One 1024-thread workgroup: assembly -> dataflow block LLT + forward
@@ -1913,10 +2017,10 @@ struct ColArgs {
 };
 constexpr int kColSpins = 1 << 20;  // bounded waits: a plan bug becomes a solve failure, never a hang
 #ifdef M3S_COL_STAMPS  // per-column wall-clock stamps (tools/col_stamps.py)
-__device__ int64_t g_col_stamp[2][512][4];
+__device__ int64_t g_col_stamp[4][2048][4];
 #define M3S_CSTAMP(ph, k, i)                                \
   do {                                                      \
-    if ((k) < 512) g_col_stamp[ph][k][i] = wall_clock64(); \
+    if ((k) < 2048) g_col_stamp[ph][k][i] = wall_clock64(); \
   } while (0)
 #else
 #define M3S_CSTAMP(ph, k, i) \
@@ -2070,36 +2174,53 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
   const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
   double *stg = stage[wave], *scr = scratch[wave], *W = Wsh[wave];
   const int want = D.epoch + 1;
-  const int base = D.epoch * (D.n_items + (int)gridDim.x * kDfWaves);  // tickets of earlier launches
+  // First round: wave g of the grid takes item g (no atomic: 1024 waves on
+  // one counter cost ~10 us of arrival skew); later rounds draw tickets from
+  // the counter. Every wave of this grid is resident at once (at most 1024
+  // waves of 28 KB-LDS workgroups: >= 4 per CU), so a wave only ever waits
+  // for items held by running waves. Draws per launch are fixed (the
+  // successful ones plus one failing draw per wave that reaches the
+  // counter), which gives the epoch base of the counter.
+  const int nW = (int)gridDim.x * kDfWaves, gw = (int)blockIdx.x * kDfWaves + wave;
+  const int draws = (D.n_items > nW ? D.n_items - nW : 0) + (D.n_items < nW ? D.n_items : nW);
+  const int base = D.epoch * draws;
   double *L = D.L;
   const int BIG = 1 << 30;
-  for (;;) {
-    const int t = wave_gticket(D.ctr) - base;
+  for (int round = 0;; round++) {
+    const int t = round == 0 ? gw : nW + wave_gticket(D.ctr) - base;
     if (t >= D.n_items) break;
     const int code = D.items[t];
     if (code < 0) {  // DIAG(k)
       const int k = -1 - code;
       const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
-      if (!wait_flags(D.sdone, dtr_slot, q0, q1, BIG, want, lane) && lane == 0) set_fail(D.flags);
+      if (lane == 0) M3S_CSTAMP(0, k, 0);
       double v = L[(size_t)k * 49 + lane49];  // assembled by the previous launch
-      v = sub_products<true, true, true>(v, L, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+      double bb = D.y[(size_t)k * 7 + lane7];
+      bool ok = true;  // the update list is waited for batch by batch
+      diag_updates_sc1(v, bb, L, dtr_slot, dtr_p, q0, q1, D.y, r7, c7, lane7, lane49, lane, stg, D.sdone, want, &ok);
+      if (!ok && lane == 0) set_fail(D.flags);
+      if (lane == 0) M3S_CSTAMP(0, k, 1);
       double Lr[7][7], dinv[7];
       if (diag_factor<true>(v, k, L, D.Dinv, scr, lane, l7, Lr, dinv) && lane == 0) set_fail(D.flags);
-      double bb = D.y[(size_t)k * 7 + lane7];
-      bb = sub_matvec<true, false, true>(bb, L, dtr_slot, dtr_p, q0, q1, D.y, lane7, lane49, lane, stg);
       fwd_solve_store<true>(bb, Lr, dinv, D.y + (size_t)k * 7, lane);
+      if (lane == 0) M3S_CSTAMP(0, k, 2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) M3S_CSTAMP(0, k, 3);
     } else if (code < D.n_tasks) {  // OFF(t)
       const int dst = task_dst[code], k = task_col[code];
       const int q0 = task_tr_ptr[code], q1 = task_tr_ptr[code + 1];
-      bool ok = wait_flags(D.sdone, task_col, code, code + 1, BIG, want, lane);  // DIAG(k)
-      ok &= wait_flags(D.sdone, tr_a, q0, q1, BIG, want, lane);
-      ok &= wait_flags(D.sdone, tr_b, q0, q1, BIG, want, lane);
-      if (!ok && lane == 0) set_fail(D.flags);
-      if (act49) W[lane] = ld_sc1(D.Dinv + (size_t)k * 49 + lane);
+      if (lane == 0) M3S_CSTAMP(3, dst, 0);
+      // the update sum first (its blocks are usually final before DIAG(k)),
+      // then DIAG(k)'s W_k
+      bool ok = true;
       double v = L[(size_t)dst * 49 + lane49];
-      v = sub_products<true, false, true>(v, L, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+      v = sub_products<true, false, true>(v, L, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg, D.sdone, want, &ok);
+      if (lane == 0) M3S_CSTAMP(3, dst, 1);
+      ok &= wait_flags(D.sdone, task_col, code, code + 1, BIG, want, lane);  // DIAG(k)
+      if (!ok && lane == 0) set_fail(D.flags);
+      if (lane == 0) M3S_CSTAMP(3, dst, 2);
+      if (act49) W[lane] = ld_sc1(D.Dinv + (size_t)k * 49 + lane);
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -2109,6 +2230,7 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       wave_lds_fence();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + dst, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) M3S_CSTAMP(3, dst, 3);
     } else {  // BORDER(b): waits for its update prefix, then border_task (sc1 reads)
       const int bt = code - D.n_tasks, nc = D.nc;
       const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
@@ -2177,9 +2299,11 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
 }
 
+constexpr int kBsCap = 40;  // L_ik blocks of a column prefetched into LDS (the rest staged)
 __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
   if (C.flags[kFlagStop]) return;
   __shared__ __attribute__((aligned(16))) double stage[kStageDoubles];
+  __shared__ double Lst[kBsCap * 49], xst[kBsCap * 7];
   const int lane = threadIdx.x;
   const int32_t *pl = C.plan;
   const int32_t *col_ptr = pl + C.off[1], *col_row = pl + C.off[2], *col_slot = pl + C.off[3],
@@ -2197,13 +2321,34 @@ __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
     const int k = corder[C.ncols - 1 - t];
     const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
     if (lane == 0) M3S_CSTAMP(1, k, 0);
+    // the factor is final (earlier launches): its blocks L_ik of this column
+    // and W_k are fetched BEFORE waiting, so only the x_i hand-off is left on
+    // the critical path
+    const int npre = (q1 - q0 < kBsCap) ? q1 - q0 : kBsCap;
+    for (int bq = 0; bq < npre; bq++)
+      if (lane < 49) Lst[bq * 49 + lane] = C.L[(size_t)col_slot[q0 + bq] * 49 + lane];
+    double wk[7];
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) wk[mm] = C.Dinv[(size_t)k * 49 + mm * 7 + lane7];
+    double rr = C.y[(size_t)k * 7 + lane7];
     if (!wait_flags(C.done2, col_row, q0, q1, C.c0, C.epoch + 1, lane) && lane == 0) set_fail(C.flags);
     if (lane == 0) M3S_CSTAMP(1, k, 1);
-    double rr = C.y[(size_t)k * 7 + lane7];
-    rr = sub_matvec<true, true, true>(rr, C.L, col_slot, col_row, q0, q1, C.y, lane7, lane49, lane, stage);
+    for (int idx = lane; idx < 7 * npre; idx += 64) {
+      const int bq = idx / 7;
+      xst[idx] = ld_sc1(C.y + (size_t)col_row[q0 + bq] * 7 + (idx - 7 * bq));
+    }
+    wave_lds_fence();
+    for (int bq = 0; bq < npre; bq++) {  // sub_matvec<TRANS>'s per-block sums, same order
+      double t0 = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) t0 += Lst[bq * 49 + mm * 7 + lane7] * xst[bq * 7 + mm];
+      rr -= t0;
+    }
+    wave_lds_fence();
+    rr = sub_matvec<true, true, true>(rr, C.L, col_slot, col_row, q0 + npre, q1, C.y, lane7, lane49, lane, stage);
     double xk = 0.0;
 #pragma unroll
-    for (int mm = 0; mm < 7; mm++) xk += C.Dinv[(size_t)k * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
+    for (int mm = 0; mm < 7; mm++) xk += wk[mm] * readlane_d(rr, mm);
     if (lane < 7) st_sc1(C.y + (size_t)k * 7 + lane, xk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(C.done2 + k, C.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2273,51 +2418,65 @@ __device__ int64_t *g_tail_stamp;
 #else
 #define M3S_DSTAMP(i)
 #endif
-__device__ __forceinline__ bool tail_diag(const double (*Dg)[17], double (*Wk)[17], double *yv_k, int jv, int rhs_row,
-                                          int lane) {
+template <bool FULL>  // FULL: jv == 16 (every tile column but possibly the last)
+__device__ __forceinline__ bool tail_diag_t(const double (*Dg)[17], double (*Wk)[17], double *yv_k, int jv,
+                                            int rhs_row, int lane) {
+  if (FULL) jv = 16;
+  __shared__ double colb[16];
+  // One pass: right-looking Cholesky by rows (lane r holds row r) and, with
+  // the same broadcast column of L, W = L^-1 by columns (lane c holds column
+  // c): at step j, W[j][c] = s_j[c] / L_jj is final and the pending s_r[c]
+  // (r > j) lose L[r][j] W[j][c]. The two sums keep their order (mm
+  // ascending); the rank-1 update is unmasked (upper-triangle entries are
+  // never read before step c zeroes them).
   const int lr = lane & 15;
   M3S_DSTAMP(110)
-  double a[16];
+  double a[16], sw[16], w[16];
 #pragma unroll
   for (int c = 0; c < 16; c++) a[c] = Dg[lr][c];
-  double dinv[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) sw[r] = (r == lane) ? 1.0 : 0.0;
+  // Branch-free: padding / RHS columns j >= jv become identity columns (and
+  // identity W rows) by selects, so their rank-1 updates are exact no-ops
+  // (no divergent control flow that would shuffle the register arrays).
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    if (j < jv) {
-      double d = readlane_d(a[j], j);
-      bad |= !(d > 0.0);
-      d = d > 0.0 ? d : 1.0;
-      const double inv = rsqrt_nr(d);
-      dinv[j] = inv;
-      a[j] = (lane > j) ? a[j] * inv : ((lane == j) ? d * inv : 0.0);
-#pragma unroll
-      for (int c = j + 1; c < 16; c++) {
-        const double lcj = readlane_d(a[j], c);
-        if (lane >= c) a[c] -= a[j] * lcj;
-      }
+    const bool real = FULL || j < jv;
+    double d = readlane_d(a[j], j);
+    bad |= real && !(d > 0.0);
+    d = (real && d > 0.0) ? d : 1.0;
+    const double inv = rsqrt_nr(d);
+    // column j scaled on every lane: lane j holds the pivot itself (d * inv
+    // = L_jj), lanes below hold L_rj; the lanes above keep finite upper-
+    // triangle values that no later step reads (no lane masks, which the
+    // compiler would keep live for all 16 steps)
+    const double aj = a[j] * inv;
+    if (FULL) {
+      a[j] = aj;
+      w[j] = sw[j] * inv;
     } else {
-      dinv[j] = 1.0;
-      a[j] = (lane == j) ? 1.0 : 0.0;
+      const double id = (lane == j) ? 1.0 : 0.0;
+      a[j] = real ? aj : id;
+      w[j] = real ? sw[j] * inv : id;
     }
+    // column j of L to every lane through LDS (readlane broadcasts of 15
+    // doubles per step spill SGPRs)
+    if (lane < 16) colb[lane] = a[j];
+    wave_lds_fence();
+#pragma unroll
+    for (int c = j + 1; c < 16; c++) {
+      const double lcj = colb[c];
+      a[c] -= a[j] * lcj;
+      sw[c] -= lcj * w[j];
+    }
+    wave_lds_fence();
   }
   M3S_DSTAMP(111)
   if (lane == rhs_row) {
 #pragma unroll
     for (int j = 0; j < 16; j++)
       if (j < jv) yv_k[j] = a[j];
-  }
-  // W = L^-1: lane c computes column c
-  double w[16];
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    double s2 = (r == lane) ? 1.0 : 0.0;
-    if (r < jv) {
-#pragma unroll
-      for (int mm = 0; mm < r; mm++) s2 -= readlane_d(a[mm], r) * w[mm];
-      s2 *= dinv[r];
-    }
-    w[r] = s2;
   }
   M3S_DSTAMP(112)
   if (lane < 16) {
@@ -2326,6 +2485,11 @@ __device__ __forceinline__ bool tail_diag(const double (*Dg)[17], double (*Wk)[1
   }
   M3S_DSTAMP(113)
   return bad;
+}
+__device__ __forceinline__ bool tail_diag(const double (*Dg)[17], double (*Wk)[17], double *yv_k, int jv, int rhs_row,
+                                          int lane) {
+  return jv == 16 ? tail_diag_t<true>(Dg, Wk, yv_k, jv, rhs_row, lane)
+                  : tail_diag_t<false>(Dg, Wk, yv_k, jv, rhs_row, lane);
 }
 
 __device__ __forceinline__ int tail_tile(int I, int J) { return I * (I + 1) / 2 + J; }
@@ -2495,6 +2659,248 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
   for (int j = tid; j < n; j += 64 * kTailNW) A.rhs[7 * A.c0 + j] = xv[j];
   if (tid == 0 && fail_s) A.flags[kFlagSplitFail] = 1;
 #undef M3S_STAMP
+}
+
+// ----------------------------- dense tail over many workgroups (default) --
+// The same left-looking 16x16-tile factorisation as tail_llt_kernel, with
+// tile column J on workgroup J (TC workgroups of 4 waves, wave w holding the
+// rows I = J + w (mod 4) in MFMA accumulator registers). Workgroup J applies
+// the update of every finished column k < J as soon as column k is published
+// (A(I,J)^T -= L(J,k) L(I,k)^T, k ascending: the single-workgroup kernel's
+// order, so the result is bitwise the same), then factors its diagonal tile,
+// forms its panel L(I,J)^T = W_J A(I,J)^T, and publishes the panel, W_J and
+// y'_J (write-through stores drained before an epoch flag). The critical
+// path per tile column is one hand-off + one tile update + the diagonal
+// factor, instead of the whole left-looking sweep of one CU (281 us at 256
+// KFs). The last workgroup then runs the back-substitution L^T x = y' over
+// the published tiles (sc1 loads).
+struct TailSync {
+  int32_t *tflag;    // [TC] epoch flags: tile column published
+  int32_t *tflag_e;  // [TC] epoch flags: its first sub-diagonal tile L(J+1, J) published
+  int epoch;
+  double *ypg;     // y' of every tile column [16 TC]
+  double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout (back-substitution A operands)
+};
+
+__device__ __forceinline__ f64x4 ld_sc1_f64x4(const double *p) {
+  f64x4 v;
+#pragma unroll
+  for (int r = 0; r < 4; r++) v[r] = ld_sc1(p + r);
+  return v;
+}
+__device__ __forceinline__ void st_sc1_f64x4(double *p, f64x4 v) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) st_sc1(p + r, v[r]);
+}
+
+__global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, TailSync S) {
+  if (A.flags[kFlagStop]) return;
+  __shared__ double Wk[16][17];
+  __shared__ double Dg[16][17];
+  __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
+  __shared__ int fail_s;
+  const int n = 7 * A.nc;
+  const int TC = (n + 15) / 16, TR = (n + 16) / 16;
+  const int In = n / 16, rn = n - 16 * In;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int J = blockIdx.x;
+  const int want = S.epoch + 1;
+  double *Lg = A.Lg, *Wg = A.Wg;
+  // rows: wave 0 holds only the diagonal tile (its factor is the critical
+  // path), waves 1..3 the rows below it, I = J + w + 3 u
+  constexpr int kRC = (kTailMaxT + 2) / 3;
+  auto rowI = [&](int u) { return wave == 0 ? (u == 0 ? J : -1) : J + wave + 3 * u; };
+  auto live = [&](int u) {
+    const int I = rowI(u);
+    return I >= 0 && I < TR;
+  };
+  if (tid == 0) fail_s = 0;
+  for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) yv[q] = 0.0;
+  __syncthreads();
+  f64x4 acc[kRC];
+#pragma unroll
+  for (int u = 0; u < kRC; u++) {
+    f64x4 v = {0.0, 0.0, 0.0, 0.0};
+    if (live(u)) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[r] = tail_entry(A, n, 16 * rowI(u) + lr, 16 * J + lk + 4 * r);
+    }
+    acc[u] = v;
+  }
+  // updates from the finished columns, k ascending, each as soon as it is
+  // published. The diagonal tile takes its last one (k = J - 1) from the tile
+  // L(J, J-1) that workgroup J - 1 publishes early, so the diagonal factor
+  // starts while the rest of panel J - 1 is still on its way.
+  auto wait_flag_tail = [&](const int32_t *f) {
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kColSpins) break;
+    }
+    if (spins > kColSpins && lane == 0) fail_s = 1;
+  };
+  auto update_rows = [&](int k) {
+    const f64x4 rk = ld_sc1_f64x4(Lg + (size_t)tail_tile(J, k) * 256 + 4 * lane);
+    f64x4 ri[kRC];
+#pragma unroll
+    for (int u = 0; u < kRC; u++)
+      if (live(u)) ri[u] = ld_sc1_f64x4(Lg + (size_t)tail_tile(rowI(u), k) * 256 + 4 * lane);
+#pragma unroll
+    for (int u = 0; u < kRC; u++) {
+      if (live(u)) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-rk[q], ri[u][q], acc[u], 0, 0, 0);
+      }
+    }
+  };
+  for (int k = 0; k + 1 < J; k++) {
+    wait_flag_tail(S.tflag + k);
+    update_rows(k);
+  }
+  if (J > 0) {
+    wait_flag_tail((wave == 0 ? S.tflag_e : S.tflag) + (J - 1));
+    update_rows(J - 1);
+  }
+  if (tid == 0) M3S_CSTAMP(2, J, 1);
+  if (wave == 0) {  // the diagonal tile
+#pragma unroll
+    for (int r = 0; r < 4; r++) Dg[lr][lk + 4 * r] = acc[0][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (tail_diag(Dg, Wk, yv + 16 * J, min(16, n - 16 * J), In == J ? rn : -1, lane) && lane == 0) fail_s = 1;
+    wave_lds_fence();  // y' of the RHS row (lane rn) for the other lanes
+    if (lane < 16) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)J * 256 + r * 16 + lane, Wk[r][lane]);
+      if (In == J) st_sc1(S.ypg + 16 * J + lane, yv[16 * J + lane]);
+    }
+  }
+  __syncthreads();  // W_J
+  if (tid == 0) M3S_CSTAMP(2, J, 2);
+  // panel L(I, J)^T = W_J A(I, J)^T; wave 1's first row (I = J + 1) first,
+  // published early for workgroup J + 1
+#pragma unroll
+  for (int u = 0; u < kRC; u++) {
+    const int I = rowI(u);
+    if (live(u) && I > J) {
+      f64x4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; q++) d = __builtin_amdgcn_mfma_f64_16x16x4f64(Wk[lr][4 * q + lk], acc[u][q], d, 0, 0, 0);
+      st_sc1_f64x4(Lg + (size_t)tail_tile(I, J) * 256 + 4 * lane, d);
+      if (I == In && lr == rn) {  // y' of this column from the RHS row
+#pragma unroll
+        for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J + lk + 4 * r, d[r]);
+      }
+      if (I < TC) {  // L(I, J) itself (operands swapped: A(I, J) W^T) for the back-substitution
+        f64x4 dt = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          dt = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[u][q], Wk[lr][4 * q + lk], dt, 0, 0, 0);
+        st_sc1_f64x4(S.LgT + (size_t)tail_tile(I, J) * 256 + 4 * lane, dt);
+      }
+      if (I == J + 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+          __hip_atomic_store(S.tflag_e + J, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          M3S_CSTAMP(2, J, 0);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave has left
+  __syncthreads();
+  if (tid == 0) {
+    if (fail_s) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S.tflag + J, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    M3S_CSTAMP(2, J, 3);
+  }
+  if (J != TC - 1) return;
+  // The last workgroup: back-substitution L^T x = y' over the published tiles
+  // (every column k < J was waited for above). Wave w owns the tile rows
+  // J' = w (mod 4) of y' (it alone updates them); x_K is formed by the owner
+  // of row K as soon as its own updates from x_{K+1..} are in, then handed to
+  // the other waves through LDS with a flag: no workgroup barrier per step.
+  // The same sums in the same order as tail_llt_kernel's loop.
+  __shared__ int xflag[kTailMaxT];
+  for (int q = tid; q < 16 * TC; q += 64 * kTailNW) yv[q] = ld_sc1(S.ypg + q);
+  for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) xv[q] = 0.0;
+  if (tid < kTailMaxT) xflag[tid] = 0;
+  __syncthreads();
+  // y_J -= L(K, J)^T x_K on the f64 MFMA: A = L(K, J)^T from the LgT tile
+  // (operand order: one 32-B load per lane), B = x_K in every column, so
+  // D[m][.] = (L^T x)[m]; lanes 0, 16, 32, 48 hold the 16 results.
+  constexpr int kTW = (kTailMaxT + kTailNW - 1) / kTailNW;  // tile rows J' of one wave
+  constexpr int kRing = 3;  // steps of tile loads in flight
+  f64x4 lt[kRing][kTW];
+  double wb[kRing][16];
+  auto bs_load = [&](int K, int slot) {
+#pragma unroll
+    for (int t = 0; t < kTW; t++) {
+      const int Jc = wave + kTailNW * t;
+      if (Jc < K) lt[slot][t] = ld_sc1_f64x4(S.LgT + (size_t)tail_tile(K, Jc) * 256 + 4 * lane);
+    }
+    if (K % kTailNW == wave && lane < 16) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) wb[slot][i] = ld_sc1(Wg + (size_t)K * 256 + i * 16 + lane);
+    }
+  };
+  // step K uses ring slot (TC - 1 - K) % kRing: compile-time in the unrolled loop
+#pragma unroll
+  for (int d = 0; d < kRing; d++)
+    if (TC - 1 - d >= 0) bs_load(TC - 1 - d, d);
+  for (int K0 = TC - 1; K0 >= 0; K0 -= kRing) {
+#pragma unroll
+    for (int d = 0; d < kRing; d++) {
+      const int K = K0 - d;
+      if (K < 0) break;
+      const int jv = min(16, n - 16 * K);
+      if (K % kTailNW == wave) {  // the owner of row K: its updates are all in
+        if (lane < 16) {
+          double x = 0.0;
+#pragma unroll
+          for (int i = 0; i < 16; i++) x += wb[d][i] * yv[16 * K + i];
+          xv[16 * K + lane] = lane < jv ? x : 0.0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        int spins = 0;
+        while (__hip_atomic_load(xflag + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && spins < (1 << 22))
+          spins++;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+      double xb[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) xb[q] = xv[16 * K + 4 * q + lk];
+      f64x4 u[kTW];
+#pragma unroll
+      for (int t = 0; t < kTW; t++) {
+        const int Jc = wave + kTailNW * t;
+        u[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+        if (Jc < K) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) u[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(lt[d][t][q], xb[q], u[t], 0, 0, 0);
+        }
+      }
+      if (K - kRing >= 0) bs_load(K - kRing, d);
+      if (lr == 0) {
+#pragma unroll
+        for (int t = 0; t < kTW; t++) {
+          const int Jc = wave + kTailNW * t;
+          if (Jc < K) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) yv[16 * Jc + lk + 4 * r] -= u[t][r];
+          }
+        }
+      }
+      wave_lds_fence();  // this wave's y' rows before it (as owner) reads them
+    }
+  }
+  __syncthreads();  // every x_K
+  for (int j = tid; j < n; j += 64 * kTailNW) A.rhs[7 * A.c0 + j] = xv[j];
+  if (tid == 0) M3S_CSTAMP(2, 511, 0);
 }
 
 // ------------------------------------------------- small dense Cholesky --
@@ -2731,6 +3137,11 @@ inline bool df_path() {  // M3S_DF=0: column tasks + border_kernel instead of th
   return !(e && e[0] == '0');
 }
 
+inline bool tail_cyc() {  // M3S_TAIL_CYC=0: the dense tail on one workgroup (tail_llt_kernel, A/B)
+  const char *e = std::getenv("M3S_TAIL_CYC");
+  return !(e && e[0] == '0');
+}
+
 inline bool tail_mfma() {  // M3S_TAIL_MFMA=0: the dense tail in sparse_llt_kernel (A/B)
   const char *e = std::getenv("M3S_TAIL_MFMA");
   return !(e && e[0] == '0');
@@ -2809,6 +3220,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.Cs = a->Cs;
   L.Xsrc = nullptr;
   L.idx = a->idx_ii2jj;
+  L.idx32 = a->idx_i32 ? 1 : 0;
   L.valid = a->valid_match;
   L.Q = a->Q;
   L.rank_i = at<int32_t>(ws, Ly.rank_i);
@@ -3005,7 +3417,18 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         T.flags = flags;
         T.nc = meta.nc;
         T.c0 = C.c0;
-        tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
+        if (tail_cyc()) {
+          TailSync Y;
+          Y.tflag = cs + 2 * (meta.m + 1) + 16 + Ly.slot_cap;
+          Y.tflag_e = Y.tflag + kTailMaxT;
+          Y.epoch = meta.epoch;
+          Y.ypg = T.Wg + (size_t)kTailMaxT * 256;
+          Y.LgT = Y.ypg + 16 * kTailMaxT;
+          const int TC = (7 * meta.nc + 15) / 16;
+          tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
+        } else {
+          tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
+        }
       }
       const int g4 = std::max(1, std::min(C.ncols, 256));
       col_backsub_kernel<<<g4, 64, 0, st>>>(C);
@@ -3869,7 +4292,9 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
 
 // Instrumented builds only (tools/trk_stamps.py, tools/col_stamps.py):
 // which = 0: persistent tracker phase stamps [2][16][8] (-DM3S_TRK_STAMPS);
-// which = 1: column-task stamps [2][512][4] (-DM3S_COL_STAMPS). Wall-clock
+// which = 1: column-task stamps [4][2048][4] (-DM3S_COL_STAMPS: factor
+// DIAG / column tasks, back-substitution, tail_cyc_kernel columns, OFF items
+// by slot). Wall-clock
 // ticks (100 MHz). Returns 1, or 0 when the build has no such stamps.
 int m3s_debug_stamps(int which, int64_t *out) {
   if (hipDeviceSynchronize() != hipSuccess) return M3S_ELAUNCH;

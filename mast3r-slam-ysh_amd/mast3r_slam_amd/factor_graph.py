@@ -8,7 +8,9 @@ pixel) and stacks the keyframe pointmaps (`get_poses_points`, :112-119). Here:
 
 * ``EdgeStore`` holds the directed edges already in two-way form, each
   undirected edge as two adjacent rows (i->j, j->i), in capacity-doubling
-  device buffers: a solve passes views, nothing is copied;
+  device buffers: a solve passes views, nothing is copied. Match indices are
+  int32 (a pixel index of one keyframe, < 2^31): the GN's first iteration
+  reads 9 B of edge data per pixel instead of 13 (m3s_gn_args.idx_i32);
 * ``KeyframeStore`` holds X_canon / C / N / T_WC in [capacity, ...] buffers
   like SharedKeyframes (frame.py:220-247); when the graph's keyframes are a
   contiguous id range (the usual case) the solve passes views and the GN
@@ -16,7 +18,11 @@ pixel) and stacks the keyframe pointmaps (`get_poses_points`, :112-119). Here:
 
 The per-edge order differs from the reference's (interleaved instead of all
 forward then all reverse); the normal equations are order-independent up to
-fp64 rounding of the per-slot sums. ``add_factors`` takes the outputs of
+fp64 rounding of the per-slot sums (tests/test_factor_graph.py checks the
+mirror against the oracle fed the reference's concatenated edge order).
+X / C keep the SharedKeyframes array-of-structs layout [cap, HW, 3]: the GN
+gathers X_i through idx, and one 12-B point per gathered pixel stays within
+one cache line (three separate planes would touch three). ``add_factors`` takes the outputs of
 mast3r_match_symmetric (the network is out of scope) and applies the
 reference's edge filter (global_opt.py:56-78).
 """
@@ -44,7 +50,7 @@ class EdgeStore:
         d, HW = self.device, self.HW
         new = dict(ii=torch.empty(2 * cap, dtype=torch.int64, device=d),
                    jj=torch.empty(2 * cap, dtype=torch.int64, device=d),
-                   idx=torch.empty(2 * cap, HW, dtype=torch.int64, device=d),
+                   idx=torch.empty(2 * cap, HW, dtype=torch.int32, device=d),
                    valid=torch.empty(2 * cap, HW, 1, dtype=torch.bool, device=d),
                    Q=torch.empty(2 * cap, HW, 1, dtype=torch.float32, device=d))
         if grow:

@@ -6,10 +6,9 @@ kernel ``mast3r_slam_backends.fuse_pointmap``.
 ``Pointmap`` holds what the reference ``Frame`` holds for this purpose
 (X_canon [HW,3], C [HW,1], N, N_updates, score) and applies the same
 filtering modes (config tracking.filtering_mode). weighted_pointmap (the
-default), indep_conf and recent run in one fused device pass; first and
-best_score are whole-tensor copies decided on the host as the reference
-does; weighted_spherical is not built (SURVEY §8f #2 lists the default
-mode) and raises.
+default), weighted_spherical, indep_conf and recent run in one fused device
+pass; first and best_score are whole-tensor copies decided on the host as the
+reference does.
 """
 from __future__ import annotations
 
@@ -59,7 +58,7 @@ class Pointmap:
             raise NotImplementedError(f"filtering_mode {self.mode!r} is not built on the device path")
         be.fuse_pointmap(self.X_canon, self.C, X.contiguous(), C.contiguous(),
                          None if T is None else _pose(T), self.mode)
-        self.N = self.N + 1 if self.mode == "weighted_pointmap" else 1
+        self.N = self.N + 1 if self.mode in ("weighted_pointmap", "weighted_spherical") else 1
         self.N_updates += 1
 
 

@@ -54,6 +54,7 @@ class GnArgs(ctypes.Structure):
         ("max_iter", ctypes.c_int), ("delta_thresh", ctypes.c_float),
         ("dx_out", _VP), ("info", _VP),
         ("workspace", _VP), ("workspace_bytes", ctypes.c_size_t),
+        ("idx_i32", ctypes.c_int),
     ]
 
 
@@ -121,7 +122,7 @@ EXPORTS = (
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
     "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_debug_stamps",
 )
-FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2}
+FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2, "weighted_spherical": 3}
 
 
 def _load(path=LIB_PATH):
@@ -246,7 +247,7 @@ def _check(t: torch.Tensor, name: str, dtype=None):
         raise RuntimeError(f"{name} must be contiguous")
     if t.device.type != "cuda":
         raise RuntimeError(f"{name} must be on a ROCm device (got {t.device}); no CPU path")
-    if dtype is not None and t.dtype != dtype:
+    if dtype is not None and t.dtype not in (dtype if isinstance(dtype, tuple) else (dtype,)):
         raise RuntimeError(f"{name} must be {dtype} (got {t.dtype})")
 
 
@@ -282,7 +283,8 @@ def make_gn_args(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, K=None, *
         _check(K, "K", torch.float32)
     _check(ii, "ii", torch.int64)
     _check(jj, "jj", torch.int64)
-    _check(idx_ii2jj, "idx_ii2jj", torch.int64)
+    # int64 as the reference passes it; int32 from the device edge store
+    _check(idx_ii2jj, "idx_ii2jj", (torch.int64, torch.int32))
     _check(valid_match, "valid_match", torch.bool)
     _check(Q, "Q", torch.float32)
     N, HW = int(Xs.shape[0]), int(Xs.shape[1])
@@ -306,6 +308,7 @@ def make_gn_args(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, K=None, *
     a = GnArgs()
     a.Twc, a.Xs, a.Cs, a.ii, a.jj = _p(Twc), _p(Xs), _p(Cs), _p(ii), _p(jj)
     a.idx_ii2jj, a.valid_match, a.Q, a.K = _p(idx_ii2jj), _p(valid_match), _p(Q), _p(K)
+    a.idx_i32 = 1 if idx_ii2jj.dtype == torch.int32 else 0
     a.N, a.HW, a.E, a.mode = N, HW, E, mode
     a.sigma_a, a.sigma_b = float(sigma_a), float(sigma_b)
     a.C_thresh, a.Q_thresh = float(C_thresh), float(Q_thresh)

@@ -6,8 +6,10 @@ TEST INFRASTRUCTURE ONLY — imported by tests/ as the checker; the product path
 
 * ``fuse_pointmap``  tracker.py:98-99 (Xkk = T_CkCf.act(Xkf)) + Frame.update_pointmap
                      (frame.py:41-100) for an initialised keyframe, modes
-                     weighted_pointmap (:73-76), indep_conf (:68-72), recent (:59-62);
-                     elementwise fp32 in the torch expressions' operation order.
+                     weighted_pointmap (:73-76), indep_conf (:68-72), recent (:59-62),
+                     weighted_spherical (:78-100, the reference's torch expressions
+                     on CPU tensors); elementwise fp32 in the torch expressions'
+                     operation order.
 * ``prep_rays``      prep_for_iter_proj (matching.py:25-49): F.normalize (eps 1e-12),
                      Scharr x/y kernels / 32 with reflect padding (image.py:5-38).
 
@@ -41,6 +43,21 @@ def fuse_pointmap(X_canon, C, X_new, C_new, T=None, mode="weighted_pointmap"):
         Co[m] = Cn[m]
     elif mode == "recent":
         Xc, Co = X.copy(), Cn.copy()
+    elif mode == "weighted_spherical":  # frame.py:78-100, the same torch ops
+        def to_sph(P):
+            r = torch.linalg.norm(P, dim=-1, keepdim=True)
+            x, y, z = torch.tensor_split(P, 3, dim=-1)
+            return torch.cat((r, torch.atan2(y, x), torch.acos(z / r)), dim=-1)
+
+        def to_cart(S):
+            r, phi, theta = torch.tensor_split(S, 3, dim=-1)
+            return torch.cat((r * torch.sin(theta) * torch.cos(phi), r * torch.sin(theta) * torch.sin(phi),
+                              r * torch.cos(theta)), dim=-1)
+
+        tC, tCn = torch.as_tensor(Co), torch.as_tensor(Cn)
+        s = ((tC * to_sph(torch.as_tensor(Xc))) + (tCn * to_sph(torch.as_tensor(X)))) / (tC + tCn)
+        Xc = to_cart(s).numpy().astype(F32)
+        Co = (Co + Cn).astype(F32)
     else:
         raise ValueError(mode)
     return Xc, Co

@@ -1,7 +1,9 @@
 """Device-resident FactorGraph mirror (mast3r_slam_amd/factor_graph.py,
 SURVEY §8f #3): CPU checks of the two-way edge store and the reference's edge
 filter (global_opt.py:56-100), GPU check of solve_GN_* against the drop-in
-entry point on the reference's prep_two_way_edges tensors."""
+entry point on the reference's prep_two_way_edges tensors, and against the
+CPU oracle fed the reference's concatenated two-way edge order (all i->j,
+then all j->i; global_opt.py:104-110)."""
 import numpy as np
 import pytest
 import torch
@@ -29,7 +31,8 @@ def test_edge_store_two_way_layout_and_growth():
     assert st.capacity >= E and dii.numel() == 2 * E
     assert torch.equal(dii[0::2], ii) and torch.equal(dii[1::2], jj)
     assert torch.equal(djj[0::2], jj) and torch.equal(djj[1::2], ii)
-    assert torch.equal(didx[0::2], i2j) and torch.equal(didx[1::2], j2i)
+    assert didx.dtype == torch.int32  # the store's int32 match indices (m3s_gn_args.idx_i32)
+    assert torch.equal(didx[0::2].long(), i2j) and torch.equal(didx[1::2].long(), j2i)
     assert torch.equal(dv[1::2], vi) and torch.equal(dQ[0::2], Qj)
     assert didx.is_contiguous() and dv.is_contiguous() and dQ.is_contiguous()
 
@@ -84,3 +87,39 @@ def test_solve_matches_dropin_on_reference_layout(calib):
     torch.cuda.synchronize()
     np.testing.assert_allclose(kf.T_WC[:N].cpu().numpy(), T.cpu().numpy(), atol=1e-5)
     assert torch.equal(kf.T_WC[0], g.T_init.data[0])  # pinned
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("calib", [False, True])
+def test_solve_matches_oracle_on_reference_edge_order(calib):
+    """The mirror (interleaved edge rows, int32 idx, keyframe views) against
+    oracle/gn_oracle.c on the reference's own two-way layout (forward half then
+    backward half, int64 idx): 10 GN iterations of LOCAL_OPT_CFG, poses within
+    the backend's 10-iteration tolerance (1e-4 absolute)."""
+    from oracle import oracle as orc
+    from oracle.tracker_oracle import constrain_points_to_ray
+
+    dev = torch.device("cuda:0")
+    N, H, W = 7, 24, 32
+    g = synthetic.make_graph(N, H, W, seed=13)
+    kf = fgm.KeyframeStore(H, W, dev, capacity=16)
+    for k in range(N):
+        kf.append(g.Xs[k].to(dev), g.Cs[k].to(dev), g.T_init.data[k].to(dev))
+    fg = fgm.FactorGraph(kf, K=g.K.to(dev))
+    assert fg.add_factors(*(t.to(dev) for t in _halves(g)), min_match_frac=0.0)
+    (fg.solve_GN_calib if calib else fg.solve_GN_rays)()
+    torch.cuda.synchronize()
+    c = fgm.LOCAL_OPT_CFG
+    if calib:
+        p = orc.make_params(orc.MODE_CALIB, c["sigma_pixel"], c["sigma_depth"], c["C_conf"], c["Q_conf"],
+                            K=g.K.numpy(), height=H, width=W, pixel_border=c["pixel_border"],
+                            z_eps=c["depth_eps"])
+        Xs = np.stack([constrain_points_to_ray((H, W), x, g.K.numpy()) for x in g.Xs.numpy()])
+    else:
+        p = orc.make_params(orc.MODE_RAYS, c["sigma_ray"], c["sigma_dist"], c["C_conf"], c["Q_conf"])
+        Xs = g.Xs.numpy()
+    T_ref, dx_ref, it, failed = orc.gn(p, g.T_init.data.numpy(), Xs, g.Cs.numpy(), g.ii.numpy(), g.jj.numpy(),
+                                       g.idx_ii2jj.numpy(), g.valid_match.numpy(), g.Q.numpy(), c["max_iters"],
+                                       c["delta_norm"])
+    assert failed == 0
+    np.testing.assert_allclose(kf.T_WC[:N].cpu().numpy(), T_ref, atol=1e-4)

@@ -38,7 +38,7 @@ for rep in range(3):
     s1.record()
     torch.cuda.synchronize()
 print(f"N={N}: solve {s0.elapsed_time(s1) * 1e3:.1f} us (HIP events, last rep)")
-st = np.zeros((2, 512, 4), np.int64)
+st = np.zeros((4, 2048, 4), np.int64)
 assert be._lib.m3s_debug_stamps(1, st.ctypes.data_as(__import__("ctypes").c_void_p)) == 1
 ri = np.unique(np.concatenate([g.ii.cpu().numpy(), g.jj.cpu().numpy()]), return_inverse=True)[1].reshape(2, -1)
 p = be.sparse_plan(N, ri[0], ri[1], split=32)
@@ -56,9 +56,13 @@ for k in range(m):
         lev[parent[k]] = max(lev[parent[k]], lev[k] + 1)
 F = st[0, :c0]
 t0 = F[:, 0].min()
+O = st[3]  # OFF items by destination slot: ticket, updates ready, DIAG(k) ready, published
+tdst = p["task_dst"]
+tcol = p["task_col"]
 us = lambda x: (x - t0) / 100.0  # noqa: E731
 print(f"sparse columns {c0}, tail columns {nc}; factor: first ticket -> last publish {us(F[:, 3].max()):.1f} us")
-print("level  cols   ticket(min/max)   ready(max)   diag(max)   publish(min/max)   per-column ready->publish (mean)")
+print("level  cols   ticket(min/max)   ready(max)   diag(max)   publish(min/max)   per-column ready->publish (mean)"
+      "   OFF: publish(max)  DIAG->OFF published (mean/max)")
 for L in range(lev[:c0].max() + 1):
     ks = cols[lev[:c0] == L]
     if not len(ks):
@@ -66,8 +70,26 @@ for L in range(lev[:c0].max() + 1):
     f = F[ks]
     print(f"{L:5d} {len(ks):5d}   {us(f[:, 0].min()):7.1f}/{us(f[:, 0].max()):7.1f}   {us(f[:, 1].max()):9.1f}"
           f"   {us(f[:, 2].max()):9.1f}   {us(f[:, 3].min()):7.1f}/{us(f[:, 3].max()):7.1f}"
-          f"   {((f[:, 3] - f[:, 1]) / 100.0).mean():8.2f}")
+          f"   {((f[:, 3] - f[:, 1]) / 100.0).mean():8.2f}", end="")
+    offs = [t for t in range(len(tdst)) if tcol[t] in set(ks.tolist())]
+    if offs:
+        op = np.array([O[tdst[t], 3] for t in offs])
+        gap = np.array([(O[tdst[t], 3] - F[tcol[t], 3]) / 100.0 for t in offs])
+        print(f"   {us(op.max()):9.1f}   {gap.mean():6.2f}/{gap.max():6.2f}")
+    else:
+        print()
 B = st[1, :c0]
 tb = B[:, 0].min()
 print(f"back-substitution: first ticket -> last x {((B[:, 2].max() - tb) / 100.0):.1f} us; per column ready->done "
       f"mean {((B[:, 2] - B[:, 1]) / 100.0).mean():.2f} us; wait (ticket->ready) max {((B[:, 1] - B[:, 0]) / 100.0).max():.1f} us")
+T = st[2]
+TC = (7 * nc + 15) // 16
+if TC:
+    tt0 = T[0, 1]
+    print(f"dense tail over {TC} workgroups (us from workgroup 0's updates done): column: updates done / "
+          f"diag done / first tile published early / published")
+    for J in range(TC):
+        a, b, c = ((T[J, 1:4] - tt0) / 100.0)
+        e = (T[J, 0] - tt0) / 100.0 if J + 1 < TC else float("nan")
+        print(f"  J={J:2d} {a:8.2f} {b:8.2f} {e:8.2f} {c:8.2f}")
+    print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")

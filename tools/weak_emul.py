@@ -2,9 +2,16 @@
 
 Per GN iteration a rank linearizes its slice (~98 directed edges at 32 KFs per
 GPU) and then runs the replicated solve of the whole 32*N-KF system. This
-times both parts with HIP events on one GPU (the all-gather is not included)
-and prints the predicted efficiency t_iter(1) / t_iter(N), for the sparse LLT,
-the persistent dense LLT (M3S_SOLVER=pdense) and the dense fallback (M3S_DENSE=1). Calib model, 512x512 (bench.py).
+builds the FULL synthetic graph of the N-GPU run (bench.py's generator and
+seed), linearizes every edge once so that the edge sums are the real system,
+then times, per iteration, rank 0's linearize of its own slice followed by the
+solve of the whole system, with HIP events. The poses are reset before every
+timed iteration, so each one solves the same real system. The all-gather
+(36 fp64 per edge) is not included. Any failed factorisation aborts the run.
+
+Prints t_iter(N) and the predicted efficiency t_iter(1) / t_iter(N).
+
+env: MODES=calib,rays  WORLDS=1,2,4,8  HW_SIDE=512  REPS=20
 """
 import os
 import sys
@@ -20,64 +27,60 @@ from mast3r_slam_amd.distributed import HipOps, edge_slice  # noqa: E402
 dev = torch.device("cuda:0")
 H = W = int(os.environ.get("HW_SIDE", "512"))
 REPS = int(os.environ.get("REPS", "20"))
-modes = os.environ.get("MODES", "sparse,pdense").split(",")
+modes = os.environ.get("MODES", "calib,rays").split(",")
+SIG = {"calib": (1.0, 10.0), "rays": (0.003, 10.0)}
 
 
 def ev():
     return torch.cuda.Event(enable_timing=True)
 
 
-base = None
+base = {}
 for world in [int(x) for x in os.environ.get("WORLDS", "1,2,4,8").split(",")]:
     N = 32 * world
-    probe = synthetic.make_graph(N, 4, 4, seed=1003, edge_range=(0, 0))
-    E = probe.n_edges
-    eb, ee, per = edge_slice(E, 0, world)
-    g = synthetic.make_graph(N, H, W, seed=1003, device=dev, edge_range=(eb, ee))
+    g = synthetic.make_graph(N, H, W, seed=1003, device=dev)
+    E = g.n_edges
+    _, ee0, _ = edge_slice(E, 0, world)
     rays = synthetic.pixel_rays(H, W, g.K)
-    Xs = (g.Xs[..., 2:3] * rays[None]).contiguous()
-    Twc = g.T_init.data.contiguous().clone()
-    row = {}
     for m in modes:
-        os.environ["M3S_DENSE"] = "1" if m == "dense" else "0"
-        os.environ["M3S_SOLVER"] = "pdense" if m == "pdense" else "sparse"
-        ops = HipOps(be.MODE_CALIB, Twc, Xs, g.Cs.contiguous(), g.ii.contiguous(), g.jj.contiguous(),
-                     g.idx_ii2jj, g.valid_match, g.Q, E, g.K, sigma_a=1.0, sigma_b=10.0, C_thresh=0.0,
-                     Q_thresh=1.5, height=H, width=W, pixel_border=-10, z_eps=1e-6)
-        es = torch.zeros(per * world, be.EDGE_SUM_STRIDE, dtype=torch.float64, device=dev)
+        Xs = (g.Xs[..., 2:3] * rays[None]).contiguous() if m == "calib" else g.Xs.contiguous()
+        T0 = g.T_init.data.contiguous().clone()
+        Twc = T0.clone()
+        mid = be.MODE_CALIB if m == "calib" else be.MODE_RAYS
+        ops = HipOps(mid, Twc, Xs, g.Cs.contiguous(), g.ii.contiguous(), g.jj.contiguous(), g.idx_ii2jj,
+                     g.valid_match, g.Q, E, g.K if m == "calib" else None, sigma_a=SIG[m][0],
+                     sigma_b=SIG[m][1], C_thresh=0.0, Q_thresh=1.5, height=H, width=W, pixel_border=-10,
+                     z_eps=1e-6)
+        es = torch.zeros(E, be.EDGE_SUM_STRIDE, dtype=torch.float64, device=dev)
         ops.prepare(0.0)
-        ops.linearize(eb, ee, es[: ee - eb])  # gathering kernel + planes
-        # the other ranks' rows: copies of this rank's (a well-posed stand-in)
-        for r in range(1, world):
-            b, e, _ = edge_slice(E, r, world)
-            k = e - b
-            es[r * per: r * per + k] = es[:k].repeat((k + ee - eb - 1) // (ee - eb), 1)[:k]
+        ops.linearize(0, E, es)  # every edge: the real system of the N-GPU run
         for _ in range(3):
-            ops.linearize(eb, ee, es[: ee - eb])
+            Twc.copy_(T0)
+            ops.linearize(0, ee0, es[:ee0])
             ops.solve(es)
         torch.cuda.synchronize()
         t_lin, t_sol = [], []
         for _ in range(REPS):
+            Twc.copy_(T0)
             a, b, c = ev(), ev(), ev()
             a.record()
-            ops.linearize(eb, ee, es[: ee - eb])
+            ops.linearize(0, ee0, es[:ee0])
             b.record()
             ops.solve(es)
             c.record()
             t_lin.append((a, b))
             t_sol.append((b, c))
         torch.cuda.synchronize()
-        lin = sum(x.elapsed_time(y) for x, y in t_lin) / REPS
-        sol = sum(x.elapsed_time(y) for x, y in t_sol) / REPS
+        lin = sum(x.elapsed_time(y) for x, y in t_lin) / REPS * 1e3
+        sol = sum(x.elapsed_time(y) for x, y in t_sol) / REPS * 1e3
         fail = int(ops.info[be.INFO_SOLVE_FAIL])
-        row[m] = (lin, sol, fail)
-        del ops
+        assert fail == 0, f"{m} N={N}: {fail} failed factorisations"
+        ops.close()
+        del ops, es
         torch.cuda.empty_cache()
-    best = min(row.values(), key=lambda v: v[0] + v[1])
-    if base is None:
-        base = best[0] + best[1]
-    txt = "  ".join(f"{m}: lin {v[0] * 1e3:.1f} us solve {v[1] * 1e3:.1f} us (fail {v[2]})" for m, v in row.items())
-    print(f"world {world} N={N} E={E} slice={ee - eb}: {txt}  -> eff {base / (best[0] + best[1]):.3f}",
-          flush=True)
-    del g, Xs
+        t = lin + sol
+        base.setdefault(m, t)
+        print(f"{m:5s} world {world} N={N} E={E} slice={ee0}: linearize {lin:7.1f} us  solve {sol:7.1f} us  "
+              f"iteration {t:7.1f} us  -> eff {base[m] / t:.3f}  (fail 0)", flush=True)
+    del g
     torch.cuda.empty_cache()

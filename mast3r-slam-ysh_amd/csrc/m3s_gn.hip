@@ -53,6 +53,9 @@ namespace {
 #ifndef M3S_PP  // packed linearize: two pixels per float2 (AccumPP) instead of row pairs
 #define M3S_PP 1
 #endif
+#ifndef M3S_GATHER_PP  // gathering (first-iteration) kernel on the pixel-pair accumulator too
+#define M3S_GATHER_PP 0
+#endif
 #ifndef M3S_PP_LDS  // PP: operands read from the LDS slot per pixel pair
 #define M3S_PP_LDS 1
 #endif
@@ -475,7 +478,12 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   float *__restrict__ pl = WPACK ? A.planes + (size_t)e_loc * NPL * HW : nullptr;
 
   // scalar accumulators here: 4 pixels of raw inputs stay live in this kernel
+  // (M3S_GATHER_PP: the pixel-pair accumulator of the packed kernel, backend only)
+#if M3S_GATHER_PP
+  typename std::conditional<TRACK, AccumFlat, AccumPP>::type acc;
+#else
   AccumFlat acc;
+#endif
   acc.zero();
 
   const int64_t p_begin = c * A.chunk_pix;
@@ -508,12 +516,30 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
       const float cjs[4] = {c4.x, c4.y, c4.z, c4.w};
       PixIn<MODE> in[4];
 #pragma unroll
-      for (int s = 0; s < 4; s++) {
+      for (int s = 0; s < 4; s++)
         in[s] = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p0 + s, ((vb >> (8 * s)) & 0xffu) != 0, ids[s],
                                           qs[s], cjs[s]);
-        float Y[3];
-        act(Tm, Xj[s], Y);
-        pixel_contrib<MODE>(acc, A.P, in[s], Y);
+#if M3S_GATHER_PP
+      if constexpr (!TRACK) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          f32x2 in2[NPL], X2[3], Y2[3];
+#pragma unroll
+          for (int k = 0; k < NPL; k++) in2[k] = f32x2{in[2 * h].v[k], in[2 * h + 1].v[k]};
+#pragma unroll
+          for (int k = 0; k < 3; k++) X2[k] = f32x2{Xj[2 * h][k], Xj[2 * h + 1][k]};
+          act2(Tm, X2, Y2);
+          pixel_contrib2<MODE, NPL>(acc, A.P, in2, Y2);
+        }
+      } else
+#endif
+      {
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          float Y[3];
+          act(Tm, Xj[s], Y);
+          pixel_contrib<MODE>(acc, A.P, in[s], Y);
+        }
       }
       if (WPACK) {
 #pragma unroll
@@ -530,9 +556,23 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
       const float Xj[3] = {Xs_j[3 * p], Xs_j[3 * p + 1], Xs_j[3 * p + 2]};
       const float cj = TRACK ? 0.0f : Cs_j[p];
       const PixIn<MODE> in = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p, vm, id, Qe[p], cj);
-      float Y[3];
-      act(Tm, Xj, Y);
-      pixel_contrib<MODE>(acc, A.P, in, Y);
+#if M3S_GATHER_PP
+      if constexpr (!TRACK) {  // the pixel in .x; .y the same pixel with weight 0
+        constexpr int sqk = MODE == 2 ? 1 : NPL - 1;  // the sqrt(q) plane (make_pixin)
+        f32x2 in2[NPL], X2[3], Y2[3];
+#pragma unroll
+        for (int k = 0; k < NPL; k++) in2[k] = f32x2{in.v[k], k == sqk ? 0.0f : in.v[k]};
+#pragma unroll
+        for (int k = 0; k < 3; k++) X2[k] = f32x2{Xj[k], Xj[k]};
+        act2(Tm, X2, Y2);
+        pixel_contrib2<MODE, NPL>(acc, A.P, in2, Y2);
+      } else
+#endif
+      {
+        float Y[3];
+        act(Tm, Xj, Y);
+        pixel_contrib<MODE>(acc, A.P, in, Y);
+      }
       if (WPACK) {
 #pragma unroll
         for (int k = 0; k < NPL; k++) pl[(size_t)k * HW + p] = in.v[k];
@@ -1478,11 +1518,11 @@ __device__ __forceinline__ void diag_updates_sc1(double &v, double &bb, const do
 // substitution -> dataflow back-substitution -> dx, retraction, ||dx||.
 // DIAG of one column: v (entry layout, lane = 7r + c) = D_k after all its
 // updates -> L_kk (row-major, upper part 0) into Lb[k], W_k = L_kk^-1
-// (row-major) into Di[k]; Lr (strictly lower L_kk) and dinv = 1 / diag, wave-
-// uniform, for the forward step. Returns true on a non-positive pivot.
+// (row-major) into Di[k] (and Wl, if given); lane c < 7 keeps column c of W_k
+// in wcol for the forward step. Returns true on a non-positive pivot.
 template <bool SC1 = false>
 __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double *Di, double *scr, int lane,
-                                            int l7, double (&Lr)[7][7], double (&dinv)[7], double *Wl = nullptr) {
+                                            int l7, double (&wcol)[7], double *Wl = nullptr) {
   // entry layout -> row layout through the wave's scratch
   if (lane < 49) scr[lane] = v;
   wave_lds_fence();
@@ -1490,64 +1530,62 @@ __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double 
 #pragma unroll
   for (int qq = 0; qq < 7; qq++) a[qq] = scr[l7 + qq];
   wave_lds_fence();
-  // Cholesky: lane r holds row r; column j of L broadcast by readlane
+  // One pass: right-looking Cholesky by rows (lane r holds row r) and, with
+  // the same column of L (broadcast through the scratch), W = L^-1 by
+  // columns (lane c holds column c): at step j, W[j][c] = s_j / L_jj is
+  // final and s_r (r > j) loses L[r][j] W[j][c]. Column j is scaled on every
+  // lane (lane j holds the pivot itself; the lanes above keep finite upper-
+  // triangle values that are masked when L_kk is stored). No per-pair
+  // readlanes, no second serial chain for W.
+  double sw[7];
+#pragma unroll
+  for (int r = 0; r < 7; r++) sw[r] = (r == lane) ? 1.0 : 0.0;
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < 7; j++) {
     const double d = readlane_d(a[j], j);
     bad |= !(d > 0.0);
     const double inv = rsqrt_nr(d);
-    dinv[j] = inv;
-    a[j] = (lane > j) ? a[j] * inv : ((lane == j) ? d * inv : 0.0);
+    a[j] *= inv;
+    wcol[j] = sw[j] * inv;
+    if (lane < 7) scr[lane] = a[j];
+    wave_lds_fence();
 #pragma unroll
     for (int cc = j + 1; cc < 7; cc++) {
-      const double lcj = readlane_d(a[j], cc);
-      if (lane >= cc) a[cc] -= a[j] * lcj;
+      const double lcj = scr[cc];
+      a[cc] -= a[j] * lcj;
+      sw[cc] -= lcj * wcol[j];
     }
-  }
-  // strictly-lower entries of L_kk as wave-uniform values
-#pragma unroll
-  for (int rr = 1; rr < 7; rr++)
-#pragma unroll
-    for (int mm = 0; mm < rr; mm++) Lr[rr][mm] = readlane_d(a[mm], rr);
-  // W = L^-1: lane c computes column c
-  double w[7];
-#pragma unroll
-  for (int rr = 0; rr < 7; rr++) {
-    double acc = (rr == lane) ? 1.0 : 0.0;
-#pragma unroll
-    for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * w[mm];
-    w[rr] = (rr >= lane) ? acc * dinv[rr] : 0.0;
+    wave_lds_fence();
   }
   if (lane < 7) {
 #pragma unroll
     for (int qq = 0; qq < 7; qq++) {
       st_blk<SC1>(Lb + (size_t)k * 49 + lane * 7 + qq, (qq <= lane) ? a[qq] : 0.0);  // row `lane` of L_kk
-      st_blk<SC1>(Di + (size_t)k * 49 + qq * 7 + lane, w[qq]);                       // column `lane` of W
-      if (Wl) Wl[qq * 7 + lane] = w[qq];
+      st_blk<SC1>(Di + (size_t)k * 49 + qq * 7 + lane, wcol[qq]);                    // column `lane` of W
+      if (Wl) Wl[qq * 7 + lane] = wcol[qq];
     }
   }
   return bad;
 }
 
-// y_k = L_kk^-1 b (lane r < 7 holds b_r), stored to yk_out[0..7)
+// y_k = W_k b (lane c < 7 holds b_c in bb and column c of W in wcol; the
+// sums run over c in order), stored to yk_out[0..7)
 template <bool SC1 = false>
-__device__ __forceinline__ void fwd_solve_store(double bb, const double (&Lr)[7][7], const double (&dinv)[7],
-                                                double *yk_out, int lane) {
-  double yk[7];
+__device__ __forceinline__ void fwd_solve_store(double bb, const double (&wcol)[7], double *scr, double *yk_out,
+                                                int lane) {
+  if (lane < 7) {
 #pragma unroll
-  for (int rr = 0; rr < 7; rr++) {
-    double acc = readlane_d(bb, rr);
-#pragma unroll
-    for (int mm = 0; mm < rr; mm++) acc -= Lr[rr][mm] * yk[mm];
-    yk[rr] = acc * dinv[rr];
+    for (int r = 0; r < 7; r++) scr[r * 7 + lane] = wcol[r] * bb;
   }
+  wave_lds_fence();
   if (lane < 7) {
     double yo = 0.0;
 #pragma unroll
-    for (int qq = 0; qq < 7; qq++) yo = (qq == lane) ? yk[qq] : yo;
+    for (int c = 0; c < 7; c++) yo += scr[lane * 7 + c];
     st_blk<SC1>(yk_out + lane, yo);
   }
+  wave_lds_fence();
 }
 
 // Border update of one dense-tail block (column-major task t over the nc x nc
@@ -1717,8 +1755,8 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       double v = Lb[(size_t)k * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
-      double Lr[7][7], dinv[7];
-      const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, Lr, dinv);
+      double wcol[7];
+      const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1727,7 +1765,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       double bb = y[k * 7 + lane7];
       for (int pi = p0; pi < p1; pi++) bb += D.parts[(size_t)pi * 56 + 49 + lane7];
       M3S_POLL(q0, q1, flag_set(&ydone[dtr_p[q]]), (bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, qa, qb, y, lane7, lane49, lane, stg)));
-      fwd_solve_store(bb, Lr, dinv, y + (size_t)k * 7, lane);
+      fwd_solve_store(bb, wcol, scr, y + (size_t)k * 7, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&ydone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
@@ -1791,10 +1829,10 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     // diagonal block kk: L_kk, W_k, forward step y_k (wave 0)
     auto tail_diag = [&](int kk) {
       const double v = Lb[(size_t)kk * 49 + lane49];
-      double Lr[7][7], dinv[7];
-      const bool bad = diag_factor(v, kk, Lb, Di, scr, lane, l7, Lr, dinv);
+      double wcol[7];
+      const bool bad = diag_factor(v, kk, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;
-      fwd_solve_store(y[kk * 7 + lane7], Lr, dinv, y + (size_t)kk * 7, lane);
+      fwd_solve_store(y[kk * 7 + lane7], wcol, scr, y + (size_t)kk * 7, lane);
     };
 #if M3S_TAIL_LOOKAHEAD
     // look-ahead: DIAG(k+1) runs on wave 0 inside step k's trailing update,
@@ -2093,11 +2131,11 @@ __global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
       // updates from the columns p (this launch: sc1)
       double v = L[(size_t)k * 49 + lane49];
       v = sub_products<true, true, true>(v, L, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
-      double Lr[7][7], dinv[7];
-      if (diag_factor<true>(v, k, L, C.Dinv, scr, lane, l7, Lr, dinv, Wsh) && lane == 0) set_fail(C.flags);
+      double wcol[7];
+      if (diag_factor<true>(v, k, L, C.Dinv, scr, lane, l7, wcol, Wsh) && lane == 0) set_fail(C.flags);
       double bb = C.y[(size_t)k * 7 + lane7];
       bb = sub_matvec<true, false, true>(bb, L, dtr_slot, dtr_p, q0, q1, C.y, lane7, lane49, lane, stg);
-      fwd_solve_store<true>(bb, Lr, dinv, C.y + (size_t)k * 7, lane);
+      fwd_solve_store<true>(bb, wcol, scr, C.y + (size_t)k * 7, lane);
     }
     __syncthreads();  // W_k in LDS; the dependencies are final for every wave
     if (tid == 0) M3S_CSTAMP(0, k, 2);
@@ -2200,9 +2238,9 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       diag_updates_sc1(v, bb, L, dtr_slot, dtr_p, q0, q1, D.y, r7, c7, lane7, lane49, lane, stg, D.sdone, want, &ok);
       if (!ok && lane == 0) set_fail(D.flags);
       if (lane == 0) M3S_CSTAMP(0, k, 1);
-      double Lr[7][7], dinv[7];
-      if (diag_factor<true>(v, k, L, D.Dinv, scr, lane, l7, Lr, dinv) && lane == 0) set_fail(D.flags);
-      fwd_solve_store<true>(bb, Lr, dinv, D.y + (size_t)k * 7, lane);
+      double wcol[7];
+      if (diag_factor<true>(v, k, L, D.Dinv, scr, lane, l7, wcol) && lane == 0) set_fail(D.flags);
+      fwd_solve_store<true>(bb, wcol, scr, D.y + (size_t)k * 7, lane);
       if (lane == 0) M3S_CSTAMP(0, k, 2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -506,7 +506,8 @@ struct ResidualParams {
 // iterations read 12-20 B per pixel and never gather from KF i. Both the
 // gathering and the packed kernels go through make_pixin + pixel_contrib (same
 // formulas; the sums differ only by FMA-contraction rounding between kernels).
-//   points: {Xi.x, Xi.y, Xi.z, sq}          rays: {ri.x, ri.y, ri.z, |Xi|, sq}
+//   points: {Xi.x, Xi.y, Xi.z, sq}          rays: {Xi.x, Xi.y, Xi.z, sq} (the unit
+//   ray X_i / |X_i| and |X_i| are formed where they are used: 16 B per pixel)
 //   calib:  {(v_t << 16 | u_t) as bits, sq, log z_i}
 // sq = sqrt(q) if the match is valid (valid_match, q > Q_thresh, ci/cj >
 // C_thresh; calib also z_i > z_eps), else 0: a zero weight zeroes the
@@ -519,9 +520,9 @@ struct PixIn<0> {
   float v[4];
 };
 template <>
-struct PixIn<1> {
-  static constexpr int kPlanes = 5;
-  float v[5];
+struct PixIn<1> {  // {X_i, sq}: the unit ray and |X_i| are formed from X_i in pixel_contrib
+  static constexpr int kPlanes = 4;
+  float v[4];
 };
 template <>
 struct PixIn<2> {
@@ -533,11 +534,9 @@ template <int MODE>
 __device__ __forceinline__ PixIn<MODE> make_pixin(const ResidualParams &P, const float *Xi, bool ok,
                                                   float q, int u_t, int v_t) {
   PixIn<MODE> r;
-  if (MODE == 1) {  // ray_align_kernel :924-963
-    const float ni = fsqrt(Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2]);
-    const float ini = frcp(ni);
-    r.v[0] = Xi[0] * ini, r.v[1] = Xi[1] * ini, r.v[2] = Xi[2] * ini, r.v[3] = ni;
-    r.v[4] = ok ? fsqrt(q) : 0.0f;
+  if (MODE == 1) {  // ray_align_kernel :924-963 (the ray of X_i is formed per use)
+    r.v[0] = Xi[0], r.v[1] = Xi[1], r.v[2] = Xi[2];
+    r.v[3] = ok ? fsqrt(q) : 0.0f;
   } else if (MODE == 2) {  // calib_proj_kernel :1360-1405
     const bool vzi = Xi[2] > P.z_eps;
     const float li = flog(Xi[2]);
@@ -557,13 +556,15 @@ template <int MODE, typename ACC>
 __device__ __forceinline__ void pixel_contrib(ACC &acc, const ResidualParams &P, const PixIn<MODE> &in,
                                               const float *Y) {
   if constexpr (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
+    const float ni = fsqrt(in.v[0] * in.v[0] + in.v[1] * in.v[1] + in.v[2] * in.v[2]);
+    const float ini = frcp(ni);
     const float nj2 = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
     const float nj = fsqrt(nj2);
     const float inj = frcp(nj);
     const float rx = Y[0] * inj, ry = Y[1] * inj, rz = Y[2] * inj;
-    const float e0 = rx - in.v[0], e1 = ry - in.v[1], e2 = rz - in.v[2];
-    const float e3 = nj - in.v[3];
-    const float sq = in.v[4];
+    const float e0 = rx - in.v[0] * ini, e1 = ry - in.v[1] * ini, e2 = rz - in.v[2] * ini;
+    const float e3 = nj - ni;
+    const float sq = in.v[3];
     const float swr = P.inv_sig_a * sq;
     const float swd = P.inv_sig_b * sq;
     const float kr = swr * swr, kd = swd * swd;
@@ -703,12 +704,14 @@ template <int MODE, int NPL>
 __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParams &P, const f32x2 (&in)[NPL],
                                                const f32x2 (&Y)[3]) {
   if constexpr (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
+    const f32x2 ni = sqrt2(fma2(in[0], in[0], fma2(in[1], in[1], in[2] * in[2])));
+    const f32x2 ini = rcp2(ni);
     const f32x2 nj2 = fma2(Y[0], Y[0], fma2(Y[1], Y[1], Y[2] * Y[2]));
     const f32x2 nj = sqrt2(nj2);
     const f32x2 inj = rcp2(nj);
     const f32x2 rx = Y[0] * inj, ry = Y[1] * inj, rz = Y[2] * inj;
-    const f32x2 e0 = rx - in[0], e1 = ry - in[1], e2 = rz - in[2], e3 = nj - in[3];
-    const f32x2 swr = in[4] * P.inv_sig_a, swd = in[4] * P.inv_sig_b;
+    const f32x2 e0 = rx - in[0] * ini, e1 = ry - in[1] * ini, e2 = rz - in[2] * ini, e3 = nj - ni;
+    const f32x2 swr = in[3] * P.inv_sig_a, swd = in[3] * P.inv_sig_b;
     const f32x2 kr = swr * swr, kd = swd * swd;
     const f32x2 hk = splat2(P.huber_k);
     // huber(sw e) sw^2 = min(1, k / |sw e|) sw^2

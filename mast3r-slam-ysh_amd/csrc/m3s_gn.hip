@@ -154,9 +154,9 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
-  // target-side planes of every edge (5 planes = rays, the widest mode)
+  // target-side planes of every edge (4 planes = rays / points, the widest modes)
   L.planes = off;
-  off = align_up(off + sizeof(float) * 5 * (size_t)E * (size_t)HW, 256);
+  off = align_up(off + sizeof(float) * 4 * (size_t)E * (size_t)HW, 256);
   L.total = off;
   return L;
 }
@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
 #define M3S_PK_WAVES (M3S_PP ? 3 : 4)
 #endif
 #ifndef M3S_PK_WAVES_RAYS
-#define M3S_PK_WAVES_RAYS (M3S_PP ? 3 : 1)
+#define M3S_PK_WAVES_RAYS (M3S_PP ? 2 : 1)
 #endif
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_PK_WAVES)

@@ -4,7 +4,11 @@ roofline.traffic). Fabric read bytes = TCC_EA0_RDREQ_128B x 128 B + the other
 (64 B) requests x 64 B, the gfx950 counting of MI355X_MICROARCH.md (a 128-B
 request is tallied once); writes = TCC_EA0_WRREQ_64B x 64 B.
 
-usage: python tools/pmc_summary.py gpurun_out/pmc [kernel-substring] [out.json]"""
+usage: python tools/pmc_summary.py gpurun_out/pmc [kernel-substring] [out.json] [kf]
+
+The record carries the sha256 prefix of the library it was collected on and
+the keyframe count; bench.py reports it as roofline.traffic only for that
+same build and workload."""
 import csv
 import glob
 import json
@@ -14,7 +18,8 @@ from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 kern = sys.argv[2] if len(sys.argv) > 2 else "linearize_packed_kernel"
-out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_linearize_c3.json"
+out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc/linearize_c3.json"
+kf = int(sys.argv[4]) if len(sys.argv) > 4 else 32
 tot, disp = defaultdict(float), defaultdict(set)
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -26,7 +31,13 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
 avg = {c: tot[c] / len(disp[c]) for c in tot}
 rd128 = avg.get("TCC_EA0_RDREQ_128B_sum", 0.0)
 rd = avg.get("TCC_EA0_RDREQ_sum", 0.0)
+import hashlib  # noqa: E402
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+_lib = os.path.join(ROOT, "mast3r-slam-ysh_amd", "mast3r_slam_backends", "libm3s_gn.so")
 res = {
+    "lib_sha256_16": hashlib.sha256(open(_lib, "rb").read()).hexdigest()[:16],
+    "kf": kf,
     "note": "C3 (calib, 98 directed edges x 262144 px). Per-launch averages from rocprofv3 --pmc passes over "
             "bench.py (tools/pmc_bench.sh, one counter group per run; tools/pmc_summary.py). Fabric bytes = "
             "TCC_EA0_RDREQ_128B_sum x 128 B + the 64-B requests x 64 B; writes = TCC_EA0_WRREQ_64B_sum x 64 B.",

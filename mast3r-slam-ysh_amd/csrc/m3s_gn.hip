@@ -3750,6 +3750,18 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
     ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_j), M.rj.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
                          st) == hipSuccess;
   }
+  // Test hook for the bounded waits (tests/test_gpu_backend.py): drop one item
+  // of sparse_llt_kernel's dispatch list, so the items that read its blocks
+  // wait on a flag that is never set; the waits time out and the iteration
+  // ends as a solve failure (dx = 0) instead of hanging.
+  if (const char *e = std::getenv("M3S_DEBUG_DROP_ITEM"); e && M.sparse && !M.h_plan.empty()) {
+    const int d = std::atoi(e);
+    int32_t *wp = M.h_plan.data() + M.img.off_wave_ptr, *wi = M.h_plan.data() + M.img.off_witems;
+    if (d >= 0 && d < wp[1]) {
+      for (int t = d; t + 1 < wp[1]; t++) wi[t] = wi[t + 1];
+      wp[1] -= 1;
+    }
+  }
   if (M.sparse && !M.h_plan.empty())
     ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.plan), M.h_plan.data(), sizeof(int32_t) * M.h_plan.size(),
                          hipMemcpyHostToDevice, st) == hipSuccess;

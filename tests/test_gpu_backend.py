@@ -173,6 +173,29 @@ def test_gn_singular_system_zero_dx(be):
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
 
 
+def test_gn_broken_plan_times_out_as_solve_failure(be, monkeypatch):
+    """A plan bug must end as a solve failure, never a hang (the LLT's flag
+    waits are bounded). M3S_DEBUG_DROP_ITEM removes the first item of the
+    dispatch list (a leaf DIAG): the items reading its blocks time out, the
+    iteration reports INFO_SOLVE_FAIL with dx = 0 and the poses untouched."""
+    import time
+
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(12, 24, 32, seed=37)
+    monkeypatch.setenv("M3S_DEBUG_DROP_ITEM", "0")
+    t0 = time.time()
+    T_gpu, dx, info = run_gpu(be, "rays", g, 1, 0.0)
+    dt = time.time() - t0
+    assert info[be.INFO_SOLVE_FAIL] == 1 and info[be.INFO_ITERS] == 1
+    assert np.all(dx == 0)
+    np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
+    assert dt < 60.0
+    monkeypatch.delenv("M3S_DEBUG_DROP_ITEM")
+    T_ok, _, info = run_gpu(be, "rays", g, 1, 0.0)  # the same graph, intact plan
+    assert info[be.INFO_SOLVE_FAIL] == 0 and not np.array_equal(T_ok, g.T_init.data.numpy())
+
+
 def test_gn_bad_edge_ids_flagged(be):
     """More unique ids than poses -> flagged, nothing computed (the reference
     would read out of bounds)."""

@@ -93,9 +93,14 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 // rows (n + 1 <= 16 kTailMaxT) and its scratch (dense bordered tail, L tiles,
 // W_k); see the kernel
 constexpr int kTailMaxT = 32;
-inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cyc_kernel)
+inline size_t tail_gran_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y', LgT, then the granules
   const size_t nmax = 16 * kTailMaxT;
   return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2 + (size_t)kTailMaxT * 256 + nmax;
+}
+inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cyc_kernel)
+  const size_t nmax = 16 * kTailMaxT;
+  // + the tagged-granule copy of the L tiles (tail_cyc_kernel hand-offs, 16 B per entry)
+  return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 4 + (size_t)kTailMaxT * 256 + nmax;
 }
 
 struct Layout {
@@ -2445,89 +2450,105 @@ __device__ __forceinline__ double tail_entry(const TailArgs &A, int n, int i, in
   return (j >= n && i == j) ? 1.0 : v;
 }
 
-// Diagonal tile from Dg (one wave): L_kk (Cholesky by rows, lane r < 16 holds
-// row r, pivots broadcast by readlane), W_k = L_kk^-1 -> Wk, and for the tile
-// that holds the RHS row, y' of its columns -> yv_k. Columns >= jv (padding,
-// the RHS row's own column) are identity. Returns true on a non-positive
-// pivot (computed on with pivot 1; the step becomes dx = 0).
-#ifdef M3S_TAIL_STAMPS
-__device__ int64_t *g_tail_stamp;
-#define M3S_DSTAMP(i) if (lane == 0 && g_tail_stamp) g_tail_stamp[i] = wall_clock64();
-#else
-#define M3S_DSTAMP(i)
-#endif
-template <bool FULL>  // FULL: jv == 16 (every tile column but possibly the last)
-__device__ __forceinline__ bool tail_diag_t(const double (*Dg)[17], double (*Wk)[17], double *yv_k, int jv,
-                                            int rhs_row, int lane) {
+// Diagonal tile (one wave, round 2): the tile stays in the MFMA C layout it
+// was accumulated in (lane l, register r = A[(l >> 4) + 4 r][l & 15]) and is
+// factored in four steps of 4 columns on the f64 MFMA. Step b: the 4x4 block
+// D_b goes to every lane through LDS (the only LDS round trip of the step);
+// every lane factors it in registers (L_D, W_D = L_D^-1); the panel
+// P = A[:, 4b..4b+3] W_D^T is ONE MFMA (W_D x register b of the tile, which
+// is the B operand as it stands, and the result lands in A-operand order);
+// the trailing update A -= P P^T is one more. W = L^-1 is accumulated as the
+// product of the elementary block-column inverses (two MFMAs per step, off
+// the critical path). Round 1's by-rows form broadcast every column through
+// LDS and ran ~2000 f64 instructions on one wave (~4 us per tile; this form
+// is ~4x fewer). Padding columns / rows (>= jv, incl. the RHS row's own
+// column) are identity; the RHS row's panel values are y' (-> yv_k). W ->
+// Wk[16][17] (row-major). Returns true on a non-positive pivot (computed on
+// with pivot 1; the step becomes dx = 0).
+template <bool FULL>  // FULL: jv == 16 (every tile column but possibly the last): no padding masks
+__device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row,
+                                                 int lane) {
   if (FULL) jv = 16;
-  __shared__ double colb[16];
-  // One pass: right-looking Cholesky by rows (lane r holds row r) and, with
-  // the same broadcast column of L, W = L^-1 by columns (lane c holds column
-  // c): at step j, W[j][c] = s_j[c] / L_jj is final and the pending s_r[c]
-  // (r > j) lose L[r][j] W[j][c]. The two sums keep their order (mm
-  // ascending); the rank-1 update is unmasked (upper-triangle entries are
-  // never read before step c zeroes them).
-  const int lr = lane & 15;
-  M3S_DSTAMP(110)
-  double a[16], sw[16], w[16];
+  __shared__ double xd[4][16], xw[4][16];
+  const int lr = lane & 15, lk = lane >> 4;
+  f64x4 M;  // W accumulator, identity
 #pragma unroll
-  for (int c = 0; c < 16; c++) a[c] = Dg[lr][c];
-#pragma unroll
-  for (int r = 0; r < 16; r++) sw[r] = (r == lane) ? 1.0 : 0.0;
-  // Branch-free: padding / RHS columns j >= jv become identity columns (and
-  // identity W rows) by selects, so their rank-1 updates are exact no-ops
-  // (no divergent control flow that would shuffle the register arrays).
+  for (int r = 0; r < 4; r++) M[r] = (lk + 4 * r == lr) ? 1.0 : 0.0;
   bool bad = false;
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const bool real = FULL || j < jv;
-    double d = readlane_d(a[j], j);
-    bad |= real && !(d > 0.0);
-    d = (real && d > 0.0) ? d : 1.0;
-    const double inv = rsqrt_nr(d);
-    // column j scaled on every lane: lane j holds the pivot itself (d * inv
-    // = L_jj), lanes below hold L_rj; the lanes above keep finite upper-
-    // triangle values that no later step reads (no lane masks, which the
-    // compiler would keep live for all 16 steps)
-    const double aj = a[j] * inv;
-    if (FULL) {
-      a[j] = aj;
-      w[j] = sw[j] * inv;
-    } else {
-      const double id = (lane == j) ? 1.0 : 0.0;
-      a[j] = real ? aj : id;
-      w[j] = real ? sw[j] * inv : id;
-    }
-    // column j of L to every lane through LDS (readlane broadcasts of 15
-    // doubles per step spill SGPRs)
-    if (lane < 16) colb[lane] = a[j];
+  for (int b = 0; b < 4; b++) {
+    const int c0 = 4 * b;
+    // D_b[i][j] = A[c0 + i][c0 + j]: register b of the lanes with column lr in the block
+    if (lr >= c0 && lr < c0 + 4) xd[b][4 * lk + lr - c0] = a[b];
     wave_lds_fence();
+    bool real[4];
 #pragma unroll
-    for (int c = j + 1; c < 16; c++) {
-      const double lcj = colb[c];
-      a[c] -= a[j] * lcj;
-      sw[c] -= lcj * w[j];
+    for (int m = 0; m < 4; m++) real[m] = FULL || c0 + m < jv;
+    double D[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) {
+        const double v = xd[b][4 * i + j];
+        D[i][j] = (real[i] && real[j]) ? v : (i == j ? 1.0 : 0.0);
+      }
+    // 4x4 Cholesky and W_D = L_D^-1, on every lane
+    double L[4][4], Wd[4][4], iv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      double d = D[j][j];
+      bad |= real[j] && !(d > 0.0);
+      d = d > 0.0 ? d : 1.0;
+      iv[j] = rsqrt_nr(d);
+#pragma unroll
+      for (int i = j + 1; i < 4; i++) L[i][j] = D[i][j] * iv[j];
+#pragma unroll
+      for (int i = j + 1; i < 4; i++)
+#pragma unroll
+        for (int k = j + 1; k <= i; k++) D[i][k] -= L[i][j] * L[k][j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      Wd[i][i] = iv[i];
+#pragma unroll
+      for (int j = 0; j < i; j++) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = j; k < i; k++) s += L[i][k] * Wd[k][j];
+        Wd[i][j] = -s * iv[i];
+      }
+    }
+    // A operands: Wpad[lr][lk] = W_D[lr][lk] (lr < 4); A1[lr][lk] = (W_D - I)[lr - c0][lk] (lr in the
+    // block): W_D through LDS (every lane holds it; lane 0 writes, each lane reads its entry)
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) xw[b][4 * i + k] = k <= i ? Wd[i][k] : 0.0;
     }
     wave_lds_fence();
+    const double wpad = lr < 4 ? xw[b][4 * lr + lk] : 0.0;
+    const double a1 =
+        (lr >= c0 && lr < c0 + 4) ? xw[b][4 * (lr - c0) + lk] - (lr - c0 == lk ? 1.0 : 0.0) : 0.0;
+    // panel P[lr][lk] = L[lr][c0 + lk] (rows above the block and padding columns 0)
+    double p = __builtin_amdgcn_mfma_f64_16x16x4f64(wpad, a[b], f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0)[0];
+    p = (lr >= c0 && (FULL || c0 + lk < jv)) ? p : 0.0;
+    if (!FULL && lr == rhs_row && c0 + lk < jv) yv_k[c0 + lk] = p;
+    a = __builtin_amdgcn_mfma_f64_16x16x4f64(-p, p, a, 0, 0, 0);  // A -= P P^T
+    // W <- (elementary inverse of block column b) W: the block rows by W_D,
+    // then the real rows below lose P_below times them
+    const f64x4 Y = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, M[b], M, 0, 0, 0);
+    const double a2 = (lr >= c0 + 4 && (FULL || lr < jv)) ? -p : 0.0;
+    M = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, Y[b], Y, 0, 0, 0);
   }
-  M3S_DSTAMP(111)
-  if (lane == rhs_row) {
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-      if (j < jv) yv_k[j] = a[j];
-  }
-  M3S_DSTAMP(112)
-  if (lane < 16) {
-#pragma unroll
-    for (int r = 0; r < 16; r++) Wk[r][lane] = w[r];
-  }
-  M3S_DSTAMP(113)
+  for (int r = 0; r < 4; r++) Wk[lk + 4 * r][lr] = M[r];
   return bad;
 }
-__device__ __forceinline__ bool tail_diag(const double (*Dg)[17], double (*Wk)[17], double *yv_k, int jv, int rhs_row,
-                                          int lane) {
-  return jv == 16 ? tail_diag_t<true>(Dg, Wk, yv_k, jv, rhs_row, lane)
-                  : tail_diag_t<false>(Dg, Wk, yv_k, jv, rhs_row, lane);
+__device__ __forceinline__ bool tail_diag_mfma(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row,
+                                               int lane) {
+  return jv == 16 ? tail_diag_mfma_t<true>(a, Wk, yv_k, jv, rhs_row, lane)
+                  : tail_diag_mfma_t<false>(a, Wk, yv_k, jv, rhs_row, lane);
 }
 
 __device__ __forceinline__ int tail_tile(int I, int J) { return I * (I + 1) / 2 + J; }
@@ -2541,7 +2562,6 @@ __device__ __forceinline__ f64x4 tail_load(const double *Lg, int t, int lane) {
 __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
   if (A.flags[kFlagStop]) return;
   __shared__ double Wk[16][17];  // W_k of the current step
-  __shared__ double Dg[16][17];  // diagonal tile staging
   __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
   __shared__ int fail_s;
   const int n = 7 * A.nc;
@@ -2555,7 +2575,6 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
   __syncthreads();
 #ifdef M3S_TAIL_STAMPS
   int64_t *stamp = reinterpret_cast<int64_t *>(Wg + (size_t)kTailMaxT * 256);
-  if (tid == 0) g_tail_stamp = stamp;
 #define M3S_STAMP(i) if (tid == 0) stamp[i] = wall_clock64();
 #else
 #define M3S_STAMP(i)
@@ -2611,12 +2630,9 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
 #undef M3S_TAIL_UPD
     M3S_STAMP(1 + 3 * k)
     if (wave == 0) {  // diag: tile (k, k) is wave 0's u = 0
-#pragma unroll
-      for (int r = 0; r < 4; r++) Dg[lr][lk + 4 * r] = acc[0][r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (tail_diag(Dg, Wk, yv + 16 * k, min(16, n - 16 * k), In == k ? rn : -1, lane) && lane == 0) fail_s = 1;
+      if (tail_diag_mfma(acc[0], Wk, yv + 16 * k, min(16, n - 16 * k), In == k ? rn : -1, lane) && lane == 0)
+        fail_s = 1;
+      wave_lds_fence();
       if (lane < 16) {
 #pragma unroll
         for (int r = 0; r < 16; r++) Wg[(size_t)k * 256 + r * 16 + lane] = Wk[r][lane];
@@ -2713,12 +2729,13 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
 // KFs). The last workgroup then runs the back-substitution L^T x = y' over
 // the published tiles (sc1 loads).
 struct TailSync {
-  int32_t *tflag;    // [TC] epoch flags: tile column published
-  int32_t *tflag_e;  // [TC] epoch flags: its first sub-diagonal tile L(J+1, J) published
+  int32_t *tflag;    // [TC] epoch flags: tile column published (W_J, y'_J, the LgT tiles: back-substitution)
   int epoch;
   double *ypg;     // y' of every tile column [16 TC]
   double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout (back-substitution A operands)
+  double *LgG;     // the L tiles as tagged granules, [tile][64][4] x {double, epoch tag, 0} (16 B; zeroed per call)
 };
+constexpr size_t kTailGranBytes = (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 64 * 4 * 16;
 
 __device__ __forceinline__ f64x4 ld_sc1_f64x4(const double *p) {
   f64x4 v;
@@ -2731,12 +2748,50 @@ __device__ __forceinline__ void st_sc1_f64x4(double *p, f64x4 v) {
   for (int r = 0; r < 4; r++) st_sc1(p + r, v[r]);
 }
 
+// Tagged-granule tile hand-off (MI355X_MICROARCH.md, handoff-1to1 / R2): each
+// entry is one 16-B write-through store {value, epoch tag}, read back by a
+// 16-B sc1 buffer load; the consumer checks the tags, so there is no flag, no
+// producer drain and no second round trip (flag, then payload).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+struct GranTile {
+  u32x4 v[4];
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(double *p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)kTailGranBytes, 0x00020000);
+}
+__device__ __forceinline__ void gran_load(__amdgpu_buffer_rsrc_t R, int tile, int lane, GranTile &g) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) g.v[r] = __builtin_amdgcn_raw_buffer_load_b128(R, ((tile * 64 + lane) * 4 + r) * 16, 0, 16);
+}
+__device__ __forceinline__ bool gran_ready(const GranTile &g, int want) {  // wave-uniform
+  const bool ok = g.v[0].z == (unsigned)want && g.v[1].z == (unsigned)want && g.v[2].z == (unsigned)want &&
+                  g.v[3].z == (unsigned)want;
+  return __ballot(!ok) == 0;
+}
+__device__ __forceinline__ f64x4 gran_val(const GranTile &g) {
+  f64x4 d;
+#pragma unroll
+  for (int r = 0; r < 4; r++) d[r] = __longlong_as_double((long long)(((unsigned long long)g.v[r].y << 32) | g.v[r].x));
+  return d;
+}
+__device__ __forceinline__ void gran_store(__amdgpu_buffer_rsrc_t R, int tile, int lane, f64x4 d, int want) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(d[r]);
+    const u32x4 w = {(unsigned)(b & 0xffffffffu), (unsigned)(b >> 32), (unsigned)want, 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(w, R, ((tile * 64 + lane) * 4 + r) * 16, 0, 16);
+  }
+}
+
+// Round 2: the L tiles go from workgroup to workgroup as tagged granules
+// (one hop = one store + one polled load), the panel follows the updates
+// without a workgroup barrier (waves 1..3 wait for W_J on an LDS flag), and
+// the column flag only guards what the back-substitution reads.
 __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, TailSync S) {
   if (A.flags[kFlagStop]) return;
   __shared__ double Wk[16][17];
-  __shared__ double Dg[16][17];
   __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
-  __shared__ int fail_s;
+  __shared__ int fail_s, wready;
   const int n = 7 * A.nc;
   const int TC = (n + 15) / 16, TR = (n + 16) / 16;
   const int In = n / 16, rn = n - 16 * In;
@@ -2744,7 +2799,8 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
   const int lr = lane & 15, lk = lane >> 4;
   const int J = blockIdx.x;
   const int want = S.epoch + 1;
-  double *Lg = A.Lg, *Wg = A.Wg;
+  double *Wg = A.Wg;
+  const __amdgpu_buffer_rsrc_t R = gran_rsrc(S.LgG);
   // rows: wave 0 holds only the diagonal tile (its factor is the critical
   // path), waves 1..3 the rows below it, I = J + w + 3 u
   constexpr int kRC = (kTailMaxT + 2) / 3;
@@ -2753,7 +2809,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     const int I = rowI(u);
     return I >= 0 && I < TR;
   };
-  if (tid == 0) fail_s = 0;
+  if (tid == 0) fail_s = 0, wready = 0;
   for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) yv[q] = 0.0;
   __syncthreads();
   f64x4 acc[kRC];
@@ -2766,84 +2822,131 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     }
     acc[u] = v;
   }
-  // updates from the finished columns, k ascending, each as soon as it is
-  // published. The diagonal tile takes its last one (k = J - 1) from the tile
-  // L(J, J-1) that workgroup J - 1 publishes early, so the diagonal factor
-  // starts while the rest of panel J - 1 is still on its way.
-  auto wait_flag_tail = [&](const int32_t *f) {
+  // updates from the finished columns, k ascending (the single-workgroup
+  // kernel's order: bitwise the same sums), each tile as soon as it lands
+  auto poll_tile = [&](int t, GranTile &g) {
     int spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+    for (;;) {
+      gran_load(R, t, lane, g);
+      if (gran_ready(g, want)) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kColSpins) break;
-    }
-    if (spins > kColSpins && lane == 0) fail_s = 1;
-  };
-  auto update_rows = [&](int k) {
-    const f64x4 rk = ld_sc1_f64x4(Lg + (size_t)tail_tile(J, k) * 256 + 4 * lane);
-    f64x4 ri[kRC];
-#pragma unroll
-    for (int u = 0; u < kRC; u++)
-      if (live(u)) ri[u] = ld_sc1_f64x4(Lg + (size_t)tail_tile(rowI(u), k) * 256 + 4 * lane);
-#pragma unroll
-    for (int u = 0; u < kRC; u++) {
-      if (live(u)) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-rk[q], ri[u][q], acc[u], 0, 0, 0);
+      if (++spins > kColSpins) {
+        if (lane == 0) fail_s = 1;
+        break;
       }
     }
   };
-  for (int k = 0; k + 1 < J; k++) {
-    wait_flag_tail(S.tflag + k);
-    update_rows(k);
-  }
-  if (J > 0) {
-    wait_flag_tail((wave == 0 ? S.tflag_e : S.tflag) + (J - 1));
-    update_rows(J - 1);
-  }
-  if (tid == 0) M3S_CSTAMP(2, J, 1);
-  if (wave == 0) {  // the diagonal tile
+  f64x4 rk_last = {0.0, 0.0, 0.0, 0.0};  // tile L(J, J-1): waves 1..3 apply column J - 1 row by row below
+  for (int k = 0; k < J; k++) {
+    GranTile gk;
+    poll_tile(tail_tile(J, k), gk);
+    const f64x4 rk = gran_val(gk);
+    if (wave == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) Dg[lr][lk + 4 * r] = acc[0][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (tail_diag(Dg, Wk, yv + 16 * J, min(16, n - 16 * J), In == J ? rn : -1, lane) && lane == 0) fail_s = 1;
-    wave_lds_fence();  // y' of the RHS row (lane rn) for the other lanes
+      for (int q = 0; q < 4; q++) acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(-rk[q], rk[q], acc[0], 0, 0, 0);
+    } else if (k + 1 == J) {
+      rk_last = rk;
+    } else {
+      // every row's tile of column k: all loads in flight at once, the rows
+      // that have landed are applied, the rest polled again
+      unsigned pend = 0;
+#pragma unroll
+      for (int u = 0; u < kRC; u++)
+        if (live(u)) pend |= 1u << u;
+      int spins = 0;
+      while (pend) {
+        GranTile g[kRC];
+#pragma unroll
+        for (int u = 0; u < kRC; u++)
+          if (pend & (1u << u)) gran_load(R, tail_tile(rowI(u), k), lane, g[u]);
+#pragma unroll
+        for (int u = 0; u < kRC; u++) {
+          if ((pend & (1u << u)) && gran_ready(g[u], want)) {
+            const f64x4 ri = gran_val(g[u]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-rk[q], ri[q], acc[u], 0, 0, 0);
+            pend &= ~(1u << u);
+          }
+        }
+        if (pend) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kColSpins) {
+            if (lane == 0) fail_s = 1;
+            break;
+          }
+        }
+      }
+    }
+  }
+  if (wave == 0) {  // the diagonal tile: factor, W_J
+    if (tid == 0) M3S_CSTAMP(2, J, 1);
+    if (tid == 0) M3S_CSTAMP(2, 600 + J, 0);
+    if (tail_diag_mfma(acc[0], Wk, yv + 16 * J, min(16, n - 16 * J), In == J ? rn : -1, lane) && lane == 0)
+      fail_s = 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // Wk (and y') before the flag
+    if (lane == 0) __hip_atomic_store(&wready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (tid == 0) M3S_CSTAMP(2, J, 2);
     if (lane < 16) {
 #pragma unroll
       for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)J * 256 + r * 16 + lane, Wk[r][lane]);
       if (In == J) st_sc1(S.ypg + 16 * J + lane, yv[16 * J + lane]);
     }
-  }
-  __syncthreads();  // W_J
-  if (tid == 0) M3S_CSTAMP(2, J, 2);
-  // panel L(I, J)^T = W_J A(I, J)^T; wave 1's first row (I = J + 1) first,
-  // published early for workgroup J + 1
+  } else {
+    // row by row, the sub-diagonal tile first: the update from column J - 1
+    // (as its tile lands), then the panel tile L(I, J)^T = W_J A(I, J)^T,
+    // handed off as granules at once
+    bool have_w = false;
 #pragma unroll
-  for (int u = 0; u < kRC; u++) {
-    const int I = rowI(u);
-    if (live(u) && I > J) {
-      f64x4 d = {0.0, 0.0, 0.0, 0.0};
+    for (int u = 0; u < kRC; u++) {
+      const int I = rowI(u);
+      if (live(u)) {
+        if (J > 0) {
+          GranTile g;
+          poll_tile(tail_tile(I, J - 1), g);
+          const f64x4 ri = gran_val(g);
 #pragma unroll
-      for (int q = 0; q < 4; q++) d = __builtin_amdgcn_mfma_f64_16x16x4f64(Wk[lr][4 * q + lk], acc[u][q], d, 0, 0, 0);
-      st_sc1_f64x4(Lg + (size_t)tail_tile(I, J) * 256 + 4 * lane, d);
-      if (I == In && lr == rn) {  // y' of this column from the RHS row
+          for (int q = 0; q < 4; q++) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-rk_last[q], ri[q], acc[u], 0, 0, 0);
+        }
+        if (!have_w) {
+          int spins = 0;
+          while (__hip_atomic_load(&wready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
+                 spins < (1 << 20)) {
+            __builtin_amdgcn_s_sleep(1);
+            spins++;
+          }
+          if (spins >= (1 << 20) && lane == 0) fail_s = 1;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          have_w = true;
+        }
+        f64x4 d = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J + lk + 4 * r, d[r]);
+        for (int q = 0; q < 4; q++) d = __builtin_amdgcn_mfma_f64_16x16x4f64(Wk[lr][4 * q + lk], acc[u][q], d, 0, 0, 0);
+        gran_store(R, tail_tile(I, J), lane, d, want);
+        if (I == J + 1 && tid == 64) M3S_CSTAMP(2, J, 0);
+        if (I == In && lr == rn) {  // y' of this column from the RHS row
+#pragma unroll
+          for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J + lk + 4 * r, d[r]);
+        }
       }
-      if (I < TC) {  // L(I, J) itself (operands swapped: A(I, J) W^T) for the back-substitution
+    }
+    // L(I, J) itself (operands swapped: A(I, J) W^T) for the back-substitution,
+    // after every hand-off of this wave (16-B write-through stores)
+    const __amdgpu_buffer_rsrc_t RT =
+        __builtin_amdgcn_make_buffer_rsrc(S.LgT, 0, kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 8, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < kRC; u++) {
+      const int I = rowI(u);
+      if (live(u) && I < TC) {
         f64x4 dt = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-          dt = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[u][q], Wk[lr][4 * q + lk], dt, 0, 0, 0);
-        st_sc1_f64x4(S.LgT + (size_t)tail_tile(I, J) * 256 + 4 * lane, dt);
-      }
-      if (I == J + 1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-          __hip_atomic_store(S.tflag_e + J, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          M3S_CSTAMP(2, J, 0);
-        }
+        for (int q = 0; q < 4; q++) dt = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[u][q], Wk[lr][4 * q + lk], dt, 0, 0, 0);
+        const unsigned long long b0 = __double_as_longlong(dt[0]), b1 = __double_as_longlong(dt[1]),
+                                 b2 = __double_as_longlong(dt[2]), b3 = __double_as_longlong(dt[3]);
+        const u32x4 w0 = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
+        const u32x4 w1 = {(unsigned)b2, (unsigned)(b2 >> 32), (unsigned)b3, (unsigned)(b3 >> 32)};
+        const int off = (tail_tile(I, J) * 256 + 4 * lane) * 8;
+        __builtin_amdgcn_raw_buffer_store_b128(w0, RT, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(w1, RT, off + 16, 0, 16);
       }
     }
   }
@@ -2862,6 +2965,17 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
   // the other waves through LDS with a flag: no workgroup barrier per step.
   // The same sums in the same order as tail_llt_kernel's loop.
   __shared__ int xflag[kTailMaxT];
+  if (wave == 0) {  // every column's W, y' and LgT tiles are out (column flags, one per lane)
+    int spins = 0;
+    while (__ballot(lane < TC && __hip_atomic_load(S.tflag + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kColSpins) {
+        if (lane == 0) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
   for (int q = tid; q < 16 * TC; q += 64 * kTailNW) yv[q] = ld_sc1(S.ypg + q);
   for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) xv[q] = 0.0;
   if (tid < kTailMaxT) xflag[tid] = 0;
@@ -3458,10 +3572,10 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         if (tail_cyc()) {
           TailSync Y;
           Y.tflag = cs + 2 * (meta.m + 1) + 16 + Ly.slot_cap;
-          Y.tflag_e = Y.tflag + kTailMaxT;
           Y.epoch = meta.epoch;
           Y.ypg = T.Wg + (size_t)kTailMaxT * 256;
           Y.LgT = Y.ypg + 16 * kTailMaxT;
+          Y.LgG = tail + tail_gran_offset_doubles();
           const int TC = (7 * meta.nc + 15) / 16;
           tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
         } else {
@@ -3742,6 +3856,9 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.flags), M.h_flags, sizeof M.h_flags, hipMemcpyHostToDevice, st) == hipSuccess;
   ok &= hipMemsetAsync(at<uint32_t>(ws, Ly.edge_cnt), 0, edge_cnt_bytes(E), st) == hipSuccess;
   ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
+  if (M.nc > 0)  // the tail's tagged granules: no tag of an earlier call may match this call's epochs
+    ok &= hipMemsetAsync(at<double>(ws, Ly.tail) + tail_gran_offset_doubles(), 0,
+                         sizeof(double) * (tail_scratch_doubles() - tail_gran_offset_doubles()), st) == hipSuccess;
   M.epoch = 0;
   ok &= hipMemcpyAsync(a->info, M.h_info, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
   if (E > 0) {

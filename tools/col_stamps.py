@@ -91,5 +91,6 @@ if TC:
     for J in range(TC):
         a, b, c = ((T[J, 1:4] - tt0) / 100.0)
         e = (T[J, 0] - tt0) / 100.0 if J + 1 < TC else float("nan")
-        print(f"  J={J:2d} {a:8.2f} {b:8.2f} {e:8.2f} {c:8.2f}")
+        dg = (T[J, 2] - T[600 + J, 0]) / 100.0 if T[600 + J, 0] else float("nan")
+        print(f"  J={J:2d} {a:8.2f} {b:8.2f} {e:8.2f} {c:8.2f}   (diagonal factor alone {dg:5.2f})")
     print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")

@@ -11,7 +11,7 @@ timed iteration, so each one solves the same real system. The all-gather
 
 Prints t_iter(N) and the predicted efficiency t_iter(1) / t_iter(N).
 
-env: MODES=calib,rays  WORLDS=1,2,4,8  HW_SIDE=512  REPS=20
+env: MODES=calib,rays  WORLDS=1,2,4,8  HW_SIDE=512  REPS=20  M3S_LIB=variants/lib_X.so
 """
 import os
 import sys
@@ -21,6 +21,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "mast3r-slam-ysh_amd")]
 import torch  # noqa: E402
 
 import mast3r_slam_backends as be  # noqa: E402
+
+if os.environ.get("M3S_LIB"):  # a library variant (tools/mkvar.sh) for A/B
+    be._lib = be._load(os.path.abspath(os.environ["M3S_LIB"]))
 from mast3r_slam_amd import synthetic  # noqa: E402
 from mast3r_slam_amd.distributed import HipOps, edge_slice  # noqa: E402
 

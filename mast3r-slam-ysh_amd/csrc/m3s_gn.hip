@@ -2888,7 +2888,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     if (tid == 0) M3S_CSTAMP(2, J, 2);
     if (lane < 16) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)J * 256 + r * 16 + lane, Wk[r][lane]);
+      for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)J * 256 + lane * 16 + r, Wk[r][lane]);  // W^T
       if (In == J) st_sc1(S.ypg + 16 * J + lane, yv[16 * J + lane]);
     }
   } else {
@@ -2976,78 +2976,128 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     }
   }
   __syncthreads();
-  for (int q = tid; q < 16 * TC; q += 64 * kTailNW) yv[q] = ld_sc1(S.ypg + q);
+  if (tid == 0) M3S_CSTAMP(2, 698, 0);
+  // every W_K^T to LDS (rows padded to 17: conflict-free column reads)
+  __shared__ double WlT[kTailMaxT * 16 * 17];
+  {  // all loads in flight at once (16-B sc1 buffer loads; out of range past TC reads zeros)
+    constexpr int kWL = kTailMaxT * 256 / (2 * 64 * kTailNW);
+    const __amdgpu_buffer_rsrc_t RW = __builtin_amdgcn_make_buffer_rsrc(Wg, 0, kTailMaxT * 256 * 8, 0x00020000);
+    u32x4 wv[kWL];
+#pragma unroll
+    for (int i = 0; i < kWL; i++) {
+      const int q2 = 2 * (tid + 64 * kTailNW * i);
+      wv[i] = __builtin_amdgcn_raw_buffer_load_b128(RW, q2 < 256 * TC ? q2 * 8 : 0x7fffff00, 0, 16);
+    }
+    double yl[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int q = tid + 64 * kTailNW * i;
+      yl[i] = q < 16 * TC ? ld_sc1(S.ypg + q) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kWL; i++) {
+      const int q2 = 2 * (tid + 64 * kTailNW * i);
+      WlT[(q2 >> 4) * 17 + (q2 & 15)] = __longlong_as_double((long long)(((unsigned long long)wv[i].y << 32) | wv[i].x));
+      WlT[(q2 >> 4) * 17 + (q2 & 15) + 1] =
+          __longlong_as_double((long long)(((unsigned long long)wv[i].w << 32) | wv[i].z));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int q = tid + 64 * kTailNW * i;
+      if (q < 16 * TC) yv[q] = yl[i];
+    }
+  }
   for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) xv[q] = 0.0;
   if (tid < kTailMaxT) xflag[tid] = 0;
   __syncthreads();
-  // y_J -= L(K, J)^T x_K on the f64 MFMA: A = L(K, J)^T from the LgT tile
-  // (operand order: one 32-B load per lane), B = x_K in every column, so
-  // D[m][.] = (L^T x)[m]; lanes 0, 16, 32, 48 hold the 16 results.
+  // y_J -= L(K, J)^T x_K from the LgT tile (operand order: 32 B per lane).
+  // The operands of the next step are in flight while this one runs: every
+  // load is a 16-B sc1 buffer load issued unconditionally (rows a step does
+  // not need read out of range, which returns zeros without a memory access),
+  // so each step issues the same number of loads and the compiler waits for
+  // exactly the older step's (24 per wave, two steps = 48 < the 63 vmcnt).
+  // Per step K the owner of row K - 1 applies x_K to that row first and forms
+  // x_{K-1} at once (the chain per step is one tile update + one 16-term
+  // dot product), then applies x_K to its other rows. Each row still takes
+  // its updates in decreasing K (the same sums).
   constexpr int kTW = (kTailMaxT + kTailNW - 1) / kTailNW;  // tile rows J' of one wave
-  constexpr int kRing = 3;  // steps of tile loads in flight
+  constexpr int kRing = 3;
+  const __amdgpu_buffer_rsrc_t RT =
+      __builtin_amdgcn_make_buffer_rsrc(S.LgT, 0, kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 8, 0x00020000);
+  constexpr int kFar = 0x7fffff00;  // out of range
   f64x4 lt[kRing][kTW];
-  double wb[kRing][16];
+  auto ld2 = [&](int off, double &x0, double &x1) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(RT, off, 0, 16);
+    x0 = __longlong_as_double((long long)(((unsigned long long)v.y << 32) | v.x));
+    x1 = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
+  };
   auto bs_load = [&](int K, int slot) {
 #pragma unroll
     for (int t = 0; t < kTW; t++) {
       const int Jc = wave + kTailNW * t;
-      if (Jc < K) lt[slot][t] = ld_sc1_f64x4(S.LgT + (size_t)tail_tile(K, Jc) * 256 + 4 * lane);
-    }
-    if (K % kTailNW == wave && lane < 16) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) wb[slot][i] = ld_sc1(Wg + (size_t)K * 256 + i * 16 + lane);
+      const int off = (K >= 0 && Jc < K) ? (tail_tile(K, Jc) * 256 + 4 * lane) * 8 : kFar;
+      double x0, x1, x2, x3;
+      ld2(off, x0, x1);
+      ld2(off + 16, x2, x3);
+      lt[slot][t] = f64x4{x0, x1, x2, x3};
     }
   };
-  // step K uses ring slot (TC - 1 - K) % kRing: compile-time in the unrolled loop
+  auto form_x = [&](int K) {  // the owner of row K, all of whose updates are in
+    const int jv = min(16, n - 16 * K);
+    if (lane < 16) {
+      double x = 0.0;
 #pragma unroll
-  for (int d = 0; d < kRing; d++)
-    if (TC - 1 - d >= 0) bs_load(TC - 1 - d, d);
+      for (int i = 0; i < 16; i++) x += WlT[(K * 16 + lane) * 17 + i] * yv[16 * K + i];
+      xv[16 * K + lane] = lane < jv ? x : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) M3S_CSTAMP(2, 700 + K, 0);
+  };
+#pragma unroll
+  for (int d = 0; d < kRing; d++) bs_load(TC - 1 - d, d);
+  if (tid == 0) M3S_CSTAMP(2, 699, 0);
+  if ((TC - 1) % kTailNW == wave) form_x(TC - 1);
   for (int K0 = TC - 1; K0 >= 0; K0 -= kRing) {
 #pragma unroll
     for (int d = 0; d < kRing; d++) {
       const int K = K0 - d;
-      if (K < 0) break;
-      const int jv = min(16, n - 16 * K);
-      if (K % kTailNW == wave) {  // the owner of row K: its updates are all in
-        if (lane < 16) {
-          double x = 0.0;
-#pragma unroll
-          for (int i = 0; i < 16; i++) x += wb[d][i] * yv[16 * K + i];
-          xv[16 * K + lane] = lane < jv ? x : 0.0;
+      if (K >= 0) {
+        if (K % kTailNW != wave) {  // (the owner formed x_K itself, in the step before)
+          int spins = 0;
+          while (__hip_atomic_load(xflag + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
+                 spins < (1 << 22))
+            spins++;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        int spins = 0;
-        while (__hip_atomic_load(xflag + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && spins < (1 << 22))
-          spins++;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      }
-      double xb[4];
+        double xb[4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) xb[q] = xv[16 * K + 4 * q + lk];
-      f64x4 u[kTW];
+        for (int q = 0; q < 4; q++) xb[q] = xv[16 * K + 4 * q + lk];
 #pragma unroll
-      for (int t = 0; t < kTW; t++) {
-        const int Jc = wave + kTailNW * t;
-        u[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-        if (Jc < K) {
+        for (int pass = 0; pass < 2; pass++) {
 #pragma unroll
-          for (int q = 0; q < 4; q++) u[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(lt[d][t][q], xb[q], u[t], 0, 0, 0);
-        }
-      }
-      if (K - kRing >= 0) bs_load(K - kRing, d);
-      if (lr == 0) {
+          for (int t = 0; t < kTW; t++) {
+            const int Jc = wave + kTailNW * t;
+            if (pass == 0 ? Jc == K - 1 : Jc < K - 1) {
+              // (L^T x)[m], m = lr: lane l holds L(K,Jc)^T[lr][lk + 4q]; the 4 lanes of
+              // one m add their partial sums (VALU: the MFMA form spent 15/16 of its work
+              // on copies of x)
+              double u = 0.0;
 #pragma unroll
-        for (int t = 0; t < kTW; t++) {
-          const int Jc = wave + kTailNW * t;
-          if (Jc < K) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) yv[16 * Jc + lk + 4 * r] -= u[t][r];
+              for (int q = 0; q < 4; q++) u += lt[d][t][q] * xb[q];
+              u += __shfl_xor(u, 16);
+              u += __shfl_xor(u, 32);
+              if (lane < 16) yv[16 * Jc + lane] -= u;
+              if (pass == 0) {
+                wave_lds_fence();  // row K - 1's y' before this wave reads it
+                form_x(K - 1);
+              }
+            }
           }
         }
+        wave_lds_fence();
       }
-      wave_lds_fence();  // this wave's y' rows before it (as owner) reads them
+      bs_load(K - kRing, d);
     }
   }
   __syncthreads();  // every x_K

@@ -94,3 +94,6 @@ if TC:
         dg = (T[J, 2] - T[600 + J, 0]) / 100.0 if T[600 + J, 0] else float("nan")
         print(f"  J={J:2d} {a:8.2f} {b:8.2f} {e:8.2f} {c:8.2f}   (diagonal factor alone {dg:5.2f})")
     print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")
+    if T[699, 0]:
+        print(f"  back-substitution: flags seen {(T[698, 0] - tt0) / 100.0:.2f}, loop start {(T[699, 0] - tt0) / 100.0:.2f}; "
+              "x_K published at " + " ".join(f"{(T[700 + K, 0] - tt0) / 100.0:.2f}" for K in range(TC - 1, -1, -1)))

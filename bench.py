@@ -61,7 +61,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_PATH = os.path.join(ROOT, "profiles", "pmc", "linearize_c3.json")
+# shipped with the tree (profiles/ stays on the build host): the PMC record of the benched library
+PMC_PATH = os.path.join(ROOT, "pmc", "linearize_c3.json")
 SEED = 1003  # 1000 + config number
 
 
@@ -338,12 +339,15 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per
     b2b_ms = ev0.elapsed_time(ev1) / args.lin_reps
     achieved = bytes_alg / (lin_ms * 1e-3) / 1e9
     first_ms = sum(first) / len(first)
-    traffic, traffic_note = None, "no PMC record"
+    traffic, traffic_note, gather_traffic = None, "no PMC record", None
     if os.path.exists(PMC_PATH) and world == 1 and args.mode == "calib":
         rec = json.load(open(PMC_PATH))
         if rec.get("lib_sha256_16") == lib_digest() and rec.get("kf") == args.kf_per_gpu:
             traffic = rec.get("hbm_bytes_per_launch")
             traffic_note = rec.get("note", "PMC pass of this library build")
+            g = rec.get("gather") or {}
+            if g.get("lib_sha256_16") == rec.get("lib_sha256_16"):
+                gather_traffic = {"read": g.get("hbm_bytes_per_launch"), "write": g.get("hbm_write_bytes_per_launch")}
         else:
             traffic_note = "PMC record is of another library build: not reported"
     return {
@@ -366,6 +370,7 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per
             "avg_launch_ms": round(first_ms, 5),
             "achieved": round(bytes_alg / (first_ms * 1e-3) / 1e9, 1),
             "frac": round(bytes_alg / (first_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": gather_traffic,
         },
         "solve": {
             "kernels": "fp64 sparse LLT + retraction (sparse_llt_kernel [+ border_kernel]), stepwise "

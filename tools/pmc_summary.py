@@ -1,10 +1,13 @@
 """Per-launch averages of the PMC passes of tools/pmc_bench.sh for one kernel
--> profiles/pmc_linearize_c3.json (bench.py reads hbm_bytes_per_launch as
+-> pmc/linearize_c3.json (bench.py reads hbm_bytes_per_launch as
 roofline.traffic). Fabric read bytes = TCC_EA0_RDREQ_128B x 128 B + the other
 (64 B) requests x 64 B, the gfx950 counting of MI355X_MICROARCH.md (a 128-B
 request is tallied once); writes = TCC_EA0_WRREQ_64B x 64 B.
 
-usage: python tools/pmc_summary.py gpurun_out/pmc [kernel-substring] [out.json] [kf]
+usage: python tools/pmc_summary.py gpurun_out/pmc [kernel-substring] [out.json] [kf] [merge-key]
+
+With merge-key (e.g. "gather" for the first-iteration kernel "linearize_kernel<"), the
+summary is stored under that key of the existing out.json instead of replacing it.
 
 The record carries the sha256 prefix of the library it was collected on and
 the keyframe count; bench.py reports it as roofline.traffic only for that
@@ -18,8 +21,9 @@ from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 kern = sys.argv[2] if len(sys.argv) > 2 else "linearize_packed_kernel"
-out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc/linearize_c3.json"
+out = sys.argv[3] if len(sys.argv) > 3 else "pmc/linearize_c3.json"
 kf = int(sys.argv[4]) if len(sys.argv) > 4 else 32
+merge = sys.argv[5] if len(sys.argv) > 5 else None
 tot, disp = defaultdict(float), defaultdict(set)
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -47,5 +51,11 @@ res = {
     "dispatches_per_counter": {c: len(v) for c, v in disp.items()},
     "counters": avg,
 }
-json.dump(res, open(out, "w"), indent=1)
+os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+if merge:
+    base = json.load(open(out))
+    base[merge] = res
+    json.dump(base, open(out, "w"), indent=1)
+else:
+    json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: res[k] for k in ("hbm_bytes_per_launch", "hbm_write_bytes_per_launch")}))

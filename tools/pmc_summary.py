@@ -6,7 +6,7 @@ request is tallied once); writes = TCC_EA0_WRREQ_64B x 64 B.
 
 usage: python tools/pmc_summary.py gpurun_out/pmc [kernel-substring] [out.json] [kf] [merge-key]
 
-With merge-key (e.g. "gather" for the first-iteration kernel "linearize_kernel<"), the
+With merge-key (e.g. "gather" for the first-iteration kernel "linearize_kernel": rocprofv3 reports names without template arguments, and "linearize_packed_kernel" does not contain it), the
 summary is stored under that key of the existing out.json instead of replacing it.
 
 The record carries the sha256 prefix of the library it was collected on and

@@ -126,6 +126,15 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
   L.rank_j = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
+  // flags, ranks, linearize task table and sparse plan are contiguous: one
+  // H2D copy per call uploads them all (gn_prepare_impl)
+  const int64_t m0 = N > 1 ? N - 1 : 0;
+  L.tasks = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
+  L.slot_cap = std::min<int64_t>(m0 * (m0 + 1) / 2, 64 * m0 + 4096) + 1;
+  L.plan_cap = (int64_t(1) << 22) + 16 * E + 64 * m0;
+  L.plan = off;
+  off = align_up(off + sizeof(int32_t) * (size_t)L.plan_cap, 256);
   L.first = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(2 * E + 1), 256);
   L.edge_cnt = off;  // per-edge chunk arrival counters (fused finalize), zeroed per call
@@ -141,10 +150,6 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   const int64_t m = N > 1 ? N - 1 : 0;
   L.fin = off;
   off = align_up(off + sizeof(double) * 56 * (size_t)(E + 1), 256);
-  L.slot_cap = std::min<int64_t>(m * (m + 1) / 2, 64 * m + 4096) + 1;
-  L.plan_cap = (int64_t(1) << 22) + 16 * E + 64 * m;
-  L.plan = off;
-  off = align_up(off + sizeof(int32_t) * (size_t)L.plan_cap, 256);
   L.Lblk = off;
   off = align_up(off + sizeof(double) * 49 * (size_t)L.slot_cap, 256);
   L.Dinv = off;
@@ -157,8 +162,6 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
   off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
-  L.tasks = off;
-  off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
   // target-side planes of every edge (4 planes = rays / points, the widest modes)
   L.planes = off;
   off = align_up(off + sizeof(float) * 4 * (size_t)E * (size_t)HW, 256);
@@ -3836,23 +3839,53 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
 // the ids, fetch or build the plan, and enqueue its upload. The host buffers
 // of every upload live in the workspace's registry entry until the next
 // prepare on that workspace (which syncs first), so nothing waits here.
+// Pinned host staging for the per-call transfers of gn_prepare_impl: the D2H
+// reads (K, ii, jj) and ONE H2D upload of flags | ranks | task table | plan
+// (contiguous in the workspace). Pageable copies were one staged,
+// host-synchronous transfer each (~7 per call); the event guards the upload
+// buffer until the previous call's copy has left it.
+struct Staging {
+  std::mutex mu;
+  char *down = nullptr, *up = nullptr;
+  size_t down_cap = 0, up_cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+Staging g_stage;
+bool pinned_reserve(char *&p, size_t &cap, size_t need) {
+  if (need <= cap) return true;
+  if (p) (void)hipHostFree(p);
+  p = nullptr, cap = 0;
+  const size_t n = std::max<size_t>(need + need / 2, 1 << 16);
+  if (hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault) != hipSuccess) return false;
+  cap = n;
+  return true;
+}
+
 int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
-  float hK[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // calib intrinsics, read with ii/jj
+  std::lock_guard<std::mutex> stage_lock(g_stage.mu);
+  if (!g_stage.ev && hipEventCreateWithFlags(&g_stage.ev, hipEventDisableTiming) != hipSuccess) return M3S_ELAUNCH;
+  if (g_stage.pending && hipEventSynchronize(g_stage.ev) != hipSuccess) return M3S_ELAUNCH;
+  g_stage.pending = false;
+  const int64_t E = a->E;
+  if (!pinned_reserve(g_stage.down, g_stage.down_cap, 64 + 2 * sizeof(int64_t) * (size_t)E)) return M3S_ELAUNCH;
+  float *hK = reinterpret_cast<float *>(g_stage.down);  // calib intrinsics, read with ii/jj
+  int64_t *hii = reinterpret_cast<int64_t *>(g_stage.down + 64), *hjj = hii + E;
+  for (int q = 0; q < 9; q++) hK[q] = 0.f;
   if (a->mode == M3S_MODE_CALIB &&
-      hipMemcpyAsync(hK, a->K, sizeof hK, hipMemcpyDeviceToHost, st) != hipSuccess)
+      hipMemcpyAsync(hK, a->K, sizeof(float) * 9, hipMemcpyDeviceToHost, st) != hipSuccess)
     return M3S_ELAUNCH;
   if (a->N > 1 && a->dx_out && hipMemsetAsync(a->dx_out, 0, sizeof(float) * 7 * (a->N - 1), st) != hipSuccess)
     return M3S_ELAUNCH;
-  const int64_t E = a->E;
-  std::vector<int64_t> hii(E), hjj(E);
-  if (E > 0 && (hipMemcpyAsync(hii.data(), a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(hjj.data(), a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess))
+  if (E > 0 && hipMemcpyAsync(hii, a->ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return M3S_ELAUNCH;
+  if (E > 0 && hipMemcpyAsync(hjj, a->jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st) != hipSuccess)
     return M3S_ELAUNCH;
   if (hipStreamSynchronize(st) != hipSuccess) return M3S_ELAUNCH;
   std::vector<int32_t> ri, rj;
-  const int nu = host_remap(hii.data(), hjj.data(), E, ri, rj);
+  const int nu = host_remap(hii, hjj, E, ri, rj);
   const bool bad = nu > a->N;
   const char *fd = std::getenv("M3S_DENSE");
   const bool force_dense = fd && fd[0] == '1';
@@ -3905,20 +3938,13 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   PlanMeta &M = g_reg[ws];
   M = std::move(meta);
   bool ok = true;
-  ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.flags), M.h_flags, sizeof M.h_flags, hipMemcpyHostToDevice, st) == hipSuccess;
   ok &= hipMemsetAsync(at<uint32_t>(ws, Ly.edge_cnt), 0, edge_cnt_bytes(E), st) == hipSuccess;
   ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
   if (M.nc > 0)  // the tail's tagged granules: no tag of an earlier call may match this call's epochs
     ok &= hipMemsetAsync(at<double>(ws, Ly.tail) + tail_gran_offset_doubles(), 0,
                          sizeof(double) * (tail_scratch_doubles() - tail_gran_offset_doubles()), st) == hipSuccess;
   M.epoch = 0;
-  ok &= hipMemcpyAsync(a->info, M.h_info, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
-  if (E > 0) {
-    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_i), M.h_ri.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
-                         st) == hipSuccess;
-    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.rank_j), M.rj.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice,
-                         st) == hipSuccess;
-  }
+
   // Test hook for the bounded waits (tests/test_gpu_backend.py): drop one item
   // of sparse_llt_kernel's dispatch list, so the items that read its blocks
   // wait on a flag that is never set; the waits time out and the iteration
@@ -3931,12 +3957,28 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       wp[1] -= 1;
     }
   }
-  if (M.sparse && !M.h_plan.empty())
-    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.plan), M.h_plan.data(), sizeof(int32_t) * M.h_plan.size(),
-                         hipMemcpyHostToDevice, st) == hipSuccess;
-  if (M.n_blocks > 0)
-    ok &= hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), M.tasks.data(), sizeof(int32_t) * M.tasks.size(),
-                         hipMemcpyHostToDevice, st) == hipSuccess;
+  // one upload: flags | rank_i | rank_j | tasks | plan (the layout keeps them
+  // in this order), then info (the caller's tensor) from the same buffer
+  const bool with_plan = M.sparse && !M.h_plan.empty();
+  const bool with_tasks = M.n_blocks > 0;
+  size_t n_up = with_plan ? Ly.plan - Ly.flags + sizeof(int32_t) * M.h_plan.size()
+                          : with_tasks ? Ly.tasks - Ly.flags + sizeof(int32_t) * M.tasks.size()
+                                       : Ly.rank_j - Ly.flags + sizeof(int32_t) * (size_t)E;
+  n_up = align_up(n_up, 16);
+  if (!pinned_reserve(g_stage.up, g_stage.up_cap, n_up + sizeof M.h_info)) return M3S_ELAUNCH;
+  char *up = g_stage.up;
+  memcpy(up, M.h_flags, sizeof M.h_flags);
+  if (E > 0) {
+    memcpy(up + (Ly.rank_i - Ly.flags), M.h_ri.data(), sizeof(int32_t) * E);
+    memcpy(up + (Ly.rank_j - Ly.flags), M.rj.data(), sizeof(int32_t) * E);
+  }
+  if (with_tasks) memcpy(up + (Ly.tasks - Ly.flags), M.tasks.data(), sizeof(int32_t) * M.tasks.size());
+  if (with_plan) memcpy(up + (Ly.plan - Ly.flags), M.h_plan.data(), sizeof(int32_t) * M.h_plan.size());
+  memcpy(up + n_up, M.h_info, sizeof M.h_info);
+  ok &= hipMemcpyAsync(at<char>(ws, Ly.flags), up, n_up, hipMemcpyHostToDevice, st) == hipSuccess;
+  ok &= hipMemcpyAsync(a->info, up + n_up, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
+  ok &= hipEventRecord(g_stage.ev, st) == hipSuccess;
+  g_stage.pending = ok;
   return ok ? M3S_OK : M3S_ELAUNCH;
 }
 

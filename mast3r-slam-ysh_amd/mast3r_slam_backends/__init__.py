@@ -298,10 +298,11 @@ def make_gn_args(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, K=None, *
     if jj.numel() != E or idx_ii2jj.numel() != E * HW or valid_match.numel() != E * HW or Q.numel() != E * HW:
         raise RuntimeError("edge tensors must be [E, HW(,1)] with E = ii.size(0)")
     dev = Xs.device
+    # no fill launches: m3s_gn_prepare zeroes dx and uploads info on the stream
     if dx is None:
-        dx = torch.zeros(max(N - 1, 0), 7, dtype=torch.float32, device=dev)
+        dx = torch.empty(max(N - 1, 0), 7, dtype=torch.float32, device=dev)
     if info is None:
-        info = torch.zeros(8, dtype=torch.int32, device=dev)
+        info = torch.empty(8, dtype=torch.int32, device=dev)
     ws_bytes = int(_lib.m3s_gn_workspace_size(N, HW, E))
     if workspace is None or workspace.numel() < ws_bytes:
         workspace = _workspace(ws_bytes, dev)

@@ -40,5 +40,3 @@ for k in range(TC):
     a, b, c = (st[1 + 3 * k:4 + 3 * k] - t0) / 100.0
     print(f"  k={k:2d}  {a:8.2f} {b:8.2f} {c:8.2f}")
 print(f"  back-substitution done {(st[100] - t0) / 100.0:.2f} us")
-d = (st[110:114] - st[110]) / 100.0
-print(f"  last diag: cholesky {d[1]:.2f} us, W {d[2] - d[1]:.2f} us, W store {d[3] - d[2]:.2f} us")

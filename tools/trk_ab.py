@@ -1,0 +1,13 @@
+import os, sys
+ROOT = "/root/repo" if os.path.exists("/root/repo") else os.getcwd()
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mast3r-slam-ysh_amd")]
+import torch
+import bench
+import mast3r_slam_backends as be
+from mast3r_slam_amd import synthetic
+dev = torch.device("cuda:0")
+for rnd in range(2):
+    for p in sys.argv[1:]:
+        be._lib = be._load(os.path.abspath(p))
+        r = bench.tracker_leg(be, synthetic, dev, 512, 512, reps=50)
+        print(os.path.basename(p), r["gn_iters_per_s"], r["ms_per_solve"], flush=True)

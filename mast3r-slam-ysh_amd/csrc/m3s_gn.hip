@@ -1726,6 +1726,9 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
   if (tid == 0) fail_s = 0, next_item = 0, next_col = 0, next_b0 = 0;
   __syncthreads();
+#if defined(M3S_LLT_EXIT) && M3S_LLT_EXIT == 1  // phase-timing builds only (tools/llt_phase_ab.py)
+  return;
+#endif
 
   // 1. factorisation + forward substitution as a dataflow over work items:
   // DIAG(k) (diagonal block and W_k = L_kk^-1, then the forward step of y_k),
@@ -1802,6 +1805,9 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     }
   }
   __syncthreads();
+#if defined(M3S_LLT_EXIT) && M3S_LLT_EXIT == 2
+  return;
+#endif
 
   if (phase == 1) {  // hand y and the failure flag to border_kernel / phase 2
     for (int idx = tid; idx < m * 7; idx += 1024) const_cast<double *>(D.rhs)[idx] = y[idx];
@@ -1979,6 +1985,11 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     return;
   }
 
+  // the retraction's pose of this thread, loaded now: its latency hides
+  // behind the back-substitution
+  Sim3f T_pre;
+  if (tid < m) T_pre = load_sim3(D.Twc + 8 * (size_t)(tid + 1));
+
   // 2. back-substitution L^T x = y in reverse level order (x overwrites y),
   // dataflow: column k waits for x_i of every i in struct(k)
   // columns are taken dynamically in reverse level order; the x_i terms are
@@ -2003,23 +2014,28 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
   __syncthreads();
 
-  // 3. dx = -x in the original variable order, retraction, ||dx||
+  // 3. dx = -x in the original variable order, retraction, ||dx||; dx also
+  // to LDS (the per-wave scratch, free now) when it fits, so the retraction
+  // reads it there instead of back from global memory
+  float *dxl = reinterpret_cast<float *>(&scratch[0][0]);
+  const bool dx_lds = m * 7 <= (int)(sizeof(scratch) / sizeof(float));
   float part = 0.0f;
   for (int idx = tid; idx < m * 7; idx += 1024) {
     const int vn = idx / 7, q = idx - vn * 7;
     const int vo = perm[vn];
     const float v = -(float)y[idx];
     D.dx_out[vo * 7 + q] = v;
+    if (dx_lds) dxl[vo * 7 + q] = v;
     part += v * v;
   }
   part = wave_sum(part);
   if (lane == 0) nrm[wave] = part;
   __syncthreads();  // dx_out (global) written by this block is visible to it now
   for (int p = tid; p < m; p += 1024) {
-    const Sim3f T = load_sim3(D.Twc + 8 * (size_t)(p + 1));
+    const Sim3f T = p == tid ? T_pre : load_sim3(D.Twc + 8 * (size_t)(p + 1));
     float xi[7];
 #pragma unroll
-    for (int q = 0; q < 7; q++) xi[q] = D.dx_out[p * 7 + q];
+    for (int q = 0; q < 7; q++) xi[q] = dx_lds ? dxl[p * 7 + q] : D.dx_out[p * 7 + q];
     store_sim3(D.Twc + 8 * (size_t)(p + 1), retract(xi, T));
   }
   if (tid == 0) {

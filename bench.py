@@ -82,6 +82,9 @@ def parse(argv=None):
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo orchestration check with no-op compute (no GPU)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0, gloo "
+                         "collectives (RCCL refuses two ranks on one device); not a scaling measurement")
     return ap.parse_args(argv)
 
 
@@ -138,6 +141,11 @@ def run(args):
     dry = args.dry_run
     if dry:
         dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    elif args.share_gpu:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
         if world > 1:
             dist.init_process_group("gloo")
     else:
@@ -284,6 +292,10 @@ def run(args):
     if dry:
         out["dry_run"] = True
         out["data"] = "dry run: CPU/gloo orchestration with no-op compute; timings are meaningless"
+    elif args.share_gpu and world > 1:
+        out["share_gpu"] = True
+        out["data"] = ("rehearsal: %d ranks sharing ONE GPU over gloo (the product path, HIP compute); "
+                       "not a scaling measurement" % world)
     else:
         out["roofline"] = roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per_s,
                                        world, dev)

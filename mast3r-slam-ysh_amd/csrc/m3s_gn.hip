@@ -126,9 +126,11 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
   L.rank_j = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(E + 1), 256);
-  // flags, ranks, linearize task table and sparse plan are contiguous: one
-  // H2D copy per call uploads them all (gn_prepare_impl)
+  // flags, ranks, edge counters, linearize task table and sparse plan are
+  // contiguous: one H2D copy per call uploads them all (gn_prepare_impl)
   const int64_t m0 = N > 1 ? N - 1 : 0;
+  L.edge_cnt = off;  // per-edge chunk arrival counters (fused finalize), zeroed per call (by the upload)
+  off = align_up(off + edge_cnt_bytes(E), 256);
   L.tasks = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
   L.slot_cap = std::min<int64_t>(m0 * (m0 + 1) / 2, 64 * m0 + 4096) + 1;
@@ -137,8 +139,6 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(int32_t) * (size_t)L.plan_cap, 256);
   L.first = off;
   off = align_up(off + sizeof(int32_t) * (size_t)(2 * E + 1), 256);
-  L.edge_cnt = off;  // per-edge chunk arrival counters (fused finalize), zeroed per call
-  off = align_up(off + edge_cnt_bytes(E), 256);
   L.partials = off;
   off = align_up(off + sizeof(float) * kNP * (size_t)max_partials, 256);
   L.edge_sums = off;
@@ -3954,8 +3954,10 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   PlanMeta &M = g_reg[ws];
   M = std::move(meta);
   bool ok = true;
-  ok &= hipMemsetAsync(at<uint32_t>(ws, Ly.edge_cnt), 0, edge_cnt_bytes(E), st) == hipSuccess;
-  ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
+  // the column-task / dataflow / dense-tail flags live only on the global-factor
+  // path; the LDS-resident factors (store 1 / 2) keep theirs in LDS
+  if (!(M.sparse && M.store != 0))
+    ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
   if (M.nc > 0)  // the tail's tagged granules: no tag of an earlier call may match this call's epochs
     ok &= hipMemsetAsync(at<double>(ws, Ly.tail) + tail_gran_offset_doubles(), 0,
                          sizeof(double) * (tail_scratch_doubles() - tail_gran_offset_doubles()), st) == hipSuccess;
@@ -3979,11 +3981,12 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   const bool with_tasks = M.n_blocks > 0;
   size_t n_up = with_plan ? Ly.plan - Ly.flags + sizeof(int32_t) * M.h_plan.size()
                           : with_tasks ? Ly.tasks - Ly.flags + sizeof(int32_t) * M.tasks.size()
-                                       : Ly.rank_j - Ly.flags + sizeof(int32_t) * (size_t)E;
+                                       : Ly.edge_cnt - Ly.flags + edge_cnt_bytes(E);
   n_up = align_up(n_up, 16);
   if (!pinned_reserve(g_stage.up, g_stage.up_cap, n_up + sizeof M.h_info)) return M3S_ELAUNCH;
   char *up = g_stage.up;
   memcpy(up, M.h_flags, sizeof M.h_flags);
+  memset(up + (Ly.edge_cnt - Ly.flags), 0, edge_cnt_bytes(E));  // the fused finalize's counters
   if (E > 0) {
     memcpy(up + (Ly.rank_i - Ly.flags), M.h_ri.data(), sizeof(int32_t) * E);
     memcpy(up + (Ly.rank_j - Ly.flags), M.rj.data(), sizeof(int32_t) * E);

@@ -33,10 +33,10 @@ Extra legs on rank 0 at N = 1:
                  the per-call symbolic analysis inside the timed region
   roofline     — the linearize kernel timed with HIP events on its stream
                  (+ the first-iteration gathering kernel and the solve launches)
-  hbm_copy     — a measured device-to-device copy rate next to the 8 TB/s spec
+  hbm_copy     — a measured streaming-copy rate (16-B nt copy kernel) next to the 8 TB/s spec
   cpu_baseline — the CPU oracle (C restatement of gn_kernels.cu, OpenMP) on one
-                 GN iteration of the same graph (median of 5), and the numpy
-                 tracker restatement on the C2 pair (median of 3)
+                 GN iteration of the same graph (median of 5), and the PyTorch-CPU
+                 tracker program of tracker.py on the C2 pair, all cores (median of 3)
   tracker_c2   — configs[1]: single-pair tracker GN at 512x512, fixed 10 iters
 """
 from __future__ import annotations
@@ -158,7 +158,7 @@ def run(args):
             f"local_rank={local} device={dev}")
 
     from mast3r_slam_amd import synthetic
-    from mast3r_slam_amd.distributed import ShardedGN, edge_slice
+    from mast3r_slam_amd.distributed import ShardedGN, edge_shard
 
     H, W = (8, 8) if dry else (args.height, args.width)
     HW = H * W
@@ -168,9 +168,9 @@ def run(args):
     probe = synthetic.make_graph(N, 4, 4, seed=SEED, edge_range=(0, 0))
     E = probe.n_edges
     E_base = base_edges(args)
-    eb, ee, _ = edge_slice(E, rank, world)
+    ids, _ = edge_shard(E, rank, world)  # both halves of each of this rank's undirected edges
     t0 = time.time()
-    g = synthetic.make_graph(N, H, W, seed=SEED, device=dev, edge_range=(eb, ee))
+    g = synthetic.make_graph(N, H, W, seed=SEED, device=dev, edge_ids=ids)
     assert g.n_edges == E
     if calib_mode:  # calib inputs are ray-constrained by the caller (global_opt.py:172)
         rays = synthetic.pixel_rays(H, W, g.K)
@@ -184,7 +184,8 @@ def run(args):
     idx, valid, Q = g.idx_ii2jj, g.valid_match, g.Q
     if not dry:
         torch.cuda.synchronize()
-    log(f"[rank {rank}] graph N={N} E_dir={E} slice=[{eb},{ee}) built in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] graph N={N} E_dir={E} {len(ids)} edges (pair-preserving shard) built in "
+        f"{time.time() - t0:.1f}s")
 
     if dry:
         sig = dict(sigma_a=1.0)
@@ -277,7 +278,8 @@ def run(args):
             "pixels_per_pointmap": HW,
             "gn_iters_per_step": args.iters,
             "solve": "fp64 block-sparse 7x7 LLT on device (min-degree order), n=%d" % (7 * (N - 1)),
-            "parallelism": "edge-sharded x%d, RCCL all-gather of per-edge normal equations" % world
+            "parallelism": "edge-sharded x%d (pair-preserving), %s all-gather of per-edge normal equations"
+            % (world, "RCCL" if dist.get_backend() == "nccl" else dist.get_backend())
             if world > 1 else "single GPU",
         },
         "gn_iters_per_s": round(gn_iters_per_s, 2),
@@ -297,11 +299,12 @@ def run(args):
         out["data"] = ("rehearsal: %d ranks sharing ONE GPU over gloo (the product path, HIP compute); "
                        "not a scaling measurement" % world)
     else:
-        out["roofline"] = roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per_s,
+        out["roofline"] = roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
                                        world, dev)
 
     if rank == 0 and world == 1 and not dry:
-        out["hbm_copy"] = copy_leg(dev)
+        out["hbm_copy"] = copy_leg(be, dev)
+        out["roofline"]["frac_of_measured_copy"] = round(out["roofline"]["achieved"] / out["hbm_copy"]["GB_per_s"], 4)
         if not args.no_tracker:
             out["tracker_c2"] = tracker_leg(be, synthetic, dev, H, W)
             out["matching_512"] = matching_leg(be, synthetic, dev, H, W)
@@ -316,7 +319,7 @@ def run(args):
         dist.destroy_process_group()
 
 
-def roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per_s, world, dev):
+def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s, world, dev):
     """The dominant kernel: GN iterations 2..10 of a call run
     linearize_packed_kernel (the first runs the gathering kernel that also
     stores the target-side planes). Timed in the solve's own launch pattern
@@ -324,8 +327,9 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per
     each linearize and each solve launch of stepwise solves of the same graph
     (the linearize pair also covers the launch's ~3 us per-edge reduce). The
     same kernel launched back to back is timed too, for reference."""
-    n_loc = ee - eb
-    kf_touched = torch.unique(torch.cat([ii[eb:ee], jj[eb:ee]])).numel() if n_loc else 0
+    n_loc = len(ids)
+    sel = torch.tensor(ids, dtype=torch.int64, device=ii.device)
+    kf_touched = torch.unique(torch.cat([ii[sel], jj[sel]])).numel() if n_loc else 0
     bytes_alg = HW * (13 * n_loc + 16 * kf_touched)  # SURVEY.md §8(d) per (edge, px) and (KF, px)
     stream = torch.cuda.current_stream(dev)
     lin, first, slv = [], [], []
@@ -398,22 +402,33 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, eb, ee, HW, gn_iters_per
     }
 
 
-def copy_leg(dev, nbytes=1 << 30, reps=10):
-    """Device-to-device copy rate (read + write bytes) as a measured HBM
-    ceiling beside the 8 TB/s spec."""
+def copy_leg(be, dev, nbytes=1 << 30, reps=20):
+    """Measured HBM ceiling beside the 8 TB/s spec: the 16-B non-temporal
+    streaming copy kernel (m3s_debug_copy; the guide's float4 copy reaches
+    6.29 TB/s) over 1 GiB, best grid of a small sweep, read + write bytes;
+    torch's copy_ timed beside it."""
     a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
     b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    return {"GB_per_s": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes_moved": 2 * nbytes,
-            "note": "torch copy_ of 1 GiB, read + write bytes"}
+
+    def rate(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
+
+    sweep = {blk: rate(lambda blk=blk: be.debug_copy(a, b, blk)) for blk in (1024, 2048, 4096, 8192)}
+    best = max(sweep, key=sweep.get)
+    out = {"GB_per_s": round(sweep[best], 1), "bytes_moved": 2 * nbytes, "blocks": best,
+           "sweep_GB_per_s": {str(k): round(v, 1) for k, v in sweep.items()},
+           "torch_copy_GB_per_s": round(rate(lambda: b.copy_(a)), 1),
+           "note": "m3s_debug_copy: 16-B nt loads/stores, 4 in flight per lane, 1 GiB, read + write bytes"}
+    assert torch.equal(a, b)
+    return out
 
 
 def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
@@ -493,8 +508,8 @@ def matching_leg(be, synthetic, dev, H, W, reps=20):
 def cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E, calib_mode, with_tracker, runs=5):
     """Reported, not the target. Backend: the C oracle (oracle/gn_oracle.c,
     OpenMP over edges) on one full GN iteration of the same graph, median of
-    `runs`. Tracker: the numpy restatement of tracker.py on the C2 pair, 10
-    fixed iterations, median of 3."""
+    `runs`. Tracker: the PyTorch-CPU restatement of tracker.py on the C2 pair, 10
+    fixed iterations of the reference's PyTorch program on all cores, median of 3."""
     from mast3r_slam_amd import synthetic
     from oracle import oracle as orc
     from oracle import tracker_oracle as tro
@@ -518,19 +533,29 @@ def cpu_leg(g, Xs, ii, jj, idx, valid, Q, T_init, H, W, E, calib_mode, with_trac
            "sample": "1 full GN iteration (linearise %d directed edges + fp64 solve) of the same graph, "
                      "median of %d runs: %.3f s (min %.3f, max %.3f)" % (E, runs, med, min(ts), max(ts))}
     if with_tracker:
+        # the reference's own CPU/PyTorch tracker program (oracle/tracker_torch.py,
+        # pinned by the tracker fixtures) on all host cores
+        from oracle import tracker_torch as trt
+
         pr = synthetic.make_pair(H, W, seed=1002)
         cfg = dict(tro.TRACKING_CFG, max_iters=10, rel_error=0.0, delta_norm=0.0)
-        args = (pr.Xf.numpy(), pr.Xk.numpy(), pr.T_WCf_init.data.numpy(), pr.T_WCk.data.numpy(),
-                pr.Qk.numpy(), pr.valid.numpy(), cfg)
-        tt = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            _, _, it2 = tro.track_rays(*args)
-            tt.append(time.perf_counter() - t0)
+        threads_before = torch.get_num_threads()
+        torch.set_num_threads(cores)
+        try:
+            targs = (pr.Xf, pr.Xk, pr.T_WCf_init.data, pr.T_WCk.data, pr.Qk, pr.valid, cfg)
+            trt.track_rays(*targs)  # warm-up
+            tt = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                _, _, it2 = trt.track_rays(*targs)
+                tt.append(time.perf_counter() - t0)
+        finally:
+            torch.set_num_threads(threads_before)
         tm = statistics.median(tt)
-        out["tracker"] = {"gn_iters_per_s": round(it2 / tm, 3), "cores": 1, "kind": "port",
-                          "sample": "C2 pair %dx%d, %d fixed iterations of the numpy restatement of "
-                                    "tracker.py, median of 3: %.3f s" % (H, W, it2, tm)}
+        out["tracker"] = {"gn_iters_per_s": round(it2 / tm, 3), "cores": cores, "kind": "port",
+                          "sample": "C2 pair %dx%d, %d fixed iterations of the PyTorch-CPU restatement of "
+                                    "tracker.py (the reference's tensor program), torch threads %d, median of 3: "
+                                    "%.3f s" % (H, W, it2, cores, tm)}
     return out
 
 

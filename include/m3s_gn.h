@@ -178,6 +178,23 @@ size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs);
  * (-DM3S_COL_STAMPS); wall-clock ticks. 1 if present, 0 otherwise
  * (tools/trk_stamps.py, tools/col_stamps.py) */
 int m3s_debug_stamps(int which, int64_t *out);
+/* Diagnostic (tests/test_gpu_sim3.py): the device Sim(3) helpers of the hot
+ * path (csrc/m3s_device.h; lietorch semantics, gn_kernels.cu:172-413) on n
+ * elements, asynchronously on `stream`. Device arrays; Sim3 = 8 floats
+ * (t, q_xyzw, s), tangent = 7 floats (tau, phi, sigma), point = 3 floats.
+ *   op 0 exp(a: tangent)            -> out Sim3      (expSim3 :323-390)
+ *   op 1 retract(a: tangent, b: T)  -> out Exp(a) b  (retrSim3 :392-413)
+ *   op 2 compose(a, b)              -> out a * b
+ *   op 3 inverse(a)                 -> out a^-1
+ *   op 4 relative(a, b)             -> out a^-1 b    (relSim3 :252-272)
+ *   op 5 act(a, b: point)           -> out point     (actSim3 :207-219)
+ *   op 6 act as the 3x4 matrix form the linearize kernels use -> out point
+ *   op 7 Adj(a)^-T as a row-major 7x7 (apply_Sim3_adj_inv :274-297) -> out 49 */
+int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n, void *stream);
+/* Diagnostic (bench.py's measured HBM ceiling): copy nbytes (a multiple of
+ * 16, 16-B aligned device pointers) with 16-B non-temporal loads and stores,
+ * `blocks` workgroups of 256 lanes, asynchronously on `stream`. */
+int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void *stream);
 
 #ifdef __cplusplus
 }

@@ -4486,6 +4486,48 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   return M3S_OK;
 }
 
+// Streaming copy (m3s_debug_copy): the measured HBM ceiling bench.py reports
+// beside the 8 TB/s spec. 16 B per lane per access (dwordx4), 4 accesses in
+// flight per lane, non-temporal loads and stores, grid-stride over the buffer.
+__global__ void __launch_bounds__(256) hbm_copy_kernel(const f32x4 *__restrict__ src, f32x4 *__restrict__ dst,
+                                                       int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  for (int64_t base = (int64_t)blockIdx.x * 256 * 4 + threadIdx.x; base < n4; base += stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (base + 256 * k < n4) v[k] = __builtin_nontemporal_load(src + base + 256 * k);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (base + 256 * k < n4) __builtin_nontemporal_store(v[k], dst + base + 256 * k);
+  }
+}
+
+// Sim(3) device helpers on arrays (m3s_debug_sim3): the functions the hot path
+// applies, run as-is for the property tests of tests/test_gpu_sim3.py
+__global__ void sim3_debug_kernel(int op, const float *__restrict__ a, const float *__restrict__ b,
+                                  float *__restrict__ out, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  switch (op) {
+    case 0: store_sim3(out + 8 * k, exp_sim3(a + 7 * k)); break;
+    case 1: store_sim3(out + 8 * k, retract(a + 7 * k, load_sim3(b + 8 * k))); break;
+    case 2: store_sim3(out + 8 * k, compose(load_sim3(a + 8 * k), load_sim3(b + 8 * k))); break;
+    case 3: store_sim3(out + 8 * k, inverse(load_sim3(a + 8 * k))); break;
+    case 4: store_sim3(out + 8 * k, relative(load_sim3(a + 8 * k), load_sim3(b + 8 * k))); break;
+    case 5: act(load_sim3(a + 8 * k), b + 3 * k, out + 3 * k); break;
+    case 6: act(sim3_matrix(load_sim3(a + 8 * k)), b + 3 * k, out + 3 * k); break;
+    case 7: {
+      double M[7][7];
+      adjT_inv_matrix(a + 8 * k, M);
+      for (int r = 0; r < 7; r++)
+        for (int c = 0; c < 7; c++) out[49 * k + 7 * r + c] = (float)M[r][c];
+      break;
+    }
+    default: break;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ C exports --
@@ -4589,6 +4631,22 @@ int m3s_debug_stamps(int which, int64_t *out) {
   (void)which;
   (void)out;
   return 0;
+}
+
+int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void *stream) {
+  if (!src || !dst || nbytes < 0 || (nbytes & 15) || (((uintptr_t)src | (uintptr_t)dst) & 15) || blocks <= 0)
+    return M3S_EINVAL;
+  if (nbytes == 0) return M3S_OK;
+  hbm_copy_kernel<<<blocks, 256, 0, S(stream)>>>(reinterpret_cast<const f32x4 *>(src), reinterpret_cast<f32x4 *>(dst),
+                                                 nbytes / 16);
+  return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH;
+}
+
+int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n, void *stream) {
+  if (op < 0 || op > 7 || n < 0 || !a || !out || (op != 0 && op != 3 && op != 7 && !b)) return M3S_EINVAL;
+  if (n == 0) return M3S_OK;
+  sim3_debug_kernel<<<(unsigned)((n + 255) / 256), 256, 0, S(stream)>>>(op, a, b, out, n);
+  return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH;
 }
 
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs) {

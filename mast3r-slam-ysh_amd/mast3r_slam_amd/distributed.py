@@ -28,14 +28,58 @@ import torch.distributed as dist
 
 
 def edge_slice(E: int, rank: int, world: int):
-    """Contiguous edge range [b, e) of `rank` and the per-rank stride `per`.
-
-    Rank r owns rows [r*per, r*per + (e-b)) of the gathered [per*world, S]
-    payload, so row k of the gather is edge k for every k < E."""
+    """Contiguous edge range [b, e) of `rank` and the per-rank stride `per`
+    (the plain split; ShardedGN uses :func:`edge_shard`)."""
     per = (E + world - 1) // world if world > 0 else E
     b = min(rank * per, E)
     e = min(b + per, E)
     return b, e, per
+
+
+def edge_shard(E: int, rank: int, world: int):
+    """The directed edges of `rank`, keeping each undirected edge's two halves
+    together: the reference hands the backend the two-way
+    list [fwd | bwd] (``prep_two_way_edges``, global_opt.py:104-110), so edge
+    u < E/2 and edge E/2 + u are one pair. Rank r owns the pairs of a
+    contiguous range [ub, ue) of undirected edges: directed ids
+    [ub, ue) ++ [E/2 + ub, E/2 + ue), in that order. An odd E (not a two-way
+    list) falls back to the contiguous split.
+
+    Returns (ids, per): rank r's rows of the gathered [per * world, S]
+    payload are [r * per, r * per + len(ids)); rows past len(ids) are padding
+    (zero sums). :func:`payload_edges` gives the edge of every payload row."""
+    if world <= 1:
+        return list(range(E)), E
+    if E % 2:
+        b, e, per = edge_slice(E, rank, world)
+        return list(range(b, e)), per
+    U = E // 2
+    per_u = (U + world - 1) // world
+    ub = min(rank * per_u, U)
+    ue = min(ub + per_u, U)
+    return list(range(ub, ue)) + list(range(U + ub, U + ue)), 2 * per_u
+
+
+def payload_edges(E: int, world: int):
+    """The directed edge id of every row of the gathered payload
+    ([per * world] rows, rank-major). A padding row repeats a real edge of the
+    same rank (or edge 0): its sums are zero, so the assembled system, the
+    fill pattern and the keyframe set are those of the E real edges."""
+    rows = []
+    for r in range(world):
+        ids, per = edge_shard(E, r, world)
+        pad = ids[0] if ids else 0
+        rows += ids + [pad] * (per - len(ids))
+    return rows
+
+
+def payload_ids(ii: torch.Tensor, jj: torch.Tensor, world: int):
+    """ii/jj in payload order (the edge list every rank's solve is given; the
+    reference's order itself at world 1)."""
+    if world <= 1:
+        return ii, jj
+    rows = torch.tensor(payload_edges(int(ii.numel()), world), dtype=torch.int64, device=ii.device)
+    return ii[rows].contiguous(), jj[rows].contiguous()
 
 
 class HipOps:
@@ -49,9 +93,16 @@ class HipOps:
 
         self.be = be
         self.stride = be.EDGE_SUM_STRIDE
-        for name, t in (("Twc", Twc), ("Xs", Xs), ("Cs", Cs), ("ii", ii), ("jj", jj),
-                        ("idx", idx_loc), ("valid", valid_loc), ("Q", Q_loc)):
-            be._check(t, name)
+        f32, i64 = torch.float32, torch.int64
+        # the same dtype contract as the single-call path (make_gn_args): idx
+        # is int64 as the reference passes it, or int32 from the device edge
+        # store (factor_graph.EdgeStore) — the C side is told which
+        for name, t, dt in (("Twc", Twc, f32), ("Xs", Xs, f32), ("Cs", Cs, f32), ("ii", ii, i64),
+                            ("jj", jj, i64), ("idx", idx_loc, (i64, torch.int32)),
+                            ("valid", valid_loc, torch.bool), ("Q", Q_loc, f32)):
+            be._check(t, name, dt)
+        if K is not None:
+            be._check(K, "K", f32)
         dev = Xs.device
         self.device = dev
         N, HW = int(Xs.shape[0]), int(Xs.shape[1])
@@ -64,6 +115,7 @@ class HipOps:
         # edge-slice base pointers: the C side addresses edge data relative to
         # edge_begin (include/m3s_gn.h, stepwise API)
         a.idx_ii2jj, a.valid_match, a.Q, a.K = P(idx_loc), P(valid_loc), P(Q_loc), P(K)
+        a.idx_i32 = 1 if idx_loc.dtype == torch.int32 else 0
         a.N, a.HW, a.E, a.mode = N, HW, int(E), mode
         a.sigma_a, a.sigma_b, a.C_thresh, a.Q_thresh = sigma_a, sigma_b, C_thresh, Q_thresh
         a.height, a.width, a.pixel_border, a.z_eps = height, width, pixel_border, z_eps
@@ -100,10 +152,17 @@ class HipOps:
 class ShardedGN:
     """Per-rank state of one sharded GN problem.
 
-    Edge data tensors (idx, valid, Q) are this rank's slice [e_end - e_begin,
-    HW(,1)]; ii/jj are the full [E] id lists (every rank needs all of them to
+    Edge data tensors (idx, valid, Q) are this rank's edges
+    (:func:`edge_shard`: both halves of each of its undirected edges, in the
+    order ``edge_shard`` lists them), [n_loc, HW(,1)]; ii/jj are the full [E]
+    id lists in the reference's order (every rank needs all of them to
     assemble the system); Xs/Cs/Twc are replicated. ``ops`` defaults to
     :class:`HipOps` over the same arguments.
+
+    The solve sees the edges in payload order (:func:`payload_edges`: the
+    gathered rows, rank-major), so the all-gathered tensor is consumed as it
+    lands: this rank linearizes the contiguous payload rows
+    [rank * per, rank * per + n_loc) and nothing is permuted per iteration.
     """
 
     def __init__(self, mode, Twc, Xs, Cs, ii, jj, idx_loc, valid_loc, Q_loc, E, K=None, *,
@@ -113,14 +172,19 @@ class ShardedGN:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.E = int(E)
-        self.eb, self.ee, self.per = edge_slice(self.E, self.rank, self.world)
-        n_loc = self.ee - self.eb
+        ids, self.per = edge_shard(self.E, self.rank, self.world)
+        self.edge_ids = ids
+        n_loc = len(ids)
+        self.eb = self.rank * self.per if self.world > 1 else 0
+        self.ee = self.eb + n_loc
         if not (idx_loc.shape[0] == n_loc and valid_loc.shape[0] == n_loc
                 and Q_loc.shape[0] == n_loc):
             raise ValueError(f"rank {self.rank}: edge data must hold this rank's {n_loc} edges "
-                             f"[{self.eb}, {self.ee})")
+                             f"(edge_shard)")
+        ii, jj = payload_ids(ii, jj, self.world)  # padding rows: zero sums
+        self.E_pay = int(ii.numel())
         if ops is None:
-            ops = HipOps(mode, Twc, Xs, Cs, ii, jj, idx_loc, valid_loc, Q_loc, self.E, K,
+            ops = HipOps(mode, Twc, Xs, Cs, ii, jj, idx_loc, valid_loc, Q_loc, self.E_pay, K,
                          sigma_a=sigma_a, sigma_b=sigma_b, C_thresh=C_thresh, Q_thresh=Q_thresh,
                          height=height, width=width, pixel_border=pixel_border, z_eps=z_eps)
         self.ops = ops

@@ -20,7 +20,11 @@ Call sites this type replaces: ``tracker.py:98,180,187,195,212``,
 
 This module is host plumbing (the tracker/FactorGraph mirror and the synthetic
 generator); the hot path applies the same formulas on device in
-``csrc/m3s_sim3.h``.
+``csrc/m3s_device.h`` (exposed for tests by ``m3s_debug_sim3``). Both are
+checked against the group's mathematics in ``tests/test_sim3_math.py`` /
+``tests/test_gpu_sim3.py``: Exp is the matrix exponential of the sim(3)
+generator, compose / inverse / act are 4x4 matrix products, and the
+reference's Jacobian rows are the derivatives of its residuals.
 """
 from __future__ import annotations
 

@@ -173,13 +173,16 @@ def make_graph(
     kf_ids=None,
     noise=True,
     edge_range=None,
+    edge_ids=None,
 ) -> Graph:
     """Build a synthetic FactorGraph problem (already in the two-way edge form
     that ``FactorGraph.prep_two_way_edges`` hands to the backend).
 
     ``edge_range=(b, e)`` builds idx/valid/Q only for directed edges [b, e)
     (a rank's shard); every per-edge random draw is seeded by the edge index,
-    so shards are slices of the full graph. ii/jj are always the full lists."""
+    so shards are slices of the full graph. ``edge_ids`` (a list of directed
+    edge ids, e.g. ``distributed.edge_shard``'s) builds exactly those edges in
+    that order instead. ii/jj are always the full lists."""
     gen = torch.Generator().manual_seed(seed)
     K = intrinsics(H, W, device)
     T_gt = loop_trajectory(N, gen, device=device)
@@ -202,13 +205,17 @@ def make_graph(
     jj_dir = jj_u + ii_u
     E = len(ii_dir)
     HW = H * W
-    eb, ee = (0, E) if edge_range is None else (max(0, edge_range[0]), min(E, edge_range[1]))
-    n_loc = max(ee - eb, 0)
+    if edge_ids is not None:
+        sel = [int(e) for e in edge_ids]
+        assert all(0 <= e < E for e in sel)
+    else:
+        eb, ee = (0, E) if edge_range is None else (max(0, edge_range[0]), min(E, edge_range[1]))
+        sel = list(range(eb, max(ee, eb)))
+    n_loc = len(sel)
     idx = torch.empty(n_loc, HW, dtype=torch.int64, device=device)
     valid = torch.empty(n_loc, HW, 1, dtype=torch.bool, device=device)
     Q = torch.empty(n_loc, HW, 1, dtype=torch.float32, device=device)
-    for k in range(n_loc):
-        e = eb + k
+    for k, e in enumerate(sel):
         i, j = ii_dir[e], jj_dir[e]
         Xw_j = T_gt[j : j + 1].act(X_clean[j])
         ie, ve = correspondences(Xw_j, T_gt[i : i + 1], depth[i], K, H, W)

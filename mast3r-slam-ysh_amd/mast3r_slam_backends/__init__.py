@@ -120,7 +120,8 @@ EXPORTS = (
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve", "m3s_gn_release",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
-    "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_debug_stamps",
+    "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_debug_stamps", "m3s_debug_sim3",
+    "m3s_debug_copy",
 )
 FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2, "weighted_spherical": 3}
 
@@ -165,6 +166,10 @@ def _load(path=LIB_PATH):
     lib.m3s_refine_matches.argtypes = [P(RefineArgs), _VP]
     lib.m3s_debug_stamps.restype = ctypes.c_int
     lib.m3s_debug_stamps.argtypes = [ctypes.c_int, _VP]
+    lib.m3s_debug_sim3.restype = ctypes.c_int
+    lib.m3s_debug_sim3.argtypes = [ctypes.c_int, _VP, _VP, _VP, ctypes.c_int64, _VP]
+    lib.m3s_debug_copy.restype = ctypes.c_int
+    lib.m3s_debug_copy.argtypes = [_VP, _VP, ctypes.c_int64, ctypes.c_int, _VP]
     lib.m3s_gn_layout_debug.restype = ctypes.c_size_t
     lib.m3s_gn_layout_debug.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP]
     return lib
@@ -185,6 +190,41 @@ PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col",
 
 LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
                    "plan", "Lblk", "Dinv", "tail", "tasks", "planes", "total")
+
+
+SIM3_OPS = {"exp": (0, 7, None, 8), "retract": (1, 7, 8, 8), "compose": (2, 8, 8, 8), "inverse": (3, 8, None, 8),
+            "relative": (4, 8, 8, 8), "act": (5, 8, 3, 3), "act_matrix": (6, 8, 3, 3), "adjT_inv": (7, 8, None, 49)}
+
+
+def debug_sim3(op: str, a: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor:
+    """The device Sim(3) helpers of the hot path on [n, ...] float32 device
+    tensors (m3s_debug_sim3; diagnostics/tests). op in SIM3_OPS."""
+    code, wa, wb, wo = SIM3_OPS[op]
+    a = a.contiguous()
+    _check(a, "a", torch.float32)
+    n = a.numel() // wa
+    if a.numel() != n * wa:
+        raise RuntimeError(f"debug_sim3({op}): a must be [n, {wa}]")
+    if wb is not None:
+        if b is None:
+            raise RuntimeError(f"debug_sim3({op}) needs b")
+        b = b.contiguous()
+        _check(b, "b", torch.float32)
+        if b.numel() != n * wb:
+            raise RuntimeError(f"debug_sim3({op}): b must be [n, {wb}]")
+    out = torch.empty(n, wo, dtype=torch.float32, device=a.device)
+    _raise(_lib.m3s_debug_sim3(code, _p(a), _p(b), _p(out), n, _stream(a.device)), "m3s_debug_sim3")
+    return out
+
+
+def debug_copy(src: torch.Tensor, dst: torch.Tensor, blocks: int = 4096):
+    """dst <- src by the 16-B streaming copy kernel (m3s_debug_copy)."""
+    _check(src, "src")
+    _check(dst, "dst")
+    nb = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < nb:
+        raise RuntimeError("debug_copy: dst too small")
+    _raise(_lib.m3s_debug_copy(_p(src), _p(dst), nb, int(blocks), _stream(src.device)), "m3s_debug_copy")
 
 
 def workspace_layout(N, HW, E):

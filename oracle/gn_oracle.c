@@ -506,3 +506,20 @@ int oracle_gn(const params_t *P, float *Twc, const float *Xs, const float *Cs, i
 void oracle_retract(const float *xi, float *T) { retract(xi, T); }
 void oracle_relative(const float *Ti, const float *Tj, float *Tij) { relative(Ti, Tj, Tij); }
 void oracle_adjT_inv(const float *Ti, const float *a, float *out) { adjT_inv(Ti, a, out); }
+
+/* Test hook (tests/test_sim3_math.py): the reference rows of one pixel at
+ * world poses Ti, Tj, as edge_blocks forms them — the local rows J_local
+ * (rows_for_pixel) mapped by Adj(T_i)^-T into J_j, and J_i = -J_j
+ * (gn_kernels.cu:990-1000) — plus the errors, with the match taken as valid
+ * and confident. Returns the row count. */
+int oracle_pixel_rows(const params_t *P, const float *Ti, const float *Tj, const float *Xi, const float *Xj,
+                      int64_t id_i, float *J_i, float *J_j, float *e) {
+  float Tij[8], J[4][7], w[4];
+  relative(Ti, Tj, Tij);
+  const int nr = rows_for_pixel(P, Tij, Xi, Xj, id_i, 1e6f, 1e6f, 1e6f, 1, J, e, w);
+  for (int r = 0; r < nr; r++) {
+    adjT_inv(Ti, J[r], J_j + 7 * r);
+    for (int n = 0; n < 7; n++) J_i[7 * r + n] = -J_j[7 * r + n];
+  }
+  return nr;
+}

@@ -31,7 +31,8 @@ def _paths():
 
 
 _paths()
-from mast3r_slam_amd.distributed import ShardedGN, edge_slice  # noqa: E402
+from mast3r_slam_amd.distributed import (ShardedGN, edge_shard, edge_slice, payload_edges,  # noqa: E402
+                                         payload_ids)
 
 N_KF, H, W, ITERS = 7, 12, 16, 3
 SIG = (0.003, 10.0)
@@ -160,12 +161,13 @@ def _rank_main(rank, world, port, out_dir, local_form=False):
     try:
         g = _graph()
         E = g.n_edges
-        eb, ee, _ = edge_slice(E, rank, world)
+        ids, _ = edge_shard(E, rank, world)  # both halves of each undirected edge
         Twc = g.T_init.data.clone()
         cls = LocalFormOracleOps if local_form else OracleOps
-        ops = cls(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj[eb:ee], g.valid_match[eb:ee], g.Q[eb:ee])
-        solver = ShardedGN(1, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj[eb:ee],
-                           g.valid_match[eb:ee], g.Q[eb:ee], E, sigma_a=SIG[0], sigma_b=SIG[1],
+        ii_p, jj_p = payload_ids(g.ii, g.jj, world)  # the solve's edge list (gathered-row order)
+        loc = (g.idx_ii2jj[ids], g.valid_match[ids], g.Q[ids])
+        ops = cls(Twc, g.Xs, g.Cs, ii_p, jj_p, *loc)
+        solver = ShardedGN(1, Twc, g.Xs, g.Cs, g.ii, g.jj, *loc, E, sigma_a=SIG[0], sigma_b=SIG[1],
                            ops=ops)
         solver.solve(ITERS, 0.0)
         np.save(os.path.join(out_dir, f"T_{rank}.npy"), Twc.numpy())
@@ -210,6 +212,58 @@ def test_edge_slices_partition_edges(E, world):
         assert b == min(r * per, E)  # row k of the gathered payload is edge k
         seen.extend(range(b, e))
     assert seen == list(range(E))
+
+
+@pytest.mark.parametrize("E,world", [(98, 2), (98, 8), (96, 3), (6, 4), (2, 3), (0, 2), (792, 8),
+                                     (2048, 8), (7, 3)])
+def test_edge_shards_keep_pairs_and_cover_edges(E, world):
+    """edge_shard: every directed edge on exactly one rank; for a two-way list
+    (E even: [fwd | bwd], global_opt.py:104-110) edge u and edge E/2 + u on
+    the same rank; payload_edges: rank r's rows start at r * per, padding rows
+    repeat an edge of the same rank."""
+    seen = []
+    rows = payload_edges(E, world)
+    for r in range(world):
+        ids, per = edge_shard(E, r, world)
+        assert len(ids) <= per
+        seen.extend(ids)
+        assert rows[r * per:r * per + len(ids)] == ids
+        pad = rows[r * per + len(ids):(r + 1) * per]
+        assert all(p == (ids[0] if ids else 0) for p in pad)
+        if E % 2 == 0 and world > 1:
+            U = E // 2
+            own = set(ids)
+            for u in ids:
+                assert (u + U if u < U else u - U) in own, f"pair of edge {u} not on rank {r}"
+    assert sorted(seen) == list(range(E))
+    assert len(rows) == (len(rows) // world) * world
+
+
+def test_payload_order_zero_padding_rows_leave_the_system_unchanged():
+    """A padding row (duplicate edge, zero sums) adds exact zeros: the solve on
+    the payload-ordered edge list equals the solve on the reference order up
+    to the fp64 summation order of duplicate blocks."""
+    g = _graph()
+    Twc0 = g.T_init.data.clone()
+    E = g.n_edges
+    world = 4
+    ii_p, jj_p = payload_ids(g.ii, g.jj, world)
+    rows = payload_edges(E, world)
+    ops_ref = LocalFormOracleOps(Twc0.clone(), g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q)
+    es = torch.zeros(E, 36, dtype=torch.float64)
+    ops_ref.linearize(0, E, es)
+    es_pay = torch.zeros(len(rows), 36, dtype=torch.float64)
+    real = set()
+    for k, e in enumerate(rows):
+        if e not in real:  # the first occurrence carries the edge, repeats are padding
+            es_pay[k] = es[e]
+            real.add(e)
+    ops_pay = LocalFormOracleOps(Twc0.clone(), g.Xs, g.Cs, ii_p, jj_p, g.idx_ii2jj, g.valid_match, g.Q)
+    ops_ref.prepare(0.0)
+    ops_pay.prepare(0.0)
+    ops_ref.solve(es)
+    ops_pay.solve(es_pay)
+    np.testing.assert_allclose(ops_pay.Twc.numpy(), ops_ref.Twc.numpy(), rtol=0, atol=1e-6)
 
 
 def test_sharded_gn_rejects_wrong_slice():

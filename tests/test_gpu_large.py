@@ -8,12 +8,17 @@ against the CPU oracle (oracle/gn_oracle.c) on identical inputs.
 * C5: 128 keyframes, 394 directed edges (configs[4] runs it on 4 GPUs);
 * C4: 256 keyframes, 792 directed edges (configs[3] runs it on 8 GPUs).
 
-Tolerances (_check_against_oracle): measured against the same
-oracle built with fp64 sums (the exact-arithmetic yardstick); the HIP result
-must be at least as close to it as the reference's fp32 arithmetic (within
-2x) after one step and after three. The edge-sharded path (distributed.py,
-stepwise C ABI) runs with R = 4 (C5) and R = 8 (C4) in-process ranks: ranks
-bitwise identical, poses equal to the single call within the pose tolerance.
+Tolerances, against the same oracle built with fp64 sums (the
+exact-arithmetic yardstick):
+* one step: |dx_hip - dx_exact| <= 2e-4 max|dx| (the reference's fp32 sums
+  are ~1e-2 of the step away from exact at these sizes);
+* 10 iterations (delta = 0 and the reference's 1e-8): the north star's ATE
+  figure, |ATE_hip - ATE_exact| < 1e-5 m and ATE(hip vs exact) < 1e-5 m; the
+  ATE delta to the reference arithmetic (fp32 oracle) is printed and bounded
+  by that oracle's own distance from exact + 1e-5 m.
+The edge-sharded path (distributed.py, pair-preserving shards, stepwise C ABI)
+runs with R = 4 (C5) and R = 8 (C4) in-process ranks: ranks bitwise
+identical, ATE within 1e-5 m of the fp64-sum oracle.
 """
 import numpy as np
 import pytest
@@ -50,69 +55,99 @@ def c4():
     return _graph(256, 1004)
 
 
-def _gpu(be, g, iters):
+def _gpu(be, g, iters, delta=0.0):
     Twc = g.T_init.data.clone().contiguous()
     info = torch.zeros(8, dtype=torch.int32, device=DEV)
     (dx,) = be.gauss_newton_rays(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q, 0.003, 10.0,
-                                 0.0, 1.5, iters, 0.0, info=info)
+                                 0.0, 1.5, iters, delta, info=info)
     torch.cuda.synchronize()
     return Twc.cpu().numpy(), dx.cpu().numpy(), info.cpu().numpy()
 
 
-def _oracle(g, iters, f64=False):
+def _oracle(g, iters, f64=False, delta=0.0):
     from oracle import oracle as orc
 
     p = orc.make_params(orc.MODE_RAYS, 0.003, 10.0, 0.0, 1.5)
     host = [t.cpu().numpy() for t in (g.T_init.data, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q)]
-    return orc.gn(p, *host, iters, 0.0, f64=f64)
+    return orc.gn(p, *host, iters, delta, f64=f64)
 
 
-def _check_against_oracle(be, g):
-    """The reference's fp32 sums over 262k pixels per edge carry ~1e-6
-    relative noise, which cond(H) of a several-hundred-pose loop graph
-    amplifies to ~1e-2 of the step: the reference is no closer than that to
-    the exact step itself. The oracle built with fp64 sums (same per-pixel
-    fp32 arithmetic) is the yardstick: the HIP step must be at least as close
-    to it as the reference arithmetic is (within 2x), and consistent with the
-    reference oracle to the sum of both noise levels."""
-    T1, dx1, info1 = _gpu(be, g, 1)
+# Stated bounds. The yardstick is the oracle built with fp64
+# per-edge sums (same per-pixel fp32 arithmetic): exact summation, which the
+# reference's fp32 sums over 262k pixels per edge (x cond(H) of a
+# several-hundred-pose loop graph) are ~1e-2 of the step away from.
+DX_REL_TOL = 2e-4   # one step: |dx_hip - dx_exact| <= DX_REL_TOL * max|dx_exact|
+ATE_TOL_M = 1e-5    # north star: |ATE_hip - ATE_exact| and ATE(hip vs exact) after 10 iterations
+
+
+def _one_step(be, g):
+    _, dx1, info1 = _gpu(be, g, 1)
     _, dx1_ref, it1, failed1 = _oracle(g, 1)
     _, dx1_x, _, _ = _oracle(g, 1, f64=True)
     assert it1 == 1 and failed1 == 0
     assert info1[be.INFO_ITERS] == 1 and info1[be.INFO_SOLVE_FAIL] == 0 and info1[be.INFO_BAD_EDGE] == 0
     scale = np.abs(dx1_x).max()
     assert scale > 1e-4  # the step is real
-    floor = 1e-6 + 1e-5 * scale
     e_gpu, e_ref = np.abs(dx1 - dx1_x).max(), np.abs(dx1_ref - dx1_x).max()
-    print(f"one step: max|dx|={scale:.3e} |hip-exact|={e_gpu:.3e} |ref-exact|={e_ref:.3e} "
-          f"|hip-ref|={np.abs(dx1 - dx1_ref).max():.3e}")
-    assert e_gpu <= max(2.0 * e_ref, floor), (e_gpu, e_ref)
-    np.testing.assert_allclose(dx1, dx1_ref, rtol=0, atol=e_gpu + e_ref + floor)
-    T3, dx3, info3 = _gpu(be, g, 3)
-    T3_ref, dx3_ref, it3, failed3 = _oracle(g, 3)
-    T3_x, _, _, _ = _oracle(g, 3, f64=True)
-    assert info3[be.INFO_ITERS] == it3 == 3 and info3[be.INFO_SOLVE_FAIL] == failed3 == 0
-    np.testing.assert_array_equal(T3[0], g.T_init.data[0].cpu().numpy())  # rank 0 fixed
-    p_gpu, p_ref = np.abs(T3 - T3_x).max(), np.abs(T3_ref - T3_x).max()
-    print(f"three steps: |hip-exact|={p_gpu:.3e} |ref-exact|={p_ref:.3e} |hip-ref|={np.abs(T3 - T3_ref).max():.3e}")
-    assert p_gpu <= max(2.0 * p_ref, 1e-5), (p_gpu, p_ref)
-    np.testing.assert_allclose(T3, T3_ref, rtol=0, atol=p_gpu + p_ref + 1e-5)
-    return T3, p_gpu + p_ref + 1e-5
+    print(f"one step: max|dx|={scale:.3e} |hip-exact|={e_gpu:.3e} ({e_gpu / scale:.2e} rel) "
+          f"|ref-exact|={e_ref:.3e} ({e_ref / scale:.2e} rel) |hip-ref|={np.abs(dx1 - dx1_ref).max():.3e}")
+    assert e_gpu <= DX_REL_TOL * scale, (e_gpu, scale)
+
+
+def _ate_10(be, g, label):
+    """10 GN iterations, delta = 0 and the reference's delta = 1e-8
+    (base.yaml:49): ATE (evaluate.ate_rmse, the evo_ape -as restatement) of
+    the HIP, reference-arithmetic (fp32 oracle) and fp64-sum oracle
+    trajectories against GT and against each other."""
+    from mast3r_slam_amd import evaluate
+
+    gt = g.T_gt.data.cpu().numpy()
+    T_h0, _, inf0 = _gpu(be, g, 10, 0.0)
+    T_h8, _, inf8 = _gpu(be, g, 10, 1e-8)
+    T_r8, _, it_r8, f_r8 = _oracle(g, 10, delta=1e-8)
+    T_x, _, it_x, f_x = _oracle(g, 10, f64=True, delta=1e-8)
+    assert inf0[be.INFO_ITERS] == 10 and inf0[be.INFO_SOLVE_FAIL] == 0 and f_r8 == 0 and f_x == 0
+    # fp32 steps never fall below 1e-8 here: every path runs the 10 iterations
+    assert inf8[be.INFO_ITERS] == it_r8 == it_x == 10, (inf8[be.INFO_ITERS], it_r8, it_x)
+    np.testing.assert_array_equal(T_h8, T_h0)  # delta unused when no step stops the loop
+    np.testing.assert_array_equal(T_h0[0], g.T_init.data[0].cpu().numpy())  # rank 0 fixed
+    a = {k: evaluate.ate_rmse(T, gt) for k, T in (("init", g.T_init.data.cpu().numpy()), ("hip", T_h0),
+                                                    ("ref", T_r8), ("exact", T_x))}
+    pair = {"hip~ref": evaluate.ate_rmse(T_h0, T_r8), "hip~exact": evaluate.ate_rmse(T_h0, T_x),
+            "ref~exact": evaluate.ate_rmse(T_r8, T_x)}
+    print(f"{label} 10 it ATE vs GT [m]: init {a['init']:.6f} hip {a['hip']:.8f} ref(fp32) {a['ref']:.8f} "
+          f"exact(fp64 sums) {a['exact']:.8f}")
+    print(f"{label} |ATE_hip-ATE_ref| {abs(a['hip'] - a['ref']):.3e}  |ATE_hip-ATE_exact| "
+          f"{abs(a['hip'] - a['exact']):.3e}  |ATE_ref-ATE_exact| {abs(a['ref'] - a['exact']):.3e}")
+    print(f"{label} trajectory ATE between: hip~ref {pair['hip~ref']:.3e} hip~exact {pair['hip~exact']:.3e} "
+          f"ref~exact {pair['ref~exact']:.3e}; max|pose| hip-exact {np.abs(T_h0 - T_x).max():.3e} "
+          f"ref-exact {np.abs(T_r8 - T_x).max():.3e}")
+    assert a["hip"] < 0.5 * a["init"]
+    assert abs(a["hip"] - a["exact"]) < ATE_TOL_M, (a["hip"], a["exact"])
+    assert pair["hip~exact"] < ATE_TOL_M, pair
+    # the reference's own arithmetic is further from exact than the HIP path
+    # (its fp32 sums): the HIP-vs-reference ATE delta is bounded by that noise
+    # plus the north star's 1e-5 m (DESIGN.md §5 gives the measured figures)
+    assert abs(a["hip"] - a["ref"]) <= abs(a["ref"] - a["exact"]) + ATE_TOL_M, a
+    return T_h0, T_x
 
 
 def _sharded(be, g, world, iters):
-    """R in-process ranks over the stepwise C ABI; the all-gather is a cat."""
-    from mast3r_slam_amd.distributed import HipOps, edge_slice
+    """R in-process ranks over the stepwise C ABI, pair-preserving shards
+    (distributed.edge_shard); the all-gather is a cat of the rank payloads."""
+    from mast3r_slam_amd.distributed import HipOps, edge_shard, payload_ids
 
     E = g.n_edges
+    ii_p, jj_p = payload_ids(g.ii, g.jj, world)
     ranks = []
     for r in range(world):
-        eb, ee, per = edge_slice(E, r, world)
+        ids, per = edge_shard(E, r, world)
+        sel = torch.tensor(ids, dtype=torch.int64, device=DEV)
         Twc = g.T_init.data.clone().contiguous()
-        ops = HipOps(be.MODE_RAYS, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj[eb:ee], g.valid_match[eb:ee],
-                     g.Q[eb:ee], E, None, **SIG)
+        ops = HipOps(be.MODE_RAYS, Twc, g.Xs, g.Cs, ii_p, jj_p, g.idx_ii2jj[sel].contiguous(),
+                     g.valid_match[sel].contiguous(), g.Q[sel].contiguous(), len(ii_p), None, **SIG)
         es = torch.zeros(per, ops.stride, dtype=torch.float64, device=DEV)
-        ranks.append((eb, ee, Twc, ops, es))
+        ranks.append((r * per, r * per + len(ids), Twc, ops, es))
     for *_, ops, _ in ranks:
         ops.prepare(0.0)
     for _ in range(iters):
@@ -129,22 +164,32 @@ def _sharded(be, g, world, iters):
     return out
 
 
-def _check_sharded(be, g, world, T_single, tol):
-    res = _sharded(be, g, world, 3)
+def _check_sharded(be, g, world, T_hip, T_exact, label):
+    from mast3r_slam_amd import evaluate
+
+    res = _sharded(be, g, world, 10)
     for T, info in res:
         np.testing.assert_array_equal(T, res[0][0])  # identical inputs, deterministic kernels
-        assert info[be.INFO_ITERS] == 3 and info[be.INFO_SOLVE_FAIL] == 0
-    # per-edge sums grouped differently (edge_reduce vs the fused finalize)
-    np.testing.assert_allclose(res[0][0], T_single, rtol=0, atol=tol)
+        assert info[be.INFO_ITERS] == 10 and info[be.INFO_SOLVE_FAIL] == 0
+    gt = g.T_gt.data.cpu().numpy()
+    a_s, a_x = evaluate.ate_rmse(res[0][0], gt), evaluate.ate_rmse(T_exact, gt)
+    print(f"{label} sharded x{world}: |ATE-ATE_exact| {abs(a_s - a_x):.3e} ATE(sharded~exact) "
+          f"{evaluate.ate_rmse(res[0][0], T_exact):.3e} max|pose| vs single call {np.abs(res[0][0] - T_hip).max():.3e}")
+    assert abs(a_s - a_x) < ATE_TOL_M
+    assert evaluate.ate_rmse(res[0][0], T_exact) < ATE_TOL_M
 
 
+@pytest.mark.timeout(900)
 def test_c5_rays_128kf_matches_oracle(be, c5):
     assert c5.n_edges == 394 and c5.Xs.shape == (128, 512 * 512, 3)
-    T3, tol = _check_against_oracle(be, c5)
-    _check_sharded(be, c5, 4, T3, tol)
+    _one_step(be, c5)
+    T_hip, T_x = _ate_10(be, c5, "C5")
+    _check_sharded(be, c5, 4, T_hip, T_x, "C5")
 
 
+@pytest.mark.timeout(900)
 def test_c4_rays_256kf_matches_oracle(be, c4):
     assert c4.n_edges == 792 and c4.Xs.shape == (256, 512 * 512, 3)
-    T3, tol = _check_against_oracle(be, c4)
-    _check_sharded(be, c4, 8, T3, tol)
+    _one_step(be, c4)
+    T_hip, T_x = _ate_10(be, c4, "C4")
+    _check_sharded(be, c4, 8, T_hip, T_x, "C4")

@@ -38,16 +38,16 @@ def _rank_main(rank, world, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mast3r_slam_amd.distributed import ShardedGN, edge_slice
+    from mast3r_slam_amd.distributed import ShardedGN, edge_shard
 
     dev = torch.device("cuda:0")
     g = _graph()
     E = g.n_edges
-    eb, ee, _ = edge_slice(E, rank, world)
+    ids, _ = edge_shard(E, rank, world)  # both halves of this rank's undirected edges
     Twc = g.T_init.data.clone().to(dev).contiguous()
     gn = ShardedGN(1, Twc, g.Xs.to(dev).contiguous(), g.Cs.to(dev).contiguous(), g.ii.to(dev), g.jj.to(dev),
-                   g.idx_ii2jj[eb:ee].to(dev).contiguous(), g.valid_match[eb:ee].to(dev).contiguous(),
-                   g.Q[eb:ee].to(dev).contiguous(), E, **SIG)
+                   g.idx_ii2jj[ids].to(dev).contiguous(), g.valid_match[ids].to(dev).contiguous(),
+                   g.Q[ids].to(dev).contiguous(), E, **SIG)
     gn.solve(ITERS, 0.0)
     torch.cuda.synchronize()
     np.save(os.path.join(out_dir, f"rank{rank}.npy"), Twc.cpu().numpy())

@@ -26,20 +26,23 @@ def be():
     return be
 
 
-def sharded_solve(be, mode, g, Xs, world, iters, delta, sig):
-    from mast3r_slam_amd.distributed import HipOps, edge_slice
+def sharded_solve(be, mode, g, Xs, world, iters, delta, sig, idx_dtype=torch.int64):
+    """Pair-preserving shards (distributed.edge_shard), the solve on the
+    payload-ordered edge list (distributed.payload_ids) as ShardedGN runs it."""
+    from mast3r_slam_amd.distributed import HipOps, edge_shard, payload_ids
 
     E = g.n_edges
+    ii_p, jj_p = payload_ids(g.ii.to(DEV), g.jj.to(DEV), world)
     ranks = []
     for r in range(world):
-        eb, ee, per = edge_slice(E, r, world)
+        ids, per = edge_shard(E, r, world)
         Twc = g.T_init.data.clone().to(DEV).contiguous()
-        ops = HipOps(mode, Twc, Xs, g.Cs.to(DEV).contiguous(), g.ii.to(DEV), g.jj.to(DEV),
-                     g.idx_ii2jj[eb:ee].to(DEV).contiguous(), g.valid_match[eb:ee].to(DEV).contiguous(),
-                     g.Q[eb:ee].to(DEV).contiguous(), E, g.K.to(DEV) if mode == be.MODE_CALIB else None,
+        ops = HipOps(mode, Twc, Xs, g.Cs.to(DEV).contiguous(), ii_p, jj_p,
+                     g.idx_ii2jj[ids].to(DEV).to(idx_dtype).contiguous(), g.valid_match[ids].to(DEV).contiguous(),
+                     g.Q[ids].to(DEV).contiguous(), len(ii_p), g.K.to(DEV) if mode == be.MODE_CALIB else None,
                      **sig)
         es = torch.zeros(per, ops.stride, dtype=torch.float64, device=DEV)
-        ranks.append((eb, ee, per, Twc, ops, es))
+        ranks.append((r * per, r * per + len(ids), per, Twc, ops, es))
     for *_, ops, _ in ranks:
         ops.prepare(delta)
     for _ in range(iters):
@@ -105,3 +108,19 @@ def test_sharded_natural_termination(be):
     its = [int(i[be.INFO_ITERS]) for i in infos]
     assert its[0] == its[1] < 20
     assert all(int(i[be.INFO_CONVERGED]) == 1 for i in infos)
+
+
+def test_sharded_int32_idx_matches_int64(be):
+    """HipOps with the device edge store's int32 match indices (factor_graph
+    EdgeStore): idx_i32 is set for the C side, so the gathering linearize
+    reads 4-B ids; the poses are bitwise those of the int64 run."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(7, 48, 64, seed=41)
+    sig = dict(sigma_a=0.003, sigma_b=10.0, C_thresh=0.0, Q_thresh=1.5)
+    Xs = g.Xs.to(DEV).contiguous()
+    p64, i64 = sharded_solve(be, be.MODE_RAYS, g, Xs, 2, 4, 0.0, sig)
+    p32, i32 = sharded_solve(be, be.MODE_RAYS, g, Xs, 2, 4, 0.0, sig, idx_dtype=torch.int32)
+    for a, b in zip(p64, p32):
+        np.testing.assert_array_equal(a, b)
+    assert all(int(i[be.INFO_SOLVE_FAIL]) == 0 for i in i32)

@@ -194,3 +194,27 @@ def test_backend_oracle_singular_system_gives_zero_dx():
     assert failed == 1 and it == 1  # ||0|| < delta stops after one iteration
     assert np.all(dx == 0)
     np.testing.assert_array_equal(Twc, T0)
+
+
+@pytest.mark.parametrize("name", ["tracker_rays_64x48", "tracker_calib_64x48", "tracker_rays_identity_64x48",
+                                  "tracker_calib_identity_64x48"])
+def test_torch_tracker_matches_reference_tracker(golden_dir, name):
+    """oracle/tracker_torch.py (bench.py's PyTorch-CPU tracker baseline) is
+    the reference's tracker program: same iteration count, poses within the
+    fixture tolerance."""
+    import torch
+
+    from oracle import tracker_torch as trt
+
+    d = load(golden_dir, name)
+    t = {k: torch.from_numpy(np.asarray(v)) for k, v in d.items() if np.asarray(v).ndim > 0}
+    cfg = cfg_of(d)
+    if int(d["calib"]):
+        T_WCf, T_CkCf, it = trt.track_calib(t["Xf"], t["Xk"], t["T_WCf_init"], t["T_WCk"], t["Qk"], t["valid"],
+                                            t["meas_k"], t["valid_meas_k"], t["K"], (int(d["H"]), int(d["W"])), cfg)
+    else:
+        T_WCf, T_CkCf, it = trt.track_rays(t["Xf"], t["Xk"], t["T_WCf_init"], t["T_WCk"], t["Qk"], t["valid"], cfg)
+    assert it == int(d["n_iters"])
+    tol = pose_tol(d["tau_iter"])
+    np.testing.assert_allclose(T_WCf.numpy(), d["T_WCf"], atol=tol)
+    np.testing.assert_allclose(T_CkCf.numpy(), d["T_CkCf"], atol=tol)

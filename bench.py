@@ -29,7 +29,7 @@ same orchestration on CPU/gloo with no-op per-rank compute (a plumbing check:
 its timings mean nothing).
 
 Extra legs on rank 0 at N = 1:
-  cold         — the same steps with the host plan cache off (M3S_PLAN_CACHE=0):
+  cold         — the same steps with the host plan cache off (knob plan_cache=0):
                  the per-call symbolic analysis inside the timed region
   roofline     — the linearize kernel timed with HIP events on its stream
                  (+ the first-iteration gathering kernel and the solve launches)
@@ -251,9 +251,11 @@ def run(args):
 
     # cold calls: the host symbolic analysis (ordering, fill, schedule) inside
     # the timed region, as a SLAM backend call whose edge set changed pays it
-    os.environ["M3S_PLAN_CACHE"] = "0"
-    cold_el = timed(args.cold_steps) if args.cold_steps > 0 else None
-    del os.environ["M3S_PLAN_CACHE"]
+    if dry:
+        cold_el = None
+    else:
+        with be.knob("plan_cache", 0):
+            cold_el = timed(args.cold_steps) if args.cold_steps > 0 else None
 
     out = {
         "metric": METRIC,
@@ -287,7 +289,7 @@ def run(args):
         "cold": {
             "ms_per_step": round(cold_el / args.cold_steps * 1e3, 4) if cold_el else None,
             "gn_iters_per_s": round(args.iters * args.cold_steps / cold_el, 2) if cold_el else None,
-            "note": "plan cache off (M3S_PLAN_CACHE=0): every call re-runs the host symbolic "
+            "note": "plan cache off (knob plan_cache=0): every call re-runs the host symbolic "
                     "analysis, as a call on a changed edge set does",
         },
     }
@@ -434,7 +436,7 @@ def copy_leg(be, dev, nbytes=1 << 30, reps=20):
 def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
     """configs[1]: single-keyframe tracking GN at 512x512 (replicas only).
     The default path is the persistent one-launch tracker; the launch-per-
-    iteration path (M3S_TRACK_PERSISTENT=0) is timed beside it."""
+    iteration path (knob track_persistent=0) is timed beside it."""
     p = synthetic.make_pair(H, W, seed=1002, device=dev)
     a = (p.Xf.contiguous(), p.Xk.contiguous(), p.T_WCf_init.data.contiguous(), p.T_WCk.data.contiguous(),
          p.Qk.contiguous(), p.valid.contiguous())
@@ -452,15 +454,8 @@ def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
         return time.perf_counter() - t0
 
     dt = timed()
-    old = os.environ.get("M3S_TRACK_PERSISTENT")
-    os.environ["M3S_TRACK_PERSISTENT"] = "0"
-    try:
+    with be.knob("track_persistent", 0):
         dt_l = timed()
-    finally:
-        if old is None:
-            del os.environ["M3S_TRACK_PERSISTENT"]
-        else:
-            os.environ["M3S_TRACK_PERSISTENT"] = old
     return {"workload": "C2: 1 frame->keyframe pair, rays+dist Sim3 GN, %dx%d, %d fixed iterations"
                         % (H, W, iters),
             "gn_iters_per_s": round(reps * iters / dt, 1), "ms_per_solve": round(dt / reps * 1e3, 4),
@@ -469,7 +464,7 @@ def tracker_leg(be, synthetic, dev, H, W, iters=10, reps=50):
             "bound": "latency: one grid-wide arrival + all-partials read per iteration",
             "launch_per_iter": {"gn_iters_per_s": round(reps * iters / dt_l, 1),
                                 "ms_per_solve": round(dt_l / reps * 1e3, 4),
-                                "note": "M3S_TRACK_PERSISTENT=0: one linearize launch per iteration, "
+                                "note": "knob track_persistent=0: one linearize launch per iteration, "
                                         "45 B per pixel re-read each time"}}
 
 

@@ -191,6 +191,16 @@ int m3s_debug_stamps(int which, int64_t *out);
  *   op 6 act as the 3x4 matrix form the linearize kernels use -> out point
  *   op 7 Adj(a)^-T as a row-major 7x7 (apply_Sim3_adj_inv :274-297) -> out 49 */
 int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n, void *stream);
+/* Solver knobs (experiments / A/B tests). Defaults are the measured best;
+ * the environment (M3S_PLAN_CACHE, M3S_DENSE, M3S_DENSE_TAIL_MIN, M3S_COLS,
+ * M3S_DF, M3S_TAIL_CYC, M3S_TAIL_MFMA, M3S_BORDER_SPLIT,
+ * M3S_TRACK_PERSISTENT) is read once per process; this sets a knob at run
+ * time for the calls that follow. Names: plan_cache, dense, dense_tail_min,
+ * cols, df, tail_cyc, tail_mfma, border_split, track_persistent,
+ * debug_drop_item (test hook: drop one dispatch item of the one-workgroup
+ * LLT so its bounded waits time out). Returns the previous value, or
+ * -2^30 for an unknown name. */
+int m3s_set_knob(const char *name, int value);
 /* Diagnostic (bench.py's measured HBM ceiling): copy nbytes (a multiple of
  * 16, 16-B aligned device pointers) with 16-B non-temporal loads and stores,
  * `blocks` workgroups of 256 lanes, asynchronously on `stream`. */

@@ -32,7 +32,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <cstring>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <tuple>
@@ -3350,35 +3353,45 @@ __global__ void __launch_bounds__(64 * kBorderWaves) border_kernel(SparseDev D) 
     border_task<true>(t, nc, c0, pl, D.off, D.L, y, r7, c7, lane49, lane, lane7, act49, stg, D.tail_A, D.tail_ld);
 }
 
-inline bool cols_path() {  // M3S_COLS=0: large graphs on sparse_llt_kernel's one workgroup (A/B)
-  const char *e = std::getenv("M3S_COLS");
-  return !(e && e[0] == '0');
+// Solver knobs: the measured-best defaults, overridable per process by the
+// environment (read ONCE, at the first solve) and at run time by
+// m3s_set_knob (tests and bench legs that A/B a path in one process).
+struct Knobs {
+  std::atomic<int> plan_cache{1};      // M3S_PLAN_CACHE: 0 = symbolic analysis every call (cold calls)
+  std::atomic<int> dense{0};           // M3S_DENSE: 1 = dense fallback LLT
+  std::atomic<int> dense_tail_min{kDenseTailMin};  // M3S_DENSE_TAIL_MIN: smallest dense tail (0: never)
+  std::atomic<int> cols{1};            // M3S_COLS: 0 = large graphs on sparse_llt_kernel's one workgroup (A/B)
+  std::atomic<int> df{1};              // M3S_DF: 0 = column tasks + border_kernel instead of the dataflow (A/B)
+  std::atomic<int> tail_cyc{1};        // M3S_TAIL_CYC: 0 = the dense tail on one workgroup (A/B)
+  std::atomic<int> tail_mfma{1};       // M3S_TAIL_MFMA: 0 = the dense tail in sparse_llt_kernel (A/B)
+  std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel (A/B)
+  std::atomic<int> track_persistent{1};  // M3S_TRACK_PERSISTENT: 0 = one tracker launch per iteration
+  std::atomic<int> debug_drop_item{-1};  // test hook only (m3s_set_knob): drop one LLT dispatch item
+  Knobs() {
+    auto env = [](const char *name, std::atomic<int> &v) {
+      if (const char *e = std::getenv(name)) v = std::atoi(e);
+    };
+    env("M3S_PLAN_CACHE", plan_cache);
+    env("M3S_DENSE", dense);
+    env("M3S_DENSE_TAIL_MIN", dense_tail_min);
+    env("M3S_COLS", cols);
+    env("M3S_DF", df);
+    env("M3S_TAIL_CYC", tail_cyc);
+    env("M3S_TAIL_MFMA", tail_mfma);
+    env("M3S_BORDER_SPLIT", border_split);
+    env("M3S_TRACK_PERSISTENT", track_persistent);
+  }
+};
+Knobs &knobs() {
+  static Knobs k;  // thread-safe one-time initialisation
+  return k;
 }
-
-inline bool df_path() {  // M3S_DF=0: column tasks + border_kernel instead of the block dataflow (A/B)
-  const char *e = std::getenv("M3S_DF");
-  return !(e && e[0] == '0');
-}
-
-inline bool tail_cyc() {  // M3S_TAIL_CYC=0: the dense tail on one workgroup (tail_llt_kernel, A/B)
-  const char *e = std::getenv("M3S_TAIL_CYC");
-  return !(e && e[0] == '0');
-}
-
-inline bool tail_mfma() {  // M3S_TAIL_MFMA=0: the dense tail in sparse_llt_kernel (A/B)
-  const char *e = std::getenv("M3S_TAIL_MFMA");
-  return !(e && e[0] == '0');
-}
-
-inline bool border_split() {  // M3S_BORDER_SPLIT=0: tail border inside the one-workgroup kernel (A/B)
-  const char *e = std::getenv("M3S_BORDER_SPLIT");
-  return !(e && e[0] == '0');
-}
-
-inline int dense_tail_min() {
-  const char *e = std::getenv("M3S_DENSE_TAIL_MIN");
-  return e ? std::atoi(e) : kDenseTailMin;
-}
+inline bool cols_path() { return knobs().cols != 0; }
+inline bool df_path() { return knobs().df != 0; }
+inline bool tail_cyc() { return knobs().tail_cyc != 0; }
+inline bool tail_mfma() { return knobs().tail_mfma != 0; }
+inline bool border_split() { return knobs().border_split != 0; }
+inline int dense_tail_min() { return knobs().dense_tail_min; }
 
 struct PlanMeta {
   int epoch = 0;  // solve launches since m3s_gn_prepare (column-task flags / tickets)
@@ -3404,7 +3417,25 @@ struct PlanMeta {
   int64_t range_b = -1, range_e = -1, n_blocks = 0;
   bool planes_ok = false;
   std::vector<int32_t> tasks;
+  // the symbolic plan of this call is built by its first solve (cache miss at
+  // prepare): the host analysis then overlaps the first linearize kernel
+  bool plan_pending = false;
+  bool force_dense = false;
 };
+
+// What a solve launch reads of the registry entry: the scalars and plan
+// offsets, not the host vectors (ranks, task tables, plan image) that the
+// entry keeps alive for queued uploads.
+PlanMeta solve_view(const PlanMeta &M) {
+  PlanMeta v;
+  v.epoch = M.epoch, v.sparse = M.sparse, v.store = M.store, v.asm_lds = M.asm_lds, v.lds_bytes = M.lds_bytes;
+  v.m = M.m, v.S = M.S, v.levels = M.levels, v.plan_len = M.plan_len, v.n_items = M.n_items;
+  v.n_tasks = M.n_tasks, v.n_parts = M.n_parts, v.nc = M.nc, v.off_dfitems = M.off_dfitems;
+  v.n_dfitems = M.n_dfitems;
+  v.img = M.img;  // offsets (its data vector is empty in the registry)
+  v.plan_pending = M.plan_pending;
+  return v;
+}
 std::mutex g_reg_mu;
 std::unordered_map<const void *, PlanMeta> g_reg;
 
@@ -3501,6 +3532,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 }
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;
+int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st);
 
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
@@ -3512,12 +3544,14 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
   int32_t *stop = flags + kFlagStop;
   const int64_t n = Ly.n, ld = Ly.ld;
   if (a->N <= 1) return M3S_OK;
+  int rc0 = finish_plan(a, Ly, st);
+  if (rc0) return rc0;
   PlanMeta meta;
   {
     std::lock_guard<std::mutex> g(g_reg_mu);
     auto it = g_reg.find(ws);
     if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
-    meta = it->second;
+    meta = solve_view(it->second);
     it->second.epoch++;
   }
   int rc;
@@ -3755,10 +3789,7 @@ struct PlanCacheEntry {
 std::mutex g_cache_mu;
 // M3S_PLAN_CACHE=0: every solve call runs the host symbolic analysis (cold
 // calls; bench.py times them this way beside the cached figure)
-inline bool plan_cache_enabled() {
-  const char *e = std::getenv("M3S_PLAN_CACHE");
-  return !(e && e[0] == '0');
-}
+inline bool plan_cache_enabled() { return knobs().plan_cache != 0; }
 std::vector<PlanCacheEntry> g_cache;  // most recent first
 constexpr size_t kPlanCacheSize = 4;
 
@@ -3783,11 +3814,17 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
   const int64_t E = a->E;
   if (a->N > 1) {
     SparsePlan P;
-    // split long update lists only when the factor lives in global memory
-    // (its products are the slow, staged ones there)
-    build_sparse_plan((int)a->N, ri, rj, P, 0, 0, dense_tail_min());
-    if (sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) > kMaxLdsBytes)
-      build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1, dense_tail_min());
+    // The dispatch schedule (witems) and the split update lists (PART items)
+    // serve only the one-workgroup sparse_llt_kernel; a factor in global
+    // memory on the chip-wide path (df_factor / tail / column back-
+    // substitution) needs neither: at 256 KFs that halves the host analysis.
+    build_sparse_plan((int)a->N, ri, rj, P, 0, 0, dense_tail_min(), false);
+    const bool global_factor = sizeof(double) * ((size_t)(P.S + P.m) * 49 + (size_t)P.m * 7) > kMaxLdsBytes;
+    const bool chip_path = global_factor && cols_path() && P.m <= 512 && (P.nc == 0 || 7 * P.nc + 1 <= 16 * kTailMaxT);
+    if (global_factor && !chip_path)  // split long update lists for the staged global-factor products
+      build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1, dense_tail_min(), true);
+    else if (!chip_path)
+      schedule_plan_items(P);
     PlanImage img;
     flatten_plan(P, img);
     // df_factor_kernel's dispatch list: the sparse columns in level order,
@@ -3840,14 +3877,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       meta.img = img;
     }
   }
-  meta.rj = rj;
-  meta.h_ri = ri;
-  // task table of the full edge range (the single-GPU call and world size 1);
-  // a sharded rank's first m3s_gn_linearize builds its own
-  if (E > 0) {
-    build_tasks(meta.rj, 0, E, chunks_for(a->HW, E), meta.tasks);
-    meta.n_blocks_full = (int64_t)meta.tasks.size();
-  }
+  (void)E;
   return meta;
 }
 
@@ -3861,13 +3891,15 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
 // host-synchronous transfer each (~7 per call); the event guards the upload
 // buffer until the previous call's copy has left it.
 struct Staging {
-  std::mutex mu;
-  char *down = nullptr, *up = nullptr;
-  size_t down_cap = 0, up_cap = 0;
-  hipEvent_t ev = nullptr;
-  bool pending = false;
+  char *down = nullptr, *up = nullptr, *plan_up = nullptr;
+  size_t down_cap = 0, up_cap = 0, plan_cap = 0;
+  hipEvent_t ev = nullptr, plan_ev = nullptr;
+  bool pending = false, plan_pending = false;
 };
-Staging g_stage;
+// One staging set per device: an event recorded on one device's stream cannot
+// guard another device's copies (a process may drive GN on several GPUs).
+std::mutex g_stage_mu;
+std::unordered_map<int, Staging> g_stages;
 bool pinned_reserve(char *&p, size_t &cap, size_t need) {
   if (need <= cap) return true;
   if (p) (void)hipHostFree(p);
@@ -3877,18 +3909,55 @@ bool pinned_reserve(char *&p, size_t &cap, size_t need) {
   cap = n;
   return true;
 }
+Staging *stage_for_device() {  // caller holds g_stage_mu
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  Staging &S = g_stages[dev];
+  if (!S.ev && hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (!S.plan_ev && hipEventCreateWithFlags(&S.plan_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return &S;
+}
+
+// The per-call flag state the solve kernels of a plan rely on: the column-
+// task / dataflow / dense-tail epoch flags live only on the global-factor
+// path (the LDS-resident factors keep theirs in LDS), and no tagged granule
+// of an earlier call may match this call's epochs.
+bool reset_plan_flags(const PlanMeta &M, const Layout &Ly, void *ws, hipStream_t st) {
+  bool ok = true;
+  if (!(M.sparse && M.store != 0))
+    ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
+  if (M.nc > 0)
+    ok &= hipMemsetAsync(at<double>(ws, Ly.tail) + tail_gran_offset_doubles(), 0,
+                         sizeof(double) * (tail_scratch_doubles() - tail_gran_offset_doubles()), st) == hipSuccess;
+  return ok;
+}
+
+// Test hook for the bounded waits (tests/test_gpu_backend.py, knob
+// debug_drop_item): drop one item of sparse_llt_kernel's dispatch list, so the
+// items that read its blocks wait on a flag that is never set; the waits time
+// out and the iteration ends as a solve failure (dx = 0) instead of hanging.
+void apply_drop_item(PlanMeta &M) {
+  const int d = knobs().debug_drop_item;
+  if (d < 0 || !M.sparse || M.h_plan.empty() || M.img.off_wave_ptr >= (int64_t)M.h_plan.size()) return;
+  int32_t *wp = M.h_plan.data() + M.img.off_wave_ptr, *wi = M.h_plan.data() + M.img.off_witems;
+  if (d < wp[1]) {
+    for (int t = d; t + 1 < wp[1]; t++) wi[t] = wi[t + 1];
+    wp[1] -= 1;
+  }
+}
 
 int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
-  std::lock_guard<std::mutex> stage_lock(g_stage.mu);
-  if (!g_stage.ev && hipEventCreateWithFlags(&g_stage.ev, hipEventDisableTiming) != hipSuccess) return M3S_ELAUNCH;
-  if (g_stage.pending && hipEventSynchronize(g_stage.ev) != hipSuccess) return M3S_ELAUNCH;
-  g_stage.pending = false;
+  std::lock_guard<std::mutex> stage_lock(g_stage_mu);
+  Staging *SG = stage_for_device();
+  if (!SG) return M3S_ELAUNCH;
+  if (SG->pending && hipEventSynchronize(SG->ev) != hipSuccess) return M3S_ELAUNCH;
+  SG->pending = false;
   const int64_t E = a->E;
-  if (!pinned_reserve(g_stage.down, g_stage.down_cap, 64 + 2 * sizeof(int64_t) * (size_t)E)) return M3S_ELAUNCH;
-  float *hK = reinterpret_cast<float *>(g_stage.down);  // calib intrinsics, read with ii/jj
-  int64_t *hii = reinterpret_cast<int64_t *>(g_stage.down + 64), *hjj = hii + E;
+  if (!pinned_reserve(SG->down, SG->down_cap, 64 + 2 * sizeof(int64_t) * (size_t)E)) return M3S_ELAUNCH;
+  float *hK = reinterpret_cast<float *>(SG->down);  // calib intrinsics, read with ii/jj
+  int64_t *hii = reinterpret_cast<int64_t *>(SG->down + 64), *hjj = hii + E;
   for (int q = 0; q < 9; q++) hK[q] = 0.f;
   if (a->mode == M3S_MODE_CALIB &&
       hipMemcpyAsync(hK, a->K, sizeof(float) * 9, hipMemcpyDeviceToHost, st) != hipSuccess)
@@ -3903,37 +3972,35 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   std::vector<int32_t> ri, rj;
   const int nu = host_remap(hii, hjj, E, ri, rj);
   const bool bad = nu > a->N;
-  const char *fd = std::getenv("M3S_DENSE");
-  const bool force_dense = fd && fd[0] == '1';
+  const bool force_dense = knobs().dense == 1;
   PlanMeta meta;
-  if (!bad) {
-    bool hit = false;
-    const bool use_cache = plan_cache_enabled();
-    if (use_cache) {
-      std::lock_guard<std::mutex> g(g_cache_mu);
-      for (size_t q = 0; q < g_cache.size(); q++) {
-        const PlanCacheEntry &C = g_cache[q];
-        if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense &&
-            C.tail_min == dense_tail_min() && C.ri == ri && C.rj == rj) {
-          meta = C.meta;
-          std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
-          hit = true;
-          break;
-        }
+  bool hit = false;
+  if (!bad && plan_cache_enabled()) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    for (size_t q = 0; q < g_cache.size(); q++) {
+      const PlanCacheEntry &C = g_cache[q];
+      if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense &&
+          C.tail_min == dense_tail_min() && C.ri == ri && C.rj == rj) {
+        meta = C.meta;
+        std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
+        hit = true;
+        break;
       }
     }
-    if (!hit) {
-      meta = build_plan_meta(a, Ly, ri, rj, force_dense);
-      PlanCacheEntry C;
-      C.N = a->N, C.HW = a->HW, C.E = E, C.dense = force_dense, C.ri = ri, C.rj = rj, C.meta = meta;
-      C.tail_min = dense_tail_min();
-      std::lock_guard<std::mutex> g(g_cache_mu);
-      if (use_cache) g_cache.insert(g_cache.begin(), std::move(C));
-      if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
-    }
-  } else {
+  }
+  if (!hit) {
+    // ranks and the full-range task table now (the first linearize needs
+    // them); the symbolic plan is built by the first solve of this call,
+    // while the first linearize kernel runs (finish_plan)
     meta.h_ri = ri;
     meta.rj = rj;
+    if (E > 0) {
+      build_tasks(meta.rj, 0, E, chunks_for(a->HW, E), meta.tasks);
+      meta.n_blocks_full = (int64_t)meta.tasks.size();
+    }
+    meta.sparse = !bad && !force_dense && a->N > 1;  // the expected outcome (the dense path reads partials either way)
+    meta.plan_pending = !bad && a->N > 1;
+    meta.force_dense = force_dense;
   }
   for (int q = 0; q < 8; q++) meta.h_info[q] = 0;
   for (int q = 0; q < 64; q++) meta.h_flags[q] = 0;
@@ -3949,42 +4016,25 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   } else {
     meta.range_b = meta.range_e = -1, meta.n_blocks = 0;
   }
-  if (meta.sparse && meta.lds_bytes > 64 * 1024) set_lds_attributes_once();
+  if (meta.sparse && !meta.plan_pending && meta.lds_bytes > 64 * 1024) set_lds_attributes_once();
   std::lock_guard<std::mutex> g(g_reg_mu);
   PlanMeta &M = g_reg[ws];
   M = std::move(meta);
   bool ok = true;
-  // the column-task / dataflow / dense-tail flags live only on the global-factor
-  // path; the LDS-resident factors (store 1 / 2) keep theirs in LDS
-  if (!(M.sparse && M.store != 0))
-    ok &= hipMemsetAsync(at<int32_t>(ws, Ly.colsync), 0, Ly.tail - Ly.colsync, st) == hipSuccess;
-  if (M.nc > 0)  // the tail's tagged granules: no tag of an earlier call may match this call's epochs
-    ok &= hipMemsetAsync(at<double>(ws, Ly.tail) + tail_gran_offset_doubles(), 0,
-                         sizeof(double) * (tail_scratch_doubles() - tail_gran_offset_doubles()), st) == hipSuccess;
+  if (!M.plan_pending) ok &= reset_plan_flags(M, Ly, ws, st);
   M.epoch = 0;
-
-  // Test hook for the bounded waits (tests/test_gpu_backend.py): drop one item
-  // of sparse_llt_kernel's dispatch list, so the items that read its blocks
-  // wait on a flag that is never set; the waits time out and the iteration
-  // ends as a solve failure (dx = 0) instead of hanging.
-  if (const char *e = std::getenv("M3S_DEBUG_DROP_ITEM"); e && M.sparse && !M.h_plan.empty()) {
-    const int d = std::atoi(e);
-    int32_t *wp = M.h_plan.data() + M.img.off_wave_ptr, *wi = M.h_plan.data() + M.img.off_witems;
-    if (d >= 0 && d < wp[1]) {
-      for (int t = d; t + 1 < wp[1]; t++) wi[t] = wi[t + 1];
-      wp[1] -= 1;
-    }
-  }
-  // one upload: flags | rank_i | rank_j | tasks | plan (the layout keeps them
-  // in this order), then info (the caller's tensor) from the same buffer
-  const bool with_plan = M.sparse && !M.h_plan.empty();
+  if (!M.plan_pending) apply_drop_item(M);
+  // one upload: flags | rank_i | rank_j | edge counters | tasks [| plan] (the
+  // layout keeps them in this order), then info (the caller's tensor) from
+  // the same buffer
+  const bool with_plan = M.sparse && !M.plan_pending && !M.h_plan.empty();
   const bool with_tasks = M.n_blocks > 0;
   size_t n_up = with_plan ? Ly.plan - Ly.flags + sizeof(int32_t) * M.h_plan.size()
                           : with_tasks ? Ly.tasks - Ly.flags + sizeof(int32_t) * M.tasks.size()
                                        : Ly.edge_cnt - Ly.flags + edge_cnt_bytes(E);
   n_up = align_up(n_up, 16);
-  if (!pinned_reserve(g_stage.up, g_stage.up_cap, n_up + sizeof M.h_info)) return M3S_ELAUNCH;
-  char *up = g_stage.up;
+  if (!pinned_reserve(SG->up, SG->up_cap, n_up + sizeof M.h_info)) return M3S_ELAUNCH;
+  char *up = SG->up;
   memcpy(up, M.h_flags, sizeof M.h_flags);
   memset(up + (Ly.edge_cnt - Ly.flags), 0, edge_cnt_bytes(E));  // the fused finalize's counters
   if (E > 0) {
@@ -3996,8 +4046,65 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   memcpy(up + n_up, M.h_info, sizeof M.h_info);
   ok &= hipMemcpyAsync(at<char>(ws, Ly.flags), up, n_up, hipMemcpyHostToDevice, st) == hipSuccess;
   ok &= hipMemcpyAsync(a->info, up + n_up, sizeof M.h_info, hipMemcpyHostToDevice, st) == hipSuccess;
-  ok &= hipEventRecord(g_stage.ev, st) == hipSuccess;
-  g_stage.pending = ok;
+  ok &= hipEventRecord(SG->ev, st) == hipSuccess;
+  SG->pending = ok;
+  return ok ? M3S_OK : M3S_ELAUNCH;
+}
+
+// The deferred half of a cold prepare: the symbolic plan (ordering, fill,
+// update lists; build_plan_meta) on the host, its upload, and the per-plan
+// flag resets. Called by a call's first solve, i.e. after its first
+// linearize is on the stream: the analysis runs while that kernel does.
+int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st) {
+  void *ws = a->workspace;
+  std::vector<int32_t> ri, rj;
+  bool force_dense;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(ws);
+    if (it == g_reg.end()) return M3S_EINVAL;
+    if (!it->second.plan_pending) return M3S_OK;
+    ri = it->second.h_ri;
+    rj = it->second.rj;
+    force_dense = it->second.force_dense;
+  }
+  PlanMeta built = build_plan_meta(a, Ly, ri, rj, force_dense);
+  if (built.sparse && built.lds_bytes > 64 * 1024) set_lds_attributes_once();
+  std::lock_guard<std::mutex> stage_lock(g_stage_mu);
+  Staging *SG = stage_for_device();
+  if (!SG) return M3S_ELAUNCH;
+  if (SG->plan_pending && hipEventSynchronize(SG->plan_ev) != hipSuccess) return M3S_ELAUNCH;
+  SG->plan_pending = false;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  PlanMeta &M = g_reg[ws];
+  M.sparse = built.sparse, M.store = built.store, M.asm_lds = built.asm_lds, M.lds_bytes = built.lds_bytes;
+  M.m = built.m, M.S = built.S, M.levels = built.levels, M.plan_len = built.plan_len;
+  M.n_items = built.n_items, M.n_tasks = built.n_tasks, M.n_parts = built.n_parts, M.nc = built.nc;
+  M.off_dfitems = built.off_dfitems, M.n_dfitems = built.n_dfitems;
+  M.img = built.img;
+  M.h_plan = std::move(built.h_plan);
+  M.plan_pending = false;
+  if (plan_cache_enabled()) {
+    PlanCacheEntry C;
+    C.N = a->N, C.HW = a->HW, C.E = a->E, C.dense = force_dense, C.ri = ri, C.rj = rj;
+    C.tail_min = dense_tail_min();
+    C.meta = M;
+    C.meta.tasks_r.clear();
+    C.meta.tasks_old.clear();
+    std::lock_guard<std::mutex> gc(g_cache_mu);
+    g_cache.insert(g_cache.begin(), std::move(C));
+    if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
+  }
+  bool ok = reset_plan_flags(M, Ly, ws, st);
+  apply_drop_item(M);
+  if (M.sparse && !M.h_plan.empty()) {
+    const size_t nb = sizeof(int32_t) * M.h_plan.size();
+    if (!pinned_reserve(SG->plan_up, SG->plan_cap, nb)) return M3S_ELAUNCH;
+    memcpy(SG->plan_up, M.h_plan.data(), nb);
+    ok &= hipMemcpyAsync(at<char>(ws, Ly.plan), SG->plan_up, nb, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok &= hipEventRecord(SG->plan_ev, st) == hipSuccess;
+    SG->plan_pending = ok;
+  }
   return ok ? M3S_OK : M3S_ELAUNCH;
 }
 
@@ -4407,10 +4514,7 @@ int track_ppl(int64_t HW) {
   return 0;
 }
 // M3S_TRACK_PERSISTENT=0: one launch per iteration (A/B of the persistent kernel)
-bool track_persistent_enabled() {
-  const char *e = std::getenv("M3S_TRACK_PERSISTENT");
-  return !(e && e[0] == '0');
-}
+bool track_persistent_enabled() { return knobs().track_persistent != 0; }
 
 int track_impl(const m3s_track_args *a, int mode, void *stream) {
   if (!a || !a->Xf || !a->Xk || !a->Qk || !a->valid || !a->T_WCf || !a->T_WCk || !a->T_WCf_out ||
@@ -4631,6 +4735,24 @@ int m3s_debug_stamps(int which, int64_t *out) {
   (void)which;
   (void)out;
   return 0;
+}
+
+int m3s_set_knob(const char *name, int value) {
+  if (!name) return M3S_EINVAL;
+  Knobs &k = knobs();
+  const struct {
+    const char *n;
+    std::atomic<int> *v;
+  } tab[] = {{"plan_cache", &k.plan_cache}, {"dense", &k.dense}, {"dense_tail_min", &k.dense_tail_min},
+             {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc}, {"tail_mfma", &k.tail_mfma},
+             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent},
+             {"debug_drop_item", &k.debug_drop_item}};
+  for (const auto &t : tab)
+    if (std::strcmp(t.n, name) == 0) {
+      const int old = t.v->exchange(value);
+      return old;
+    }
+  return -(1 << 30);
 }
 
 int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void *stream) {

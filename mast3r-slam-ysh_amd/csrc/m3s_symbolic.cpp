@@ -263,8 +263,10 @@ static void schedule_items(SparsePlan &P) {
   P.wave_ptr.push_back((int32_t)P.witems.size());
 }
 
+void schedule_plan_items(SparsePlan &P) { schedule_items(P); }
+
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
-                       SparsePlan &P, int split, int64_t max_parts, int dense_min) {
+                       SparsePlan &P, int split, int64_t max_parts, int dense_min, bool schedule) {
   const int m = N > 1 ? N - 1 : 0;
   const int64_t E = (int64_t)ri.size();
   P = SparsePlan();
@@ -390,7 +392,7 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     for (int ri = ci + 1; ri < nc; ri++)
       if (P.task_dst[ct0[ci] + ri - ci - 1] != P.S - nc * (nc - 1) / 2 + ci * nc - ci * (ci + 1) / 2 + ri - ci - 1)
         nc = -1;  // not contiguous (never expected): no dense tail
-  if (nc < 0) return build_sparse_plan(N, ri, rj, P, split, max_parts, 0);
+  if (nc < 0) return build_sparse_plan(N, ri, rj, P, split, max_parts, 0, schedule);
   P.clq.assign(1, nc);
   P.clq.push_back(c0);
   P.clq.insert(P.clq.end(), ct0.begin(), ct0.end());
@@ -446,7 +448,7 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
       }
     P.items.swap(items);
   }
-  schedule_items(P);
+  if (schedule) schedule_items(P);
   // assembly lists (edge order => deterministic sums)
   std::vector<std::vector<int32_t>> asl(P.S), gl(m);
   for (int64_t e = 0; e < E; e++) {

@@ -72,8 +72,12 @@ int host_remap(const int64_t *ii, const int64_t *jj, int64_t E, std::vector<int3
 // split > 0 enables PART items of `split` updates each (at most max_parts).
 // dense_min: smallest top clique handled as a dense tail (0: never)
 constexpr int kDenseTailMin = 16;  // measured (ab_dense_tail_min.txt): a win at 42 (N = 256) and at 18 (N = 128, factor + back-sub 339 -> 253 us), a loss at 10 (N = 64)
+// schedule = false leaves wave_ptr / witems empty (only sparse_llt_kernel, the
+// one-workgroup factor, reads them; schedule_plan_items fills them later)
 void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<int32_t> &rj,
-                       SparsePlan &P, int split = 0, int64_t max_parts = 0, int dense_min = kDenseTailMin);
+                       SparsePlan &P, int split = 0, int64_t max_parts = 0, int dense_min = kDenseTailMin,
+                       bool schedule = true);
+void schedule_plan_items(SparsePlan &P);
 
 // Flattened int32 image of the plan (offsets of each array into it).
 struct PlanImage {

@@ -121,7 +121,7 @@ EXPORTS = (
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
     "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
     "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_debug_stamps", "m3s_debug_sim3",
-    "m3s_debug_copy",
+    "m3s_debug_copy", "m3s_set_knob",
 )
 FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2, "weighted_spherical": 3}
 
@@ -168,6 +168,8 @@ def _load(path=LIB_PATH):
     lib.m3s_debug_stamps.argtypes = [ctypes.c_int, _VP]
     lib.m3s_debug_sim3.restype = ctypes.c_int
     lib.m3s_debug_sim3.argtypes = [ctypes.c_int, _VP, _VP, _VP, ctypes.c_int64, _VP]
+    lib.m3s_set_knob.restype = ctypes.c_int
+    lib.m3s_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.m3s_debug_copy.restype = ctypes.c_int
     lib.m3s_debug_copy.argtypes = [_VP, _VP, ctypes.c_int64, ctypes.c_int, _VP]
     lib.m3s_gn_layout_debug.restype = ctypes.c_size_t
@@ -215,6 +217,29 @@ def debug_sim3(op: str, a: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor
     out = torch.empty(n, wo, dtype=torch.float32, device=a.device)
     _raise(_lib.m3s_debug_sim3(code, _p(a), _p(b), _p(out), n, _stream(a.device)), "m3s_debug_sim3")
     return out
+
+
+def set_knob(name: str, value: int) -> int:
+    """Set a solver knob for the calls that follow (include/m3s_gn.h
+    m3s_set_knob); returns the previous value."""
+    old = _lib.m3s_set_knob(name.encode(), int(value))
+    if old == -(1 << 30):
+        raise RuntimeError(f"unknown knob {name!r}")
+    return old
+
+
+class knob:
+    """``with knob("df", 0): ...`` — a knob set for the block, restored after."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.old = set_knob(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_knob(self.name, self.old)
 
 
 def debug_copy(src: torch.Tensor, dst: torch.Tensor, blocks: int = 4096):

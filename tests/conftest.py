@@ -19,3 +19,19 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture
+def knobs():
+    """knobs(name, value): set a solver knob (m3s_set_knob) for this test;
+    every knob set is restored at teardown."""
+    import mast3r_slam_backends as be
+
+    saved = []
+
+    def set_(name, value):
+        saved.append((name, be.set_knob(name, int(value))))
+
+    yield set_
+    for name, old in reversed(saved):
+        be.set_knob(name, old)

@@ -173,9 +173,9 @@ def test_gn_singular_system_zero_dx(be):
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
 
 
-def test_gn_broken_plan_times_out_as_solve_failure(be, monkeypatch):
+def test_gn_broken_plan_times_out_as_solve_failure(be, knobs):
     """A plan bug must end as a solve failure, never a hang (the LLT's flag
-    waits are bounded). M3S_DEBUG_DROP_ITEM removes the first item of the
+    waits are bounded). the debug_drop_item knob removes the first item of the
     dispatch list (a leaf DIAG): the items reading its blocks time out, the
     iteration reports INFO_SOLVE_FAIL with dx = 0 and the poses untouched."""
     import time
@@ -183,7 +183,7 @@ def test_gn_broken_plan_times_out_as_solve_failure(be, monkeypatch):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(12, 24, 32, seed=37)
-    monkeypatch.setenv("M3S_DEBUG_DROP_ITEM", "0")
+    knobs("debug_drop_item", "0")
     t0 = time.time()
     T_gpu, dx, info = run_gpu(be, "rays", g, 1, 0.0)
     dt = time.time() - t0
@@ -191,7 +191,7 @@ def test_gn_broken_plan_times_out_as_solve_failure(be, monkeypatch):
     assert np.all(dx == 0)
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
     assert dt < 60.0
-    monkeypatch.delenv("M3S_DEBUG_DROP_ITEM")
+    knobs("debug_drop_item", -1)
     T_ok, _, info = run_gpu(be, "rays", g, 1, 0.0)  # the same graph, intact plan
     assert info[be.INFO_SOLVE_FAIL] == 0 and not np.array_equal(T_ok, g.T_init.data.numpy())
 
@@ -304,36 +304,36 @@ def test_gn_tiled_cholesky_singular_zero_dx(be):
 
 
 @pytest.mark.parametrize("N,tail", [(6, "8"), (32, "8"), (70, "8"), (32, "3"), (70, "0"), (140, "8"), (256, "24")])
-def test_sparse_llt_matches_dense_llt(be, N, tail, monkeypatch):
+def test_sparse_llt_matches_dense_llt(be, N, tail, knobs):
     """Block-sparse LLT (default; LDS-resident for small plans, global for
     N >= 70; the top clique as a dense right-looking tail when it has at least
     M3S_DENSE_TAIL_MIN columns, 0 = never) against the dense fallback
     (M3S_DENSE=1) on identical inputs."""
     from mast3r_slam_amd import synthetic
 
-    monkeypatch.setenv("M3S_DENSE_TAIL_MIN", tail)
+    knobs("dense_tail_min", tail)
     g = synthetic.make_graph(N, 24, 32, seed=90 + N)
     T_s, dx_s, info_s = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.setenv("M3S_DENSE", "1")
+    knobs("dense", "1")
     T_d, dx_d, info_d = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.delenv("M3S_DENSE")
+    knobs("dense", 0)
     assert info_s[be.INFO_ITERS] == info_d[be.INFO_ITERS] == 3
     np.testing.assert_allclose(dx_s, dx_d, atol=1e-6 + 1e-5 * np.abs(dx_d).max())
     np.testing.assert_allclose(T_s, T_d, atol=1e-5)
 
 
-def test_mfma_tail_matches_block_tail_and_is_deterministic(be, monkeypatch):
+def test_mfma_tail_matches_block_tail_and_is_deterministic(be, knobs):
     """Global factor with a dense tail: tail_llt_kernel (the top clique on the
     f64 MFMA, 16x16 tiles, the default) against the 7x7-block tail of
     sparse_llt_kernel (M3S_TAIL_MFMA=0) on identical inputs; the MFMA path is
     bitwise reproducible run to run (the sharded ranks rely on it)."""
     from mast3r_slam_amd import synthetic
 
-    monkeypatch.setenv("M3S_DENSE_TAIL_MIN", "8")
+    knobs("dense_tail_min", "8")
     g = synthetic.make_graph(140, 24, 32, seed=77)
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.setenv("M3S_TAIL_MFMA", "0")
+    knobs("tail_mfma", "0")
     T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
     assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
     assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
@@ -366,7 +366,7 @@ def test_mfma_tail_one_step_matches_oracle(be, N):
 
 
 @pytest.mark.parametrize("N", [90, 140, 256])
-def test_block_dataflow_matches_column_tasks_bitwise(be, N, monkeypatch):
+def test_block_dataflow_matches_column_tasks_bitwise(be, N, knobs):
     """Large graphs: the wave-level block dataflow (df_factor_kernel, the
     default: DIAG / OFF / tail-border items over the chip) sums every block's
     update list in the same order as the column tasks + border_kernel path
@@ -375,7 +375,7 @@ def test_block_dataflow_matches_column_tasks_bitwise(be, N, monkeypatch):
 
     g = synthetic.make_graph(N, 12, 16, seed=700 + N)
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.setenv("M3S_DF", "0")
+    knobs("df", "0")
     T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
     assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
     assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
@@ -384,7 +384,7 @@ def test_block_dataflow_matches_column_tasks_bitwise(be, N, monkeypatch):
 
 
 @pytest.mark.parametrize("N", [140, 256, 400])
-def test_tail_over_workgroups_matches_one_workgroup(be, N, monkeypatch):
+def test_tail_over_workgroups_matches_one_workgroup(be, N, knobs):
     """The dense tail with one workgroup per tile column (tail_cyc_kernel, the
     default) applies every tile update of the factor in the single-workgroup
     kernel's order (tail_llt_kernel, M3S_TAIL_CYC=0); its back-substitution
@@ -394,13 +394,13 @@ def test_tail_over_workgroups_matches_one_workgroup(be, N, monkeypatch):
 
     g = synthetic.make_graph(N, 12, 16, seed=800 + N)
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
-    monkeypatch.setenv("M3S_TAIL_CYC", "0")
+    knobs("tail_cyc", "0")
     T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
     assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
     assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
     np.testing.assert_allclose(dx_a, dx_b, rtol=0, atol=1e-6 * np.abs(dx_b).max() + 1e-9)
     np.testing.assert_allclose(T_a, T_b, rtol=0, atol=1e-6)
-    monkeypatch.delenv("M3S_TAIL_CYC")  # and the default is bitwise reproducible run to run
+    knobs("tail_cyc", 1)  # and the default is bitwise reproducible run to run
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)

@@ -141,7 +141,7 @@ def test_host_tracker_mirror_raises_on_cholesky_failure(golden_dir):
 
 @pytest.mark.parametrize("calib", [False, True])
 @pytest.mark.parametrize("H,W", [(512, 512), (37, 53), (512, 1024)])
-def test_persistent_tracker_matches_launch_per_iteration(be, monkeypatch, calib, H, W):
+def test_persistent_tracker_matches_launch_per_iteration(be, knobs, calib, H, W):
     """The one-launch persistent tracker (every workgroup reduces all partials
     and runs the same 7x7 update) vs the launch-per-iteration path on the same
     pair: same iteration count, poses within the fp32 summation-order noise.
@@ -158,12 +158,12 @@ def test_persistent_tracker_matches_launch_per_iteration(be, monkeypatch, calib,
              T_WCk=p.T_WCk.data.numpy(), Qk=p.Qk.numpy(), valid=p.valid.numpy(), K=p.K.numpy(),
              H=H, W=W, max_iters=10)
     T_p, R_p, info_p = run_gpu(be, d, cfg=CFG, sync_every=0)
-    monkeypatch.setenv("M3S_TRACK_PERSISTENT", "0")
+    knobs("track_persistent", "0")
     T_l, R_l, info_l = run_gpu(be, d, cfg=CFG, sync_every=0)
     assert info_p[0] == info_l[0] == 10 and info_p[1] == info_l[1] == 0
     np.testing.assert_allclose(T_p[0], T_l[0], atol=2e-5)
     np.testing.assert_allclose(R_p[0], R_l[0], atol=2e-5)
     # deterministic: a second persistent run is bitwise identical
-    monkeypatch.setenv("M3S_TRACK_PERSISTENT", "1")
+    knobs("track_persistent", "1")
     T_p2, _, _ = run_gpu(be, d, cfg=CFG, sync_every=0)
     assert np.array_equal(T_p, T_p2)

@@ -198,8 +198,8 @@ def run_plan(p, Hjj, gj):
 @pytest.mark.parametrize("N,seed,split,tail", [(2, 0, 0, 8), (5, 1, 0, 8), (32, 2, 0, 8), (70, 3, 0, 8),
                                                (32, 4, 2, 8), (70, 5, 3, 8), (128, 6, 8, 8), (70, 3, 0, 0),
                                                (128, 6, 8, 0), (40, 7, 0, 3), (90, 8, 4, 4)])
-def test_plan_executes_to_dense_solution(be, N, seed, split, tail, monkeypatch):
-    monkeypatch.setenv("M3S_DENSE_TAIL_MIN", str(tail))
+def test_plan_executes_to_dense_solution(be, N, seed, split, tail, knobs):
+    knobs("dense_tail_min", str(tail))
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 2, 2, seed=seed, edge_range=(0, 0), kf_ids=np.arange(N) * 3 + 5)

@@ -6,6 +6,7 @@
 #include <climits>
 #include <cstdint>
 #include <queue>
+#include <thread>
 
 namespace m3s {
 
@@ -277,14 +278,26 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     if (a >= 0 && b >= 0 && a != b) adj.set(a, b), adj.set(b, a);
   }
   {  // the shallowest elimination tree among MD / MMD variants (fill breaks ties)
-    std::vector<int32_t> best = min_degree_order(m, adj, false, 0);
-    std::pair<int, int64_t> bs = etree_shape(m, adj, best);
-    for (int slack = 0; slack <= 1; slack++) {
-      std::vector<int32_t> o = min_degree_order(m, adj, true, slack);
-      const std::pair<int, int64_t> sh = etree_shape(m, adj, o);
-      if (sh.first < bs.first || (sh.first == bs.first && sh.second < bs.second)) best = o, bs = sh;
+    // The three candidates are independent: large graphs order them on three
+    // threads (the plan is on a cold call's critical path; same result).
+    std::vector<int32_t> o[3];
+    std::pair<int, int64_t> sh[3];
+    auto cand = [&](int c) {
+      o[c] = min_degree_order(m, adj, c > 0, c > 0 ? c - 1 : 0);
+      sh[c] = etree_shape(m, adj, o[c]);
+    };
+    if (m >= 96) {
+      std::thread t1(cand, 1), t2(cand, 2);
+      cand(0);
+      t1.join();
+      t2.join();
+    } else {
+      for (int c = 0; c < 3; c++) cand(c);
     }
-    P.perm = best;
+    int b = 0;
+    for (int c = 1; c < 3; c++)
+      if (sh[c].first < sh[b].first || (sh[c].first == sh[b].first && sh[c].second < sh[b].second)) b = c;
+    P.perm = std::move(o[b]);
   }
   P.iperm.assign(m, 0);
   for (int k = 0; k < m; k++) P.iperm[P.perm[k]] = k;
@@ -295,7 +308,7 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   std::vector<std::vector<int>> st(m);
   for (int k = 0; k < m; k++) Sb.for_each(k, [&](int i) { st[k].push_back(i); });
   // slots: diagonals 0..m-1, then off-diagonals column by column
-  std::vector<int> slot((size_t)m * m, -1);  // slot of (i, k), i > k
+  std::vector<int32_t> slot((size_t)m * m, -1);  // slot of (i, k), i > k
   int next = m;
   P.col_ptr.assign(1, 0);
   for (int k = 0; k < m; k++) {
@@ -322,10 +335,13 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     std::vector<int> fill(P.lev_ptr.begin(), P.lev_ptr.end() - 1);
     for (int k = 0; k < m; k++) P.lev_col[fill[lev[k]]++] = k;
   }
-  // row structure: rowst[k] = {p < k : k in struct(p)} (ascending)
+  // row structure: rowst[k] = {p < k : k in struct(p)} (ascending), also as
+  // bit rows R (R[k] has bit p): the update list of block (i, k) is
+  // rowst[k] & rowst[i], one word-wide AND per 64 columns
   std::vector<std::vector<int>> rowst(m);
+  BitRows R(m);
   for (int p = 0; p < m; p++)
-    for (int i : st[p]) rowst[i].push_back(p);
+    for (int i : st[p]) rowst[i].push_back(p), R.set(i, p);
   // dense tail: trailing columns whose structure is every later column
   int nc = 0;
   while (nc < m && (int)st[m - 1 - nc].size() == nc) nc++;
@@ -342,7 +358,6 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     P.dtr_ptr.push_back((int32_t)P.dtr_slot.size());
   }
   P.task_lev_ptr.assign(1, 0);
-  P.task_tr_ptr.assign(1, 0);
   P.ctask_ptr.assign(1, 0);
   std::vector<int32_t> ct0(nc, 0), bend((size_t)nc * nc, 0);
   for (int ci = 0; ci < nc; ci++) {  // DIAG border prefixes (dtr_p ascending)
@@ -351,33 +366,66 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     while (q < P.dtr_ptr[k + 1] && P.dtr_p[q] < c0) q++;
     bend[(size_t)ci * nc + ci] = q;
   }
+  // OFF tasks in level order and their update lists, written by index into
+  // arrays sized by a counting pass (push_back growth was most of this loop)
+  const uint64_t *Rw = R.w.data();
+  const int RW = R.words;
+  auto n_common = [&](int i, int k) {
+    int c = 0;
+    for (int q = 0; q < RW; q++) c += __builtin_popcountll(Rw[(size_t)k * RW + q] & Rw[(size_t)i * RW + q]);
+    return c;
+  };
+  size_t n_task = 0, n_tr = 0, n_it = 0;
+  for (int k = 0; k < m; k++) {
+    n_task += st[k].size();
+    if (k < c0) n_it += 1 + st[k].size();
+    for (int i : st[k]) n_tr += (size_t)n_common(i, k);
+  }
+  P.task_dst.resize(n_task);
+  P.task_col.resize(n_task);
+  P.task_tr_ptr.resize(n_task + 1);
+  P.tr_a.resize(n_tr);
+  P.tr_b.resize(n_tr);
+  P.items.resize(n_it);
+  P.ctask_ptr.resize((size_t)m + 1);
+  P.task_lev_ptr.resize((size_t)P.levels + 1);
+  int32_t *td = P.task_dst.data(), *tc = P.task_col.data(), *tp = P.task_tr_ptr.data(), *ta = P.tr_a.data(),
+          *tb = P.tr_b.data(), *itm = P.items.data();
+  size_t nt = 0, nr = 0, ni = 0, nct = 1;
+  tp[0] = 0;
   for (int l = 0; l < P.levels; l++) {
     for (int t = P.lev_ptr[l]; t < P.lev_ptr[l + 1]; t++) {
       const int k = P.lev_col[t];
-      P.ctask_ptr.push_back(P.ctask_ptr.back() + (int32_t)st[k].size());
+      P.ctask_ptr[nct] = P.ctask_ptr[nct - 1] + (int32_t)st[k].size();
+      nct++;
       if (k < c0) {  // dense-tail columns are not dataflow items
-        P.items.push_back(-1 - k);
-        for (size_t q = 0; q < st[k].size(); q++) P.items.push_back((int32_t)P.task_dst.size() + (int32_t)q);
+        itm[ni++] = -1 - k;
+        for (size_t q = 0; q < st[k].size(); q++) itm[ni++] = (int32_t)(nt + q);
       } else {
-        ct0[k - c0] = (int32_t)P.task_dst.size();
+        ct0[k - c0] = (int32_t)nt;
       }
+      const uint64_t *rk = Rw + (size_t)k * RW;
+      const int32_t *slk = slot.data() + (size_t)k * m;
       for (int i : st[k]) {
-        P.task_dst.push_back(sl(i, k));
-        P.task_col.push_back(k);
-        for (int p : rowst[k]) {
-          // i in struct(p)?  (struct lists are sorted)
-          if (Sb.test(p, i)) {
-            if (k >= c0 && p < c0) bend[(size_t)(k - c0) * nc + (i - c0)] = (int32_t)P.tr_a.size() + 1;
-            P.tr_a.push_back(sl(i, p));
-            P.tr_b.push_back(sl(k, p));
+        const int32_t *sli = slot.data() + (size_t)i * m;
+        td[nt] = sli[k];
+        tc[nt] = k;
+        // p < k with i and k both in struct(p), ascending
+        const uint64_t *ri_ = Rw + (size_t)i * RW;
+        int32_t *bd = k >= c0 ? &bend[(size_t)(k - c0) * nc + (i - c0)] : nullptr;
+        for (int q = 0; q < RW; q++)
+          for (uint64_t v = rk[q] & ri_[q]; v; v &= v - 1) {
+            const int p = q * 64 + __builtin_ctzll(v);
+            if (bd && p < c0) *bd = (int32_t)nr + 1;
+            ta[nr] = sli[p];
+            tb[nr] = slk[p];
+            nr++;
           }
-        }
-        if (k >= c0 && bend[(size_t)(k - c0) * nc + (i - c0)] == 0)  // no border updates
-          bend[(size_t)(k - c0) * nc + (i - c0)] = P.task_tr_ptr.back();
-        P.task_tr_ptr.push_back((int32_t)P.tr_a.size());
+        if (bd && *bd == 0) *bd = tp[nt];  // no border updates
+        tp[++nt] = (int32_t)nr;
       }
     }
-    P.task_lev_ptr.push_back((int32_t)P.task_dst.size());
+    P.task_lev_ptr[l + 1] = (int32_t)nt;
   }
   // column tasks: sparse columns in level order; first OFF task per column
   P.ctask0.assign(m, 0);
@@ -449,25 +497,35 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
     P.items.swap(items);
   }
   if (schedule) schedule_items(P);
-  // assembly lists (edge order => deterministic sums)
-  std::vector<std::vector<int32_t>> asl(P.S), gl(m);
-  for (int64_t e = 0; e < E; e++) {
+  // assembly lists (edge order => deterministic sums), by counting sort
+  P.asm_ptr.assign(P.S + 1, 0);
+  P.g_ptr.assign(m + 1, 0);
+  auto ends = [&](int64_t e, int &pa, int &pb) {
     const int a = ri[e] - 1, b = rj[e] - 1;
-    if (a == b) continue;  // Hs[0]+Hs[1]+Hs[2]+Hs[3] = 0 on the same pose
-    const int pa = a >= 0 ? P.iperm[a] : -1, pb = b >= 0 ? P.iperm[b] : -1;
-    if (pa >= 0) asl[pa].push_back((int32_t)e), gl[pa].push_back((int32_t)(e << 1));
-    if (pb >= 0) asl[pb].push_back((int32_t)e), gl[pb].push_back((int32_t)(e << 1 | 1));
-    if (pa >= 0 && pb >= 0) asl[sl(std::max(pa, pb), std::min(pa, pb))].push_back((int32_t)e);
+    pa = a >= 0 ? P.iperm[a] : -1, pb = b >= 0 ? P.iperm[b] : -1;
+    return a != b;  // Hs[0]+Hs[1]+Hs[2]+Hs[3] = 0 on the same pose
+  };
+  for (int64_t e = 0; e < E; e++) {
+    int pa, pb;
+    if (!ends(e, pa, pb)) continue;
+    if (pa >= 0) P.asm_ptr[pa + 1]++, P.g_ptr[pa + 1]++;
+    if (pb >= 0) P.asm_ptr[pb + 1]++, P.g_ptr[pb + 1]++;
+    if (pa >= 0 && pb >= 0) P.asm_ptr[sl(std::max(pa, pb), std::min(pa, pb)) + 1]++;
   }
-  P.asm_ptr.assign(1, 0);
-  for (int s = 0; s < P.S; s++) {
-    P.asm_edge.insert(P.asm_edge.end(), asl[s].begin(), asl[s].end());
-    P.asm_ptr.push_back((int32_t)P.asm_edge.size());
-  }
-  P.g_ptr.assign(1, 0);
-  for (int v = 0; v < m; v++) {
-    P.g_edge.insert(P.g_edge.end(), gl[v].begin(), gl[v].end());
-    P.g_ptr.push_back((int32_t)P.g_edge.size());
+  for (int q = 0; q < P.S; q++) P.asm_ptr[q + 1] += P.asm_ptr[q];
+  for (int q = 0; q < m; q++) P.g_ptr[q + 1] += P.g_ptr[q];
+  P.asm_edge.assign(P.asm_ptr[P.S], 0);
+  P.g_edge.assign(P.g_ptr[m], 0);
+  std::vector<int32_t> af(P.asm_ptr.begin(), P.asm_ptr.end() - 1), gf(P.g_ptr.begin(), P.g_ptr.end() - 1);
+  for (int64_t e = 0; e < E; e++) {
+    int pa, pb;
+    if (!ends(e, pa, pb)) continue;
+    if (pa >= 0) P.asm_edge[af[pa]++] = (int32_t)e, P.g_edge[gf[pa]++] = (int32_t)(e << 1);
+    if (pb >= 0) P.asm_edge[af[pb]++] = (int32_t)e, P.g_edge[gf[pb]++] = (int32_t)(e << 1 | 1);
+    if (pa >= 0 && pb >= 0) {
+      const int s2 = sl(std::max(pa, pb), std::min(pa, pb));
+      P.asm_edge[af[s2]++] = (int32_t)e;
+    }
   }
 }
 

@@ -173,16 +173,25 @@ def test_gn_singular_system_zero_dx(be):
     np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
 
 
-def test_gn_broken_plan_times_out_as_solve_failure(be, knobs):
+@pytest.mark.parametrize("N,tail", [(12, None), (140, 8)])
+def test_gn_broken_plan_times_out_as_solve_failure(be, knobs, N, tail):
     """A plan bug must end as a solve failure, never a hang (the LLT's flag
-    waits are bounded). the debug_drop_item knob removes the first item of the
+    waits are bounded). The debug_drop_item knob removes the first item of the
     dispatch list (a leaf DIAG): the items reading its blocks time out, the
-    iteration reports INFO_SOLVE_FAIL with dx = 0 and the poses untouched."""
+    iteration reports INFO_SOLVE_FAIL with dx = 0 and the poses untouched.
+    N = 12: the one-workgroup dataflow (sparse_llt_kernel; knob lvl = 0, the
+    level-synchronous kernel has no waits); N = 140 with a dense tail: the
+    chip-wide path (df_factor_kernel's epoch flags, tail_cyc_kernel's tagged
+    granules, col_backsub_kernel)."""
     import time
 
     from mast3r_slam_amd import synthetic
 
-    g = synthetic.make_graph(12, 24, 32, seed=37)
+    g = synthetic.make_graph(N, 12 if N > 64 else 24, 16 if N > 64 else 32, seed=37)
+    if tail is None:
+        knobs("lvl", 0)
+    else:
+        knobs("dense_tail_min", tail)
     knobs("debug_drop_item", "0")
     t0 = time.time()
     T_gpu, dx, info = run_gpu(be, "rays", g, 1, 0.0)
@@ -194,6 +203,36 @@ def test_gn_broken_plan_times_out_as_solve_failure(be, knobs):
     knobs("debug_drop_item", -1)
     T_ok, _, info = run_gpu(be, "rays", g, 1, 0.0)  # the same graph, intact plan
     assert info[be.INFO_SOLVE_FAIL] == 0 and not np.array_equal(T_ok, g.T_init.data.numpy())
+
+
+def test_workspace_reuse_across_solver_paths(be, knobs):
+    """One workspace for a chip-wide solve (global factor, dense tail: epoch
+    flags and tagged granules), then an LDS-resident solve, then the chip-wide
+    one again: flags, granules and tickets left by an earlier call must not be
+    taken for this call's; each dx equals a fresh-workspace run bitwise."""
+    from mast3r_slam_amd import synthetic
+
+    knobs("dense_tail_min", 8)
+    big = synthetic.make_graph(140, 12, 16, seed=61)
+    small = synthetic.make_graph(12, 12, 16, seed=62)
+
+    def call(g, ws):
+        Twc = g.T_init.data.clone().to(DEV).contiguous()
+        args = [t.to(DEV).contiguous() for t in (g.Xs, g.Cs, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q)]
+        a, keep = be.make_gn_args(be.MODE_RAYS, Twc, *args, sigma_a=0.003, sigma_b=10.0, C_thresh=0.0,
+                                  Q_thresh=1.5, max_iter=3, delta_thresh=0.0, workspace=ws)
+        (dx,) = be._run_gn("m3s_gauss_newton_rays", a, keep)
+        torch.cuda.synchronize()
+        return Twc.cpu().numpy(), dx.cpu().numpy(), keep["info"].cpu().numpy()
+
+    nbytes = max(be._lib.m3s_gn_workspace_size(g.Xs.shape[0], g.Xs.shape[1], g.n_edges) for g in (big, small))
+    ws = torch.zeros(nbytes, dtype=torch.uint8, device=DEV)
+    seq = [call(g, ws) for g in (big, small, big)]
+    for g, got in zip((big, small, big), seq):
+        ref = call(g, None)
+        assert got[2][be.INFO_SOLVE_FAIL] == 0 and got[2][be.INFO_ITERS] == 3
+        np.testing.assert_array_equal(got[1], ref[1])
+        np.testing.assert_array_equal(got[0], ref[0])
 
 
 def test_gn_bad_edge_ids_flagged(be):
@@ -404,3 +443,25 @@ def test_tail_over_workgroups_matches_one_workgroup(be, N, knobs):
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)
+
+
+@pytest.mark.parametrize("N,mode", [(3, "rays"), (6, "rays"), (12, "calib"), (32, "rays"), (32, "calib"),
+                                    (48, "rays")])
+def test_level_llt_matches_dataflow_llt_bitwise(be, N, mode, knobs):
+    """Small graphs: the level-synchronous LLT (sparse_lvl_kernel, the default
+    for LDS-resident plans without a dense tail) sums the same lists in the
+    same order as the item dataflow (sparse_llt_kernel<1>, knob lvl = 0):
+    poses, dx and info agree bitwise, natural termination included."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 24, 32, seed=900 + N)
+    Xs = constrained(g) if mode == "calib" else None
+    for iters, delta in ((4, 0.0), (20, 1e-4)):
+        T_a, dx_a, info_a = run_gpu(be, mode, g, iters, delta, Xs=Xs)
+        knobs("lvl", 0)
+        T_b, dx_b, info_b = run_gpu(be, mode, g, iters, delta, Xs=Xs)
+        knobs("lvl", 1)
+        np.testing.assert_array_equal(info_a, info_b)
+        assert info_a[be.INFO_SOLVE_FAIL] == 0
+        np.testing.assert_array_equal(dx_a, dx_b)
+        np.testing.assert_array_equal(T_a, T_b)

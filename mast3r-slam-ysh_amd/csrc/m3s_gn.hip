@@ -2607,6 +2607,98 @@ __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
   }
 }
 
+// Back-substitution of the sparse columns in ONE workgroup, level by level
+// from the top of the elimination tree (round 3; col_backsub_kernel spread it
+// over the chip as column tasks with epoch-flag hand-offs: ~1-3 us per level
+// of flag hops for ~0.2 us of arithmetic). x lives in LDS; each column's
+// L_ik blocks are fetched in staged batches (one memory latency per batch,
+// sub_matvec), the columns of a level run on the 16 waves side by side and
+// one workgroup barrier separates the levels. Same sums in the same order as
+// col_backsub_kernel: x_k = W_k^T (y_k - sum_i L_ik^T x_i). Then dx = -x,
+// the retraction and the ||dx|| test (col_finish).
+constexpr int kBsWaves = 16;
+__global__ void __launch_bounds__(64 * kBsWaves) bs_level_kernel(ColArgs C) {
+  if (C.flags[kFlagStop]) return;
+  extern __shared__ __attribute__((aligned(16))) double bsm[];
+  __shared__ float nrm[kBsWaves];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m = C.m;
+  double *y = bsm;                                               // [m][7]
+  double *stg = bsm + (size_t)m * 7 + (size_t)wave * kStageDoubles;  // per-wave stage areas
+  const int32_t *pl = C.plan;
+  const int32_t *perm = pl + C.off[0], *col_ptr = pl + C.off[1], *col_row = pl + C.off[2],
+                *col_slot = pl + C.off[3], *lev_ptr = pl + C.off[4], *lev_col = pl + C.off[5];
+  for (int idx = tid; idx < m * 7; idx += 64 * kBsWaves) y[idx] = C.y[idx];  // y; x of the dense tail
+  const bool failed =
+      __hip_atomic_load(C.flags + kFlagSplitFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  __syncthreads();
+  const int lane7 = lane < 7 ? lane : 0;
+  const int lane49 = lane < 49 ? lane : 0;
+  int nlev = 0;
+  while (nlev < m && lev_ptr[nlev] < m) nlev++;  // levels: lev_ptr[L] == m
+  for (int l = nlev - 1; l >= 0 && !failed; l--) {
+    const int cb = lev_ptr[l], nD = lev_ptr[l + 1] - cb;
+    for (int it = wave; it < nD; it += kBsWaves) {
+      const int k = lev_col[cb + it];
+      if (k >= C.c0) continue;  // dense tail: solved by the tail kernel
+      double wk[7];
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) wk[mm] = C.Dinv[(size_t)k * 49 + mm * 7 + lane7];
+      double rr = y[k * 7 + lane7];
+      rr = sub_matvec<true, true>(rr, C.L, col_slot, col_row, col_ptr[k], col_ptr[k + 1], y, lane7, lane49, lane,
+                                  stg);
+      double xk = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) xk += wk[mm] * readlane_d(rr, mm);
+      if (lane < 7) y[k * 7 + lane] = xk;
+    }
+    __syncthreads();
+  }
+  // dx = -x in the original order, retraction, ||dx|| (col_finish, all lanes)
+  if (failed) {
+    for (int k = tid; k < 7 * m; k += 64 * kBsWaves) C.dx_out[k] = 0.0f;
+    if (tid == 0) {
+      C.flags[kFlagSplitFail] = 0;
+      C.info[M3S_INFO_ITERS] += 1;
+      C.info[M3S_INFO_SOLVE_FAIL] += 1;
+      if (0.0f < C.delta_thresh) {
+        C.info[M3S_INFO_CONVERGED] = 1;
+        C.flags[kFlagStop] = 1;
+      }
+    }
+    return;
+  }
+  float *dxs = reinterpret_cast<float *>(stg - (size_t)wave * kStageDoubles);  // the stage areas, free now
+  float part = 0.0f;
+  for (int idx = tid; idx < 7 * m; idx += 64 * kBsWaves) {
+    const int vn = idx / 7, q = idx - 7 * vn;
+    const int vo = perm[vn];
+    const float v = -(float)y[idx];
+    C.dx_out[vo * 7 + q] = v;
+    dxs[vo * 7 + q] = v;
+    part += v * v;
+  }
+  part = wave_sum(part);
+  if (lane == 0) nrm[wave] = part;
+  __syncthreads();
+  for (int p = tid; p < m; p += 64 * kBsWaves) {
+    const Sim3f T = load_sim3(C.Twc + 8 * (size_t)(p + 1));
+    float xi[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
+    store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, T));
+  }
+  if (tid == 0) {
+    float s2 = 0.0f;
+    for (int w2 = 0; w2 < kBsWaves; w2++) s2 += nrm[w2];
+    C.info[M3S_INFO_ITERS] += 1;
+    if (sqrtf(s2) < C.delta_thresh) {
+      C.info[M3S_INFO_CONVERGED] = 1;
+      C.flags[kFlagStop] = 1;
+    }
+  }
+}
+
 // ------------------------------------------- dense tail on the f64 MFMA --
 // The top clique of the elimination tree (nc block columns, n = 7 nc scalar
 // columns; SparsePlan::nc) after its border updates is a dense SPD system:
@@ -3545,6 +3637,7 @@ struct Knobs {
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel (A/B)
   std::atomic<int> track_persistent{1};  // M3S_TRACK_PERSISTENT: 0 = one tracker launch per iteration
   std::atomic<int> lvl{1};             // M3S_LVL: 0 = small graphs on sparse_llt_kernel's dataflow (A/B)
+  std::atomic<int> bs_lvl{1};          // M3S_BS_LVL: 0 = column-task back-substitution over the chip (A/B)
   std::atomic<int> debug_drop_item{-1};  // test hook only (m3s_set_knob): drop one LLT dispatch item
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -3560,6 +3653,7 @@ struct Knobs {
     env("M3S_BORDER_SPLIT", border_split);
     env("M3S_TRACK_PERSISTENT", track_persistent);
     env("M3S_LVL", lvl);
+    env("M3S_BS_LVL", bs_lvl);
   }
 };
 Knobs &knobs() {
@@ -3713,6 +3807,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;
 int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st);
+void set_lds_attributes_once();
 
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
@@ -3867,8 +3962,14 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
         }
       }
-      const int g4 = std::max(1, std::min(C.ncols, 256));
-      col_backsub_kernel<<<g4, 64, 0, st>>>(C);
+      const size_t bs_lds = sizeof(double) * ((size_t)meta.m * 7 + (size_t)kBsWaves * kStageDoubles);
+      if (knobs().bs_lvl != 0 && bs_lds <= kMaxLdsBytes) {
+        set_lds_attributes_once();
+        bs_level_kernel<<<1, 64 * kBsWaves, bs_lds, st>>>(C);
+      } else {
+        const int g4 = std::max(1, std::min(C.ncols, 256));
+        col_backsub_kernel<<<g4, 64, 0, st>>>(C);
+      }
     } else if (meta.store == 1 && meta.nc == 0 && meta.n_parts == 0 && knobs().lvl != 0)
       sparse_lvl_kernel<<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.store == 1)
@@ -3987,6 +4088,8 @@ void set_lds_attributes_once() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_lvl_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bs_level_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
   });
 }
@@ -4940,7 +5043,7 @@ int m3s_set_knob(const char *name, int value) {
     std::atomic<int> *v;
   } tab[] = {{"plan_cache", &k.plan_cache}, {"dense", &k.dense}, {"dense_tail_min", &k.dense_tail_min},
              {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc}, {"tail_mfma", &k.tail_mfma},
-             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent}, {"lvl", &k.lvl},
+             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent}, {"lvl", &k.lvl}, {"bs_lvl", &k.bs_lvl},
              {"debug_drop_item", &k.debug_drop_item}};
   for (const auto &t : tab)
     if (std::strcmp(t.n, name) == 0) {

@@ -465,3 +465,22 @@ def test_level_llt_matches_dataflow_llt_bitwise(be, N, mode, knobs):
         assert info_a[be.INFO_SOLVE_FAIL] == 0
         np.testing.assert_array_equal(dx_a, dx_b)
         np.testing.assert_array_equal(T_a, T_b)
+
+
+@pytest.mark.parametrize("N,tail", [(90, 0), (140, 8), (256, 16)])
+def test_level_backsub_matches_column_tasks_bitwise(be, N, tail, knobs):
+    """Chip-wide path: the sparse back-substitution in one workgroup by levels
+    (bs_level_kernel, the default) sums every column's terms in the order of
+    the column-task kernel over the chip (col_backsub_kernel, knob bs_lvl = 0):
+    dx and poses agree bitwise; no failures. (With and without a dense tail.)"""
+    from mast3r_slam_amd import synthetic
+
+    knobs("dense_tail_min", tail)
+    g = synthetic.make_graph(N, 12, 16, seed=950 + N)
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    knobs("bs_lvl", 0)
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
+    np.testing.assert_array_equal(dx_a, dx_b)
+    np.testing.assert_array_equal(T_a, T_b)

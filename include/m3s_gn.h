@@ -112,10 +112,11 @@ int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end,
                      double *edge_sums, void *stream);
 int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream);
 /* m3s_gn_release:   drop the host-side state m3s_gn_prepare keyed by
- *                   a->workspace (synchronises `stream` first: the state owns
- *                   the host buffers of queued uploads). Call it before the
- *                   workspace is freed or reused for another problem; the
- *                   gauss_newton_* wrappers of mast3r_slam_backends do. */
+ *                   a->workspace (no synchronisation: queued uploads read the
+ *                   library's pinned staging, never this state). Call it
+ *                   before the workspace is freed or reused for another
+ *                   problem; the gauss_newton_* wrappers of mast3r_slam_backends
+ *                   do. */
 int m3s_gn_release(const m3s_gn_args *a, void *stream);
 #define M3S_EDGE_SUM_STRIDE 36
 

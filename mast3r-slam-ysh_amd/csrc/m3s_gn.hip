@@ -3685,7 +3685,6 @@ struct PlanMeta {
   int32_t h_flags[64] = {0};
   int64_t n_blocks_full = 0;       // task-table length of the full edge range
   std::vector<int32_t> tasks_r;    // task table of a sharded rank's edge range
-  std::vector<std::vector<int32_t>> tasks_old;  // earlier tables (uploads may be queued)
   bool has_K = false;
   float K4[4] = {0.f, 0.f, 0.f, 0.f};  // fx, fy, cx, cy (calib; read once per call)
   int64_t range_b = -1, range_e = -1, n_blocks = 0;
@@ -3712,6 +3711,40 @@ PlanMeta solve_view(const PlanMeta &M) {
 }
 std::mutex g_reg_mu;
 std::unordered_map<const void *, PlanMeta> g_reg;
+
+// Pinned host staging of the per-call transfers (gn_prepare_impl: the D2H
+// reads of K, ii, jj and ONE H2D upload of flags | ranks | task table | plan;
+// finish_plan: a deferred plan; gn_linearize_impl: a sharded rank's task
+// table). Pageable copies were one staged, host-synchronous transfer each
+// (~7 per call); an event per buffer guards it until the copy that reads it
+// has left. The registry entries own no memory a queued copy still reads.
+struct Staging {
+  char *down = nullptr, *up = nullptr, *plan_up = nullptr, *tasks_up = nullptr;
+  size_t down_cap = 0, up_cap = 0, plan_cap = 0, tasks_cap = 0;
+  hipEvent_t ev = nullptr, plan_ev = nullptr, tasks_ev = nullptr;
+  bool pending = false, plan_pending = false, tasks_pending = false;
+};
+// One staging set per device: an event recorded on one device's stream cannot
+// guard another device's copies (a process may drive GN on several GPUs).
+std::mutex g_stage_mu;
+std::unordered_map<int, Staging> g_stages;
+bool pinned_reserve(char *&p, size_t &cap, size_t need) {
+  if (need <= cap) return true;
+  if (p) (void)hipHostFree(p);
+  p = nullptr, cap = 0;
+  const size_t n = std::max<size_t>(need + need / 2, 1 << 16);
+  if (hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault) != hipSuccess) return false;
+  cap = n;
+  return true;
+}
+Staging *stage_for_device() {  // caller holds g_stage_mu
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  Staging &S = g_stages[dev];
+  for (hipEvent_t *e : {&S.ev, &S.plan_ev, &S.tasks_ev})
+    if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return &S;
+}
 
 // Task table: the E_loc x chunks (edge, chunk) tasks sorted by (chunk, KF j),
 // cut into 8 contiguous runs, run x dealt to blocks x, x+8, x+16, ... so the
@@ -3772,6 +3805,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   int64_t blocks = E_loc * L.chunks;
   int pack = 0;
   {
+    std::lock_guard<std::mutex> stage_lock(g_stage_mu);  // (lock order: staging, then registry)
     std::lock_guard<std::mutex> g(g_reg_mu);
     auto it = g_reg.find(ws);
     if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
@@ -3780,13 +3814,22 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
       M.range_b = eb, M.range_e = ee, M.planes_ok = false;
       M.n_blocks = 0;
       if ((int64_t)M.rj.size() >= ee) {
-        // fresh host buffer: an earlier upload from tasks_r may still be queued
-        if (!M.tasks_r.empty()) M.tasks_old.push_back(std::move(M.tasks_r));  // freed at the next prepare
         M.tasks_r.clear();
         build_tasks(M.rj, eb, E_loc, L.chunks, M.tasks_r);
-        if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), M.tasks_r.data(), sizeof(int32_t) * M.tasks_r.size(),
-                           hipMemcpyHostToDevice, st) != hipSuccess)
+        // uploaded from pinned staging guarded by an event, so the registry
+        // entry owns no host memory a queued copy still reads (m3s_gn_release
+        // need not synchronise)
+        Staging *SG = stage_for_device();
+        const size_t nb = sizeof(int32_t) * M.tasks_r.size();
+        if (!SG) return M3S_ELAUNCH;
+        if (SG->tasks_pending && hipEventSynchronize(SG->tasks_ev) != hipSuccess) return M3S_ELAUNCH;
+        SG->tasks_pending = false;
+        if (!pinned_reserve(SG->tasks_up, SG->tasks_cap, nb)) return M3S_ELAUNCH;
+        memcpy(SG->tasks_up, M.tasks_r.data(), nb);
+        if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), SG->tasks_up, nb, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(SG->tasks_ev, st) != hipSuccess)
           return M3S_ELAUNCH;
+        SG->tasks_pending = true;
         M.n_blocks = (int64_t)M.tasks_r.size();
       }
     }
@@ -4169,41 +4212,8 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
 }
 
 // Per solve call: read ii/jj (+ K) once — the call's only host sync — rank
-// the ids, fetch or build the plan, and enqueue its upload. The host buffers
-// of every upload live in the workspace's registry entry until the next
-// prepare on that workspace (which syncs first), so nothing waits here.
-// Pinned host staging for the per-call transfers of gn_prepare_impl: the D2H
-// reads (K, ii, jj) and ONE H2D upload of flags | ranks | task table | plan
-// (contiguous in the workspace). Pageable copies were one staged,
-// host-synchronous transfer each (~7 per call); the event guards the upload
-// buffer until the previous call's copy has left it.
-struct Staging {
-  char *down = nullptr, *up = nullptr, *plan_up = nullptr;
-  size_t down_cap = 0, up_cap = 0, plan_cap = 0;
-  hipEvent_t ev = nullptr, plan_ev = nullptr;
-  bool pending = false, plan_pending = false;
-};
-// One staging set per device: an event recorded on one device's stream cannot
-// guard another device's copies (a process may drive GN on several GPUs).
-std::mutex g_stage_mu;
-std::unordered_map<int, Staging> g_stages;
-bool pinned_reserve(char *&p, size_t &cap, size_t need) {
-  if (need <= cap) return true;
-  if (p) (void)hipHostFree(p);
-  p = nullptr, cap = 0;
-  const size_t n = std::max<size_t>(need + need / 2, 1 << 16);
-  if (hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault) != hipSuccess) return false;
-  cap = n;
-  return true;
-}
-Staging *stage_for_device() {  // caller holds g_stage_mu
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  Staging &S = g_stages[dev];
-  if (!S.ev && hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess) return nullptr;
-  if (!S.plan_ev && hipEventCreateWithFlags(&S.plan_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
-  return &S;
-}
+// the ids, fetch the plan (or defer it to the first solve) and enqueue ONE
+// upload of everything the launches read (pinned staging, above).
 
 // The per-call flag state the solve kernels of a plan rely on: the column-
 // task / dataflow / dense-tail epoch flags live only on the global-factor
@@ -4388,7 +4398,6 @@ int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st) {
     C.tail_min = dense_tail_min();
     C.meta = M;
     C.meta.tasks_r.clear();
-    C.meta.tasks_old.clear();
     std::lock_guard<std::mutex> gc(g_cache_mu);
     g_cache.insert(g_cache.begin(), std::move(C));
     if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
@@ -4972,8 +4981,7 @@ int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
 
 int m3s_gn_release(const m3s_gn_args *a, void *stream) {
   if (!a || !a->workspace) return M3S_EINVAL;
-  // the entry owns the host buffers of uploads that may still be queued
-  if (hipStreamSynchronize(S(stream)) != hipSuccess) return M3S_ELAUNCH;
+  (void)stream;  // no sync: every queued upload reads pinned staging, not the entry
   std::lock_guard<std::mutex> g(g_reg_mu);
   g_reg.erase(a->workspace);
   return M3S_OK;

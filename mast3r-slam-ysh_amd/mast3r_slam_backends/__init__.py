@@ -392,8 +392,8 @@ def _run_gn(fn_name, a, keep):
     st = _stream(keep["Xs"].device)
     rc = getattr(_lib, fn_name)(ctypes.byref(a), st)
     # the per-call workspace goes back to the caching allocator: drop its host
-    # state too (m3s_gn_release; one stream sync, the call's result is needed
-    # by the caller anyway — the reference syncs every iteration)
+    # state too (m3s_gn_release: no stream sync; the call returns as soon as
+    # its launches are queued)
     rc_rel = _lib.m3s_gn_release(ctypes.byref(a), st)
     _raise(rc, fn_name)
     _raise(rc_rel, "m3s_gn_release")

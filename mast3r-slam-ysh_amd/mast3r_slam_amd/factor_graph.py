@@ -12,9 +12,11 @@ pixel) and stacks the keyframe pointmaps (`get_poses_points`, :112-119). Here:
   int32 (a pixel index of one keyframe, < 2^31): the GN's first iteration
   reads 9 B of edge data per pixel instead of 13 (m3s_gn_args.idx_i32);
 * ``KeyframeStore`` holds X_canon / C / N / T_WC in [capacity, ...] buffers
-  like SharedKeyframes (frame.py:220-247); when the graph's keyframes are a
-  contiguous id range (the usual case) the solve passes views and the GN
-  updates the stored poses in place.
+  like SharedKeyframes (frame.py:220-247), plus C / N and (calib) the
+  ray-constrained pointmaps, kept current on every write; when the graph's
+  keyframes are a contiguous id range (the usual case) the solve passes views
+  — no per-solve copy of pointmaps or confidences — and the GN updates the
+  stored poses in place.
 
 The per-edge order differs from the reference's (interleaved instead of all
 forward then all reverse); the normal equations are order-independent up to
@@ -80,36 +82,62 @@ class EdgeStore:
 
 
 class KeyframeStore:
-    """X_canon [cap,HW,3], C [cap,HW,1], N [cap], T_WC [cap,8] (SharedKeyframes layout)."""
+    """X_canon [cap,HW,3], C [cap,HW,1], N [cap], T_WC [cap,8] (SharedKeyframes
+    layout), plus what the GN reads, kept current on every write so a solve
+    passes views instead of building them:
 
-    def __init__(self, H: int, W: int, device, capacity: int = 512):
+    * ``Cn`` [cap,HW,1] = C / N, the average confidence the reference forms per
+      solve (``get_average_conf``, frame.py:107-108; global_opt.py:114-117);
+    * ``Xr`` [cap,HW,3] (when the store has intrinsics K): X_canon constrained to
+      the pixel rays, z * [(u-cx)/fx, (v-cy)/fy, 1], which solve_GN_calib forms
+      per solve (constrain_points_to_ray, global_opt.py:172)."""
+
+    def __init__(self, H: int, W: int, device, capacity: int = 512, K=None):
         self.H, self.W, self.device, self.n = H, W, device, 0
         HW = H * W
         self.X = torch.zeros(capacity, HW, 3, device=device)
         self.C = torch.zeros(capacity, HW, 1, device=device)
         self.N = torch.zeros(capacity, dtype=torch.int32, device=device)
         self.T_WC = torch.zeros(capacity, 8, device=device)
+        self.Cn = torch.zeros(capacity, HW, 1, device=device)
+        self.K = None if K is None else torch.as_tensor(K, dtype=torch.float32, device=device)
+        self.Xr = torch.zeros(capacity, HW, 3, device=device) if K is not None else None
+        if K is not None:
+            self._rays = _pixel_rays(H, W, self.K)
 
     def append(self, X, C, T_WC, N=1):
         k = self.n
+        self.n += 1
+        self.T_WC[k].copy_(T_WC.reshape(8))
+        self.set_pointmap(k, X, C, N)
+        return k
+
+    def set_pointmap(self, k, X, C, N):
+        """Keyframe k's canonical pointmap, accumulated confidence and update
+        count (after Frame.update_pointmap, frame.py:41-105), with the derived
+        Cn / Xr rows."""
         self.X[k].copy_(X.reshape(-1, 3))
         self.C[k].copy_(C.reshape(-1, 1))
-        self.N[k] = N
-        self.T_WC[k].copy_(T_WC.reshape(8))
-        self.n += 1
-        return k
+        self.N[k] = int(N)
+        torch.div(self.C[k], float(N), out=self.Cn[k])
+        if self.Xr is not None:
+            torch.mul(self.X[k][:, 2:3], self._rays, out=self.Xr[k])
 
     def update_T_WCs(self, T_WCs, idx):  # frame.py:309-311
         self.T_WC[idx] = T_WCs
 
 
-def _ray_constrained(Xs, K, H, W):
-    """constrain_points_to_ray (geometry.py:37-42): X <- z * [(u-cx)/fx, (v-cy)/fy, 1]."""
-    v, u = torch.meshgrid(torch.arange(H, device=Xs.device, dtype=Xs.dtype),
-                          torch.arange(W, device=Xs.device, dtype=Xs.dtype), indexing="ij")
-    d = torch.stack(((u.reshape(-1) - K[0, 2]) / K[0, 0], (v.reshape(-1) - K[1, 2]) / K[1, 1],
-                     torch.ones(H * W, device=Xs.device, dtype=Xs.dtype)), -1)
-    return (Xs[..., 2:3] * d).contiguous()
+def _pixel_rays(H, W, K):
+    """[(u-cx)/fx, (v-cy)/fy, 1] of the row-major pixel grid, [H*W, 3]."""
+    v, u = torch.meshgrid(torch.arange(H, device=K.device, dtype=torch.float32),
+                          torch.arange(W, device=K.device, dtype=torch.float32), indexing="ij")
+    return torch.stack(((u.reshape(-1) - K[0, 2]) / K[0, 0], (v.reshape(-1) - K[1, 2]) / K[1, 1],
+                        torch.ones(H * W, device=K.device)), -1)
+
+
+def ray_constrained(Xs, K, H, W):
+    """constrain_points_to_ray (geometry.py:37-42) of [n, HW, 3] pointmaps."""
+    return (Xs[..., 2:3] * _pixel_rays(H, W, torch.as_tensor(K, device=Xs.device))).contiguous()
 
 
 class FactorGraph:
@@ -146,25 +174,26 @@ class FactorGraph:
     def get_unique_kf_idx(self):
         return torch.unique(torch.cat([self.ii_u, self.jj_u]), sorted=True)
 
-    def _poses_points(self, uk):
-        """Views when the keyframes are ids [a, a+n); gathers otherwise."""
+    def _poses_points(self, uk, calib):
+        """Views when the keyframes are ids [a, a+n) (no copy); gathers
+        otherwise. Xs is the ray-constrained store for calib."""
         n = uk.numel()
         a = int(uk[0])
         F = self.frames
+        X = F.Xr if calib else F.X
         contiguous = int(uk[-1]) - a + 1 == n
         if contiguous:
-            Xs, Cs_acc, N, T = F.X[a:a + n], F.C[a:a + n], F.N[a:a + n], F.T_WC[a:a + n]
-        else:
-            Xs, Cs_acc, N, T = F.X[uk], F.C[uk], F.N[uk], F.T_WC[uk].contiguous()
-        Cs = (Cs_acc / N.view(-1, 1, 1).float()).contiguous()
-        return Xs, Cs, T, contiguous
+            return X[a:a + n], F.Cn[a:a + n], F.T_WC[a:a + n], contiguous
+        return X[uk], F.Cn[uk], F.T_WC[uk].contiguous(), contiguous
 
     def _solve(self, calib):
         pin = self.cfg["pin"]
         uk = self.get_unique_kf_idx()
         if uk.numel() <= pin:
             return
-        Xs, Cs, T, contiguous = self._poses_points(uk)
+        if calib and self.frames.Xr is None:
+            raise RuntimeError("solve_GN_calib needs a KeyframeStore built with K")
+        Xs, Cs, T, contiguous = self._poses_points(uk, calib)
         # the reference GN holds rank 0 fixed and writes back poses [pin:]
         # (global_opt.py:158); in place, poses 1..pin-1 are restored after
         held = T[1:pin].clone() if contiguous and pin > 1 else None
@@ -172,7 +201,7 @@ class FactorGraph:
         c = self.cfg
         if calib:
             H, W = self.frames.H, self.frames.W
-            be.gauss_newton_calib(T, _ray_constrained(Xs, self.K, H, W), Cs, self.K, ii, jj, idx, valid, Q,
+            be.gauss_newton_calib(T, Xs, Cs, self.K, ii, jj, idx, valid, Q,
                                   H, W, c["pixel_border"], c["depth_eps"], c["sigma_pixel"],
                                   c["sigma_depth"], c["C_conf"], c["Q_conf"], c["max_iters"],
                                   c["delta_norm"])

@@ -58,6 +58,32 @@ def test_add_factors_filter():
     assert fg.get_unique_kf_idx().tolist() == [0, 1, 2, 3]
 
 
+def test_keyframe_store_keeps_gn_inputs_current():
+    """Cn = C / N and Xr = constrain_points_to_ray(X) are kept on every write
+    (append, set_pointmap after a fusion), and a solve over contiguous
+    keyframes gets views of them: no per-solve copy (SURVEY.md §8f #3)."""
+    from oracle.tracker_oracle import constrain_points_to_ray
+
+    H, W = 6, 8
+    g = synthetic.make_graph(5, H, W, seed=3)
+    kf = fgm.KeyframeStore(H, W, "cpu", capacity=8, K=g.K)
+    for k in range(5):
+        kf.append(g.Xs[k], g.Cs[k] * 3.0, g.T_init.data[k], N=3)
+    kf.set_pointmap(2, g.Xs[2] * 1.5, g.Cs[2] * 4.0, 4)
+    for k in range(5):
+        scale = 1.5 if k == 2 else 1.0
+        np.testing.assert_allclose(kf.Cn[k].numpy(), g.Cs[k].numpy(), rtol=1e-6)
+        ref = constrain_points_to_ray((H, W), (g.Xs[k] * scale).numpy(), g.K.numpy())
+        np.testing.assert_allclose(kf.Xr[k].numpy(), ref, rtol=1e-6, atol=1e-7)
+    fg = fgm.FactorGraph(kf, K=g.K)
+    uk = torch.arange(1, 4)
+    for calib in (False, True):
+        Xs, Cs, T, contiguous = fg._poses_points(uk, calib)
+        assert contiguous
+        assert Xs.data_ptr() == (kf.Xr if calib else kf.X)[1].data_ptr() and Cs.data_ptr() == kf.Cn[1].data_ptr()
+        assert T.data_ptr() == kf.T_WC[1].data_ptr()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("calib", [False, True])
 def test_solve_matches_dropin_on_reference_layout(calib):
@@ -66,7 +92,7 @@ def test_solve_matches_dropin_on_reference_layout(calib):
     dev = torch.device("cuda:0")
     N, H, W = 7, 24, 32
     g = synthetic.make_graph(N, H, W, seed=11, device=dev)
-    kf = fgm.KeyframeStore(H, W, dev, capacity=16)
+    kf = fgm.KeyframeStore(H, W, dev, capacity=16, K=g.K)
     for k in range(N):
         kf.append(g.Xs[k], g.Cs[k], g.T_init.data[k])
     fg = fgm.FactorGraph(kf, K=g.K)
@@ -76,7 +102,7 @@ def test_solve_matches_dropin_on_reference_layout(calib):
     c = fgm.LOCAL_OPT_CFG
     T = g.T_init.data.clone().contiguous()
     if calib:
-        Xs = fgm._ray_constrained(g.Xs, g.K, H, W)
+        Xs = fgm.ray_constrained(g.Xs, g.K, H, W)
         be.gauss_newton_calib(T, Xs, g.Cs, g.K, g.ii, g.jj, g.idx_ii2jj, g.valid_match, g.Q, H, W,
                               c["pixel_border"], c["depth_eps"], c["sigma_pixel"], c["sigma_depth"],
                               c["C_conf"], c["Q_conf"], c["max_iters"], c["delta_norm"])
@@ -102,7 +128,7 @@ def test_solve_matches_oracle_on_reference_edge_order(calib):
     dev = torch.device("cuda:0")
     N, H, W = 7, 24, 32
     g = synthetic.make_graph(N, H, W, seed=13)
-    kf = fgm.KeyframeStore(H, W, dev, capacity=16)
+    kf = fgm.KeyframeStore(H, W, dev, capacity=16, K=g.K.to(dev))
     for k in range(N):
         kf.append(g.Xs[k].to(dev), g.Cs[k].to(dev), g.T_init.data[k].to(dev))
     fg = fgm.FactorGraph(kf, K=g.K.to(dev))

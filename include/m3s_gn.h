@@ -195,9 +195,9 @@ int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n
 /* Solver knobs (experiments / A/B tests). Defaults are the measured best;
  * the environment (M3S_PLAN_CACHE, M3S_DENSE, M3S_DENSE_TAIL_MIN, M3S_COLS,
  * M3S_DF, M3S_TAIL_CYC, M3S_TAIL_MFMA, M3S_BORDER_SPLIT,
- * M3S_TRACK_PERSISTENT, M3S_LVL, M3S_BS_LVL) is read once per process; this sets a knob at run
+ * M3S_TRACK_PERSISTENT) is read once per process; this sets a knob at run
  * time for the calls that follow. Names: plan_cache, dense, dense_tail_min,
- * cols, df, tail_cyc, tail_mfma, border_split, track_persistent, lvl, bs_lvl,
+ * cols, df, tail_cyc, tail_mfma, border_split, track_persistent,
  * debug_drop_item (test hook: drop one dispatch item of the one-workgroup
  * LLT so its bounded waits time out). Returns the previous value, or
  * -2^30 for an unknown name. */

@@ -1536,58 +1536,46 @@ __device__ __forceinline__ void diag_updates_sc1(double &v, double &bb, const do
 template <bool SC1 = false>
 __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double *Di, double *scr, int lane,
                                             int l7, double (&wcol)[7], double *Wl = nullptr) {
-  (void)l7;
-  // Every lane factors the whole block in its own registers (round 3): the
-  // 28 lower entries arrive by one LDS broadcast, and the pivot chain has no
-  // cross-lane step at all (the by-rows form paid an LDS round trip and two
-  // readlanes per pivot). Lane c < 7 then solves L w = e_c for column c of
-  // W. The operations and their order are those of the by-rows form: L_ij =
-  // (a_ij - L_i0 L_j0 - L_i1 L_j1 - ...) / L_jj, 1/L_jj by rsqrt + 2 Newton
-  // steps, w_q = (e_c[q] - L_q0 w_0 - ...) / L_qq: bitwise the same factor.
+  // entry layout -> row layout through the wave's scratch
   if (lane < 49) scr[lane] = v;
   wave_lds_fence();
-  double L[7][7];
+  double a[7];
 #pragma unroll
-  for (int i = 0; i < 7; i++)
-#pragma unroll
-    for (int j = 0; j <= i; j++) L[i][j] = scr[7 * i + j];
+  for (int qq = 0; qq < 7; qq++) a[qq] = scr[l7 + qq];
   wave_lds_fence();
+  // One pass: right-looking Cholesky by rows (lane r holds row r) and, with
+  // the same column of L (broadcast through the scratch), W = L^-1 by
+  // columns (lane c holds column c): at step j, W[j][c] = s_j / L_jj is
+  // final and s_r (r > j) loses L[r][j] W[j][c]. Column j is scaled on every
+  // lane (lane j holds the pivot itself; the lanes above keep finite upper-
+  // triangle values that are masked when L_kk is stored). No per-pair
+  // readlanes, no second serial chain for W.
+  double sw[7];
+#pragma unroll
+  for (int r = 0; r < 7; r++) sw[r] = (r == lane) ? 1.0 : 0.0;
   bool bad = false;
-  double inv[7];
 #pragma unroll
   for (int j = 0; j < 7; j++) {
-    double d = L[j][j];
-#pragma unroll
-    for (int p = 0; p < j; p++) d -= L[j][p] * L[j][p];
+    const double d = readlane_d(a[j], j);
     bad |= !(d > 0.0);
-    inv[j] = rsqrt_nr(d);
-    if (lane == 0) scr[8 * j] = d * inv[j];  // L_jj: output only (the W solve uses inv)
+    const double inv = rsqrt_nr(d);
+    a[j] *= inv;
+    wcol[j] = sw[j] * inv;
+    if (lane < 7) scr[lane] = a[j];
+    wave_lds_fence();
 #pragma unroll
-    for (int i = j + 1; i < 7; i++) {
-      double a = L[i][j];
-#pragma unroll
-      for (int p = 0; p < j; p++) a -= L[i][p] * L[j][p];
-      L[i][j] = a * inv[j];
-      if (lane == 0) scr[7 * i + j] = L[i][j];
+    for (int cc = j + 1; cc < 7; cc++) {
+      const double lcj = scr[cc];
+      a[cc] -= a[j] * lcj;
+      sw[cc] -= lcj * wcol[j];
     }
+    wave_lds_fence();
   }
-  // column `lane` of W = L^-1 (lanes >= 7: e_c = 0, discarded)
-#pragma unroll
-  for (int q = 0; q < 7; q++) {
-    double sv = (q == lane) ? 1.0 : 0.0;
-#pragma unroll
-    for (int j = 0; j < q; j++) sv -= L[q][j] * wcol[j];
-    wcol[q] = sv * inv[q];
-  }
-  // L_kk (row-major, upper part 0) from the scratch, entry layout
-  wave_lds_fence();
-  const int r = lane / 7, c = lane - 7 * (lane / 7);
-  if (lane < 49) st_blk<SC1>(Lb + (size_t)k * 49 + lane, c <= r ? scr[lane] : 0.0);
-  wave_lds_fence();
   if (lane < 7) {
 #pragma unroll
     for (int qq = 0; qq < 7; qq++) {
-      st_blk<SC1>(Di + (size_t)k * 49 + qq * 7 + lane, wcol[qq]);  // column `lane` of W
+      st_blk<SC1>(Lb + (size_t)k * 49 + lane * 7 + qq, (qq <= lane) ? a[qq] : 0.0);  // row `lane` of L_kk
+      st_blk<SC1>(Di + (size_t)k * 49 + qq * 7 + lane, wcol[qq]);                    // column `lane` of W
       if (Wl) Wl[qq * 7 + lane] = wcol[qq];
     }
   }
@@ -2064,172 +2052,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
 }
 
-// ------------------------------------------- level-synchronous small LLT --
-// Small graphs (plan, factor, W and y resident in LDS; no dense tail): the
-// block LLT by elimination-tree levels, bulk-synchronous, instead of
-// sparse_llt_kernel's item dataflow. At 32 KFs most of the dataflow's
-// critical path was flag hops and wave switches between items
-// (profiles/r01/llt_items_v4.txt: 48% of the factor span), not arithmetic.
-// Per level l (leaves first):
-//   A  DIAG(k), k in level l: D_k - sum_p L_kp L_kp^T -> L_kk, W_k = L_kk^-1,
-//      y_k = W_k (b_k - sum_p L_kp y_p); and the update sums of the level's
-//      OFF blocks, A_ik - sum_p L_ip L_kp^T, stored in place (their inputs are
-//      columns p below level l: final);
-//   B  L_ik = A'_ik W_k^T for the level's OFF blocks;
-// one workgroup barrier after each phase. Back-substitution by levels from the
-// top: x_k = W_k^T (y_k - sum_i L_ik^T x_i) (i in struct(k): higher levels).
-// Every sum runs over the same lists in the same order as sparse_llt_kernel
-// (same products, same subtraction order): bitwise the same solve.
-// (SimplicialLLT factor + solve, gn_kernels.cu:132-153; dx = 0 on failure,
-// pose_retr_kernel :415-453, ||dx|| < delta :1219-1222.)
-__global__ void __launch_bounds__(1024) sparse_lvl_kernel(SparseDev D) {
-  if (D.flags[kFlagStop]) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int fail_s;
-  __shared__ float nrm[16];
-  __shared__ double scratch[16][64];
-  const int m = D.m, S = D.S;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  constexpr int NW = 16;
-  double *Lb = smem;
-  double *Di = smem + (size_t)S * 49;
-  double *y = smem + (size_t)(S + m) * 49;
-  int32_t *after_y = reinterpret_cast<int32_t *>(y + (size_t)m * 7);
-  for (int q = tid; q < D.plan_len; q += 1024) after_y[q] = D.plan[q];
-  const int32_t *pl = after_y;
-  const int32_t *perm = pl + D.off[0], *col_ptr = pl + D.off[1], *col_row = pl + D.off[2],
-                *col_slot = pl + D.off[3], *lev_ptr = pl + D.off[4], *lev_col = pl + D.off[5],
-                *dtr_ptr = pl + D.off[6], *dtr_slot = pl + D.off[7], *dtr_p = pl + D.off[8],
-                *task_lev_ptr = pl + D.off[9], *task_dst = pl + D.off[10], *task_col = pl + D.off[11],
-                *task_tr_ptr = pl + D.off[12], *tr_a = pl + D.off[13], *tr_b = pl + D.off[14],
-                *asm_ptr = pl + D.off[15], *asm_edge = pl + D.off[16], *g_ptr = pl + D.off[17],
-                *g_edge = pl + D.off[18];
-  // the fin staging area sits where sparse_llt_kernel<1> has it (host LDS plan)
-  int32_t *sdone = after_y + ((D.plan_len + 1) & ~1);
-  const int n_flags = S + 2 * m + D.n_parts;
-  if (tid == 0) fail_s = 0;
-  __syncthreads();  // plan copy complete
-  // 0. assembly (sparse_llt_kernel's sums)
-  if (D.asm_lds) {
-    double *fl = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1));
-    for (int idx = tid; idx < D.E * kFin; idx += 1024) fl[idx] = D.fin[idx];
-    __syncthreads();
-    for (int idx = tid; idx < S * 49; idx += 1024) {
-      const int sl = idx / 49, t = idx - sl * 49;
-      double v = 0.0;
-      for (int q = asm_ptr[sl]; q < asm_ptr[sl + 1]; q++) v += fl[asm_edge[q] * kFin + t];
-      Lb[idx] = (sl < m) ? v : -v;
-    }
-    for (int idx = tid; idx < m * 7; idx += 1024) {
-      const int vv = idx / 7, t = idx - vv * 7;
-      double v = 0.0;
-      for (int q = g_ptr[vv]; q < g_ptr[vv + 1]; q++) {
-        const int ent = g_edge[q];
-        const double gj = fl[(ent >> 1) * kFin + 49 + t];
-        v += (ent & 1) ? gj : -gj;
-      }
-      y[idx] = v;
-    }
-  } else {
-    for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
-    for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
-  }
-  __syncthreads();
-  const int r = lane / 7, c = lane % 7;
-  const bool act49 = lane < 49;
-  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
-  const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
-  double *scr = scratch[wave];
-  // 1. factorisation + forward substitution, level by level
-  for (int l = 0; l < D.levels; l++) {
-    const int cb = lev_ptr[l], nD = lev_ptr[l + 1] - cb;
-    const int tb = task_lev_ptr[l], nO = task_lev_ptr[l + 1] - tb;
-    for (int it = wave; it < nD + nO; it += NW) {
-      if (it < nD) {  // DIAG(k)
-        const int k = lev_col[cb + it];
-        const int q0 = dtr_ptr[k], q1 = dtr_ptr[k + 1];
-        double v = Lb[(size_t)k * 49 + lane49];
-        v = sub_products<false, true>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, nullptr);
-        double bb = y[k * 7 + lane7];
-        bb = sub_matvec<false, false>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, nullptr);
-        double wcol[7];
-        if (diag_factor(v, k, Lb, Di, scr, lane, l7, wcol) && lane == 0) fail_s = 1;
-        fwd_solve_store(bb, wcol, scr, y + (size_t)k * 7, lane);
-      } else {  // the update sum of OFF(t), in place
-        const int t2 = tb + it - nD, dst = task_dst[t2];
-        double v = Lb[(size_t)dst * 49 + lane49];
-        v = sub_products<false, false>(v, Lb, tr_a, tr_b, task_tr_ptr[t2], task_tr_ptr[t2 + 1], r7, c7, lane49,
-                                       lane, nullptr);
-        if (act49) Lb[(size_t)dst * 49 + lane] = v;
-      }
-    }
-    __syncthreads();
-    for (int t2 = tb + wave; t2 < tb + nO; t2 += NW) {  // L_ik = A'_ik W_k^T
-      const int dst = task_dst[t2], k = task_col[t2];
-      if (act49) scr[lane] = Lb[(size_t)dst * 49 + lane];
-      wave_lds_fence();
-      double x = 0.0;
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * Di[(size_t)k * 49 + c7 + mm];
-      if (act49) Lb[(size_t)dst * 49 + lane] = x;
-      wave_lds_fence();
-    }
-    __syncthreads();
-  }
-  if (fail_s) {
-    fail_step(7 * m, D.dx_out, D.info, D.flags + kFlagStop, D.delta_thresh);
-    return;
-  }
-  Sim3f T_pre;  // the retraction's pose of this thread: its latency hides behind the back-substitution
-  if (tid < m) T_pre = load_sim3(D.Twc + 8 * (size_t)(tid + 1));
-  // 2. back-substitution L^T x = y (x overwrites y), levels from the top
-  for (int l = D.levels - 1; l >= 0; l--) {
-    const int cb = lev_ptr[l], nD = lev_ptr[l + 1] - cb;
-    for (int it = wave; it < nD; it += NW) {
-      const int k = lev_col[cb + it];
-      double rr = y[k * 7 + lane7];
-      rr = sub_matvec<false, true>(rr, Lb, col_slot, col_row, col_ptr[k], col_ptr[k + 1], y, lane7, lane49, lane,
-                                   nullptr);
-      double xk = 0.0;
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) xk += Di[(size_t)k * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
-      if (lane < 7) y[k * 7 + lane] = xk;
-    }
-    __syncthreads();
-  }
-  // 3. dx = -x in the original variable order, retraction, ||dx|| (as sparse_llt_kernel)
-  float *dxl = reinterpret_cast<float *>(&scratch[0][0]);
-  const bool dx_lds = m * 7 <= (int)(sizeof(scratch) / sizeof(float));
-  float part = 0.0f;
-  for (int idx = tid; idx < m * 7; idx += 1024) {
-    const int vn = idx / 7, q = idx - vn * 7;
-    const int vo = perm[vn];
-    const float v = -(float)y[idx];
-    D.dx_out[vo * 7 + q] = v;
-    if (dx_lds) dxl[vo * 7 + q] = v;
-    part += v * v;
-  }
-  part = wave_sum(part);
-  if (lane == 0) nrm[wave] = part;
-  __syncthreads();
-  for (int p = tid; p < m; p += 1024) {
-    const Sim3f T = p == tid ? T_pre : load_sim3(D.Twc + 8 * (size_t)(p + 1));
-    float xi[7];
-#pragma unroll
-    for (int q = 0; q < 7; q++) xi[q] = dx_lds ? dxl[p * 7 + q] : D.dx_out[p * 7 + q];
-    store_sim3(D.Twc + 8 * (size_t)(p + 1), retract(xi, T));
-  }
-  if (tid == 0) {
-    float s2 = 0.0f;
-    for (int w2 = 0; w2 < NW; w2++) s2 += nrm[w2];
-    D.info[M3S_INFO_ITERS] += 1;
-    if (sqrtf(s2) < D.delta_thresh) {
-      D.info[M3S_INFO_CONVERGED] = 1;
-      D.flags[kFlagStop] = 1;
-    }
-  }
-}
-
 // ------------------------------------- column tasks over many workgroups --
 // Large graphs (factor in global memory): the sparse columns of the
 // elimination tree below the dense tail are factored as column tasks spread
@@ -2603,98 +2425,6 @@ __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
     if (fin - C.epoch * C.ncols == C.ncols - 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       col_finish(C, lane);
-    }
-  }
-}
-
-// Back-substitution of the sparse columns in ONE workgroup, level by level
-// from the top of the elimination tree (round 3; col_backsub_kernel spread it
-// over the chip as column tasks with epoch-flag hand-offs: ~1-3 us per level
-// of flag hops for ~0.2 us of arithmetic). x lives in LDS; each column's
-// L_ik blocks are fetched in staged batches (one memory latency per batch,
-// sub_matvec), the columns of a level run on the 16 waves side by side and
-// one workgroup barrier separates the levels. Same sums in the same order as
-// col_backsub_kernel: x_k = W_k^T (y_k - sum_i L_ik^T x_i). Then dx = -x,
-// the retraction and the ||dx|| test (col_finish).
-constexpr int kBsWaves = 16;
-__global__ void __launch_bounds__(64 * kBsWaves) bs_level_kernel(ColArgs C) {
-  if (C.flags[kFlagStop]) return;
-  extern __shared__ __attribute__((aligned(16))) double bsm[];
-  __shared__ float nrm[kBsWaves];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int m = C.m;
-  double *y = bsm;                                               // [m][7]
-  double *stg = bsm + (size_t)m * 7 + (size_t)wave * kStageDoubles;  // per-wave stage areas
-  const int32_t *pl = C.plan;
-  const int32_t *perm = pl + C.off[0], *col_ptr = pl + C.off[1], *col_row = pl + C.off[2],
-                *col_slot = pl + C.off[3], *lev_ptr = pl + C.off[4], *lev_col = pl + C.off[5];
-  for (int idx = tid; idx < m * 7; idx += 64 * kBsWaves) y[idx] = C.y[idx];  // y; x of the dense tail
-  const bool failed =
-      __hip_atomic_load(C.flags + kFlagSplitFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  __syncthreads();
-  const int lane7 = lane < 7 ? lane : 0;
-  const int lane49 = lane < 49 ? lane : 0;
-  int nlev = 0;
-  while (nlev < m && lev_ptr[nlev] < m) nlev++;  // levels: lev_ptr[L] == m
-  for (int l = nlev - 1; l >= 0 && !failed; l--) {
-    const int cb = lev_ptr[l], nD = lev_ptr[l + 1] - cb;
-    for (int it = wave; it < nD; it += kBsWaves) {
-      const int k = lev_col[cb + it];
-      if (k >= C.c0) continue;  // dense tail: solved by the tail kernel
-      double wk[7];
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) wk[mm] = C.Dinv[(size_t)k * 49 + mm * 7 + lane7];
-      double rr = y[k * 7 + lane7];
-      rr = sub_matvec<true, true>(rr, C.L, col_slot, col_row, col_ptr[k], col_ptr[k + 1], y, lane7, lane49, lane,
-                                  stg);
-      double xk = 0.0;
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) xk += wk[mm] * readlane_d(rr, mm);
-      if (lane < 7) y[k * 7 + lane] = xk;
-    }
-    __syncthreads();
-  }
-  // dx = -x in the original order, retraction, ||dx|| (col_finish, all lanes)
-  if (failed) {
-    for (int k = tid; k < 7 * m; k += 64 * kBsWaves) C.dx_out[k] = 0.0f;
-    if (tid == 0) {
-      C.flags[kFlagSplitFail] = 0;
-      C.info[M3S_INFO_ITERS] += 1;
-      C.info[M3S_INFO_SOLVE_FAIL] += 1;
-      if (0.0f < C.delta_thresh) {
-        C.info[M3S_INFO_CONVERGED] = 1;
-        C.flags[kFlagStop] = 1;
-      }
-    }
-    return;
-  }
-  float *dxs = reinterpret_cast<float *>(stg - (size_t)wave * kStageDoubles);  // the stage areas, free now
-  float part = 0.0f;
-  for (int idx = tid; idx < 7 * m; idx += 64 * kBsWaves) {
-    const int vn = idx / 7, q = idx - 7 * vn;
-    const int vo = perm[vn];
-    const float v = -(float)y[idx];
-    C.dx_out[vo * 7 + q] = v;
-    dxs[vo * 7 + q] = v;
-    part += v * v;
-  }
-  part = wave_sum(part);
-  if (lane == 0) nrm[wave] = part;
-  __syncthreads();
-  for (int p = tid; p < m; p += 64 * kBsWaves) {
-    const Sim3f T = load_sim3(C.Twc + 8 * (size_t)(p + 1));
-    float xi[7];
-#pragma unroll
-    for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
-    store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, T));
-  }
-  if (tid == 0) {
-    float s2 = 0.0f;
-    for (int w2 = 0; w2 < kBsWaves; w2++) s2 += nrm[w2];
-    C.info[M3S_INFO_ITERS] += 1;
-    if (sqrtf(s2) < C.delta_thresh) {
-      C.info[M3S_INFO_CONVERGED] = 1;
-      C.flags[kFlagStop] = 1;
     }
   }
 }
@@ -3636,8 +3366,6 @@ struct Knobs {
   std::atomic<int> tail_mfma{1};       // M3S_TAIL_MFMA: 0 = the dense tail in sparse_llt_kernel (A/B)
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel (A/B)
   std::atomic<int> track_persistent{1};  // M3S_TRACK_PERSISTENT: 0 = one tracker launch per iteration
-  std::atomic<int> lvl{1};             // M3S_LVL: 0 = small graphs on sparse_llt_kernel's dataflow (A/B)
-  std::atomic<int> bs_lvl{1};          // M3S_BS_LVL: 0 = column-task back-substitution over the chip (A/B)
   std::atomic<int> debug_drop_item{-1};  // test hook only (m3s_set_knob): drop one LLT dispatch item
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -3652,8 +3380,6 @@ struct Knobs {
     env("M3S_TAIL_MFMA", tail_mfma);
     env("M3S_BORDER_SPLIT", border_split);
     env("M3S_TRACK_PERSISTENT", track_persistent);
-    env("M3S_LVL", lvl);
-    env("M3S_BS_LVL", bs_lvl);
   }
 };
 Knobs &knobs() {
@@ -3850,7 +3576,6 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;
 int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st);
-void set_lds_attributes_once();
 
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
@@ -4005,17 +3730,9 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
         }
       }
-      const size_t bs_lds = sizeof(double) * ((size_t)meta.m * 7 + (size_t)kBsWaves * kStageDoubles);
-      if (knobs().bs_lvl != 0 && bs_lds <= kMaxLdsBytes) {
-        set_lds_attributes_once();
-        bs_level_kernel<<<1, 64 * kBsWaves, bs_lds, st>>>(C);
-      } else {
-        const int g4 = std::max(1, std::min(C.ncols, 256));
-        col_backsub_kernel<<<g4, 64, 0, st>>>(C);
-      }
-    } else if (meta.store == 1 && meta.nc == 0 && meta.n_parts == 0 && knobs().lvl != 0)
-      sparse_lvl_kernel<<<1, 1024, meta.lds_bytes, st>>>(D);
-    else if (meta.store == 1)
+      const int g4 = std::max(1, std::min(C.ncols, 256));
+      col_backsub_kernel<<<g4, 64, 0, st>>>(C);
+    } else if (meta.store == 1)
       sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.store == 2)
       sparse_llt_kernel<2><<<1, 1024, meta.lds_bytes, st>>>(D);
@@ -4129,10 +3846,6 @@ void set_lds_attributes_once() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_lvl_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bs_level_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
   });
 }
@@ -5051,7 +4764,7 @@ int m3s_set_knob(const char *name, int value) {
     std::atomic<int> *v;
   } tab[] = {{"plan_cache", &k.plan_cache}, {"dense", &k.dense}, {"dense_tail_min", &k.dense_tail_min},
              {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc}, {"tail_mfma", &k.tail_mfma},
-             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent}, {"lvl", &k.lvl}, {"bs_lvl", &k.bs_lvl},
+             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent},
              {"debug_drop_item", &k.debug_drop_item}};
   for (const auto &t : tab)
     if (std::strcmp(t.n, name) == 0) {

@@ -179,8 +179,8 @@ def test_gn_broken_plan_times_out_as_solve_failure(be, knobs, N, tail):
     waits are bounded). The debug_drop_item knob removes the first item of the
     dispatch list (a leaf DIAG): the items reading its blocks time out, the
     iteration reports INFO_SOLVE_FAIL with dx = 0 and the poses untouched.
-    N = 12: the one-workgroup dataflow (sparse_llt_kernel; knob lvl = 0, the
-    level-synchronous kernel has no waits); N = 140 with a dense tail: the
+    N = 12: the one-workgroup dataflow (sparse_llt_kernel); N = 140 with a
+    dense tail: the
     chip-wide path (df_factor_kernel's epoch flags, tail_cyc_kernel's tagged
     granules, col_backsub_kernel)."""
     import time
@@ -188,9 +188,7 @@ def test_gn_broken_plan_times_out_as_solve_failure(be, knobs, N, tail):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 12 if N > 64 else 24, 16 if N > 64 else 32, seed=37)
-    if tail is None:
-        knobs("lvl", 0)
-    else:
+    if tail is not None:
         knobs("dense_tail_min", tail)
     knobs("debug_drop_item", "0")
     t0 = time.time()
@@ -443,44 +441,3 @@ def test_tail_over_workgroups_matches_one_workgroup(be, N, knobs):
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)
-
-
-@pytest.mark.parametrize("N,mode", [(3, "rays"), (6, "rays"), (12, "calib"), (32, "rays"), (32, "calib"),
-                                    (48, "rays")])
-def test_level_llt_matches_dataflow_llt_bitwise(be, N, mode, knobs):
-    """Small graphs: the level-synchronous LLT (sparse_lvl_kernel, the default
-    for LDS-resident plans without a dense tail) sums the same lists in the
-    same order as the item dataflow (sparse_llt_kernel<1>, knob lvl = 0):
-    poses, dx and info agree bitwise, natural termination included."""
-    from mast3r_slam_amd import synthetic
-
-    g = synthetic.make_graph(N, 24, 32, seed=900 + N)
-    Xs = constrained(g) if mode == "calib" else None
-    for iters, delta in ((4, 0.0), (20, 1e-4)):
-        T_a, dx_a, info_a = run_gpu(be, mode, g, iters, delta, Xs=Xs)
-        knobs("lvl", 0)
-        T_b, dx_b, info_b = run_gpu(be, mode, g, iters, delta, Xs=Xs)
-        knobs("lvl", 1)
-        np.testing.assert_array_equal(info_a, info_b)
-        assert info_a[be.INFO_SOLVE_FAIL] == 0
-        np.testing.assert_array_equal(dx_a, dx_b)
-        np.testing.assert_array_equal(T_a, T_b)
-
-
-@pytest.mark.parametrize("N,tail", [(90, 0), (140, 8), (256, 16)])
-def test_level_backsub_matches_column_tasks_bitwise(be, N, tail, knobs):
-    """Chip-wide path: the sparse back-substitution in one workgroup by levels
-    (bs_level_kernel, the default) sums every column's terms in the order of
-    the column-task kernel over the chip (col_backsub_kernel, knob bs_lvl = 0):
-    dx and poses agree bitwise; no failures. (With and without a dense tail.)"""
-    from mast3r_slam_amd import synthetic
-
-    knobs("dense_tail_min", tail)
-    g = synthetic.make_graph(N, 12, 16, seed=950 + N)
-    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
-    knobs("bs_lvl", 0)
-    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
-    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
-    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
-    np.testing.assert_array_equal(dx_a, dx_b)
-    np.testing.assert_array_equal(T_a, T_b)

@@ -1,10 +1,12 @@
 """Per-call time of the GN solve under solver-knob settings (GPU box).
 
-  python tools/knob_ab.py [M3S_LIB=variants/lib_X.so in the env for a variant]
+  KNOBS='[{"df": 1}, {"df": 0}]' python tools/knob_ab.py
+  (M3S_LIB=variants/lib_X.so in the env for a variant library)
 
 Small images (linearize negligible) so the call time is the solve path:
 median of 20 calls (HIP events) per (graph, knob setting), in one process,
 settings interleaved round-robin to cancel drift."""
+import json
 import os
 import sys
 
@@ -20,7 +22,7 @@ from mast3r_slam_amd import synthetic  # noqa: E402
 
 dev = torch.device("cuda:0")
 GRAPHS = [("calib", 32, 64, 64, 10), ("rays", 140, 32, 32, 3), ("rays", 256, 32, 32, 3)]
-SETTINGS = [dict(lvl=1, bs_lvl=1), dict(lvl=0, bs_lvl=1), dict(lvl=1, bs_lvl=0), dict(lvl=0, bs_lvl=0)]
+SETTINGS = json.loads(os.environ.get("KNOBS", "[{}]"))
 REPS = int(os.environ.get("REPS", "20"))
 
 for mode, N, H, W, iters in GRAPHS:

@@ -97,8 +97,15 @@ int m3s_gauss_newton_rays(const m3s_gn_args *a, void *stream);
 int m3s_gauss_newton_calib(const m3s_gn_args *a, void *stream);
 
 /* ---- stepwise API (edge-sharded multi-GPU path; same math as above) ----
- * m3s_gn_prepare:   rank ii/jj, build + upload the sparse plan, zero info/flags
- *                   (synchronises the stream once).
+ * m3s_gn_prepare:   one prologue kernel ranks ii/jj on the device, writes the
+ *                   task table, zeroes info/flags/dx_out and copies the ids to
+ *                   pinned host memory; no stream synchronisation. The host
+ *                   reads the ids when it first needs them (the first solve,
+ *                   or a linearize of a sub-range: it then waits for the
+ *                   prologue only) to fetch or build the sparse plan, which is
+ *                   uploaded on a side stream while the first linearize runs.
+ *                   E > 2048 (or knob prologue = 0): the host prepare, with
+ *                   one stream synchronisation.
  * m3s_gn_linearize: per-edge local normal equations for edges
  *                   [edge_begin, edge_end) into edge_sums (double[E_loc][36]:
  *                   28 upper-triangular J^T W J, 7 J^T W r, 1 cost, in the
@@ -195,9 +202,10 @@ int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n
 /* Solver knobs (experiments / A/B tests). Defaults are the measured best;
  * the environment (M3S_PLAN_CACHE, M3S_DENSE, M3S_DENSE_TAIL_MIN, M3S_COLS,
  * M3S_DF, M3S_TAIL_CYC, M3S_TAIL_MFMA, M3S_BORDER_SPLIT,
- * M3S_TRACK_PERSISTENT) is read once per process; this sets a knob at run
- * time for the calls that follow. Names: plan_cache, dense, dense_tail_min,
- * cols, df, tail_cyc, tail_mfma, border_split, track_persistent,
+ * M3S_TRACK_PERSISTENT, M3S_PROLOGUE) is read once per process; this sets a
+ * knob at run time for the calls that follow. Names: plan_cache, dense,
+ * dense_tail_min, cols, df, tail_cyc, tail_mfma, border_split,
+ * track_persistent, prologue (0: host-side prepare),
  * debug_drop_item (test hook: drop one dispatch item of the one-workgroup
  * LLT so its bounded waits time out). Returns the previous value, or
  * -2^30 for an unknown name. */

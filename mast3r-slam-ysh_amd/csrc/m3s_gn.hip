@@ -65,7 +65,19 @@ namespace {
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
-constexpr int kTargetBlocks = 2048;  // linearize grid target (edges x chunks)
+#ifndef M3S_TARGET_BLOCKS
+#define M3S_TARGET_BLOCKS 2048
+#endif
+constexpr int kTargetBlocks = M3S_TARGET_BLOCKS;  // linearize grid target (edges x chunks)
+#ifndef M3S_GATHER_BLOCKS
+#define M3S_GATHER_BLOCKS 6400
+#endif
+// the gathering kernel (first GN iteration) prefers ~3x smaller chunks: its
+// random Xi reads then stay closer together in time per XCD (C3: 249 -> 232
+// us, 128 KFs rays: 1092 -> 1004 us; profiles/r03/tb_sweep_r3f.txt)
+constexpr int kGatherBlocks = M3S_GATHER_BLOCKS;
+constexpr int kMaxBlocks = 8192;  // workspace capacity for partials (>= both targets)
+static_assert(kTargetBlocks <= kMaxBlocks && kGatherBlocks <= kMaxBlocks, "linearize grid target above capacity");
 constexpr int kMaxSmallNp = 224;     // register Cholesky limit (n + 1 <= 7 * 32)
 constexpr int kCholThreads = 512;    // 16 x 32 thread grid
 constexpr int64_t kMaxLd = 8192;     // tiled path: back-substitution keeps x in LDS
@@ -77,9 +89,9 @@ constexpr int kFlagSplitFail = 2;  // sparse LLT split launches: a pivot failure
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-inline int64_t chunks_for(int64_t HW, int64_t E_loc) {
+inline int64_t chunks_for(int64_t HW, int64_t E_loc, int64_t target = kTargetBlocks) {
   const int64_t max_chunks = (HW + kBlockPix - 1) / kBlockPix;
-  int64_t c = (kTargetBlocks + E_loc - 1) / (E_loc > 0 ? E_loc : 1);
+  int64_t c = (target + E_loc - 1) / (E_loc > 0 ? E_loc : 1);
   if (c < 1) c = 1;
   if (c > max_chunks) c = max_chunks;
   // make the chunk a multiple of kBlockPix, then recount
@@ -108,7 +120,7 @@ inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cy
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      colsync, tail, tasks, planes, total;
+      colsync, tail, eorder, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -121,7 +133,7 @@ inline size_t edge_cnt_bytes(int64_t E) { return (sizeof(uint32_t) * (size_t)(E 
 inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   Layout L;
   const int64_t n = 7 * (N > 1 ? N - 1 : 0);
-  const int64_t max_partials = kTargetBlocks + E + 1;
+  const int64_t max_partials = kMaxBlocks + E + 1;
   size_t off = 0;
   L.flags = off;
   off = align_up(off + 64 * sizeof(int32_t), 256);
@@ -134,8 +146,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   const int64_t m0 = N > 1 ? N - 1 : 0;
   L.edge_cnt = off;  // per-edge chunk arrival counters (fused finalize), zeroed per call (by the upload)
   off = align_up(off + edge_cnt_bytes(E), 256);
-  L.tasks = off;
-  off = align_up(off + sizeof(int32_t) * (size_t)(kTargetBlocks + E + 16), 256);
+  L.eorder = off;  // linearize edge order (block -> (edge, chunk), block_task)
+  off = align_up(off + sizeof(int32_t) * (size_t)(E + 16), 256);
   L.slot_cap = std::min<int64_t>(m0 * (m0 + 1) / 2, 64 * m0 + 4096) + 1;
   L.plan_cap = (int64_t(1) << 22) + 16 * E + 64 * m0;
   L.plan = off;
@@ -203,7 +215,9 @@ struct LinArgs {
   const int32_t *rank_i;
   const int32_t *rank_j;
   const int32_t *stop;
-  const int32_t *tasks;    // block -> task (e_loc * chunks + c), -1 = idle; null = identity
+  const int32_t *eorder;   // the launch's edges sorted by KF j (block_task); null: block = task
+  int64_t per, E_loc;      // block_task: 8 runs of `per` blocks; edges of the launch
+  uint32_t cnt_base;       // edge_cnt arrivals before this launch in the call (edge_tail)
   float *planes;           // per-edge target-side planes (PixIn), [E_loc][kPlanes][HW]
   float *partials;         // [task][36]
   uint32_t *edge_cnt;      // non-null: the last chunk of an edge to finish also finalizes it into fin
@@ -214,7 +228,17 @@ struct LinArgs {
   float rel_error, delta_norm;
   int64_t HW, edge_begin, chunks, chunk_pix;
   ResidualParams P;
+  const float *Kd;  // calib backend: the caller's 3x3 K (device), read by the kernels (P.fx.. unset)
 };
+
+// The residual parameters of a launch: the intrinsics of a calib backend
+// launch come from the caller's K on the device (uniform loads), so the first
+// linearize of a call can be enqueued before the host has read anything back.
+__device__ __forceinline__ ResidualParams kparams(const LinArgs &A) {
+  ResidualParams P = A.P;
+  if (A.Kd) P.fx = A.Kd[0], P.fy = A.Kd[4], P.cx = A.Kd[2], P.cy = A.Kd[5];
+  return P;
+}
 
 // one pixel's gathered inputs -> target-side inputs (shared by all paths)
 template <int MODE, bool TRACK>
@@ -241,9 +265,17 @@ __device__ __forceinline__ PixIn<MODE> gather_pixel(const LinArgs &A, const floa
   return make_pixin<MODE>(A.P, Xi, ok, q, u_t, v_t);
 }
 
-// block -> (edge, chunk) through the XCD-grouped task table
+// block -> task (e_loc * chunks + c). The E_loc x chunks tasks sorted by
+// (chunk, KF j) are cut into 8 contiguous runs and run x is dealt to blocks
+// x, x + 8, x + 16, ...: the edges that stream the same Xj chunk run back to
+// back on one XCD (blocks b and b + 8 share an XCD under round-robin
+// placement; speed only: partials are indexed by task). -1: idle padding.
 __device__ __forceinline__ int64_t block_task(const LinArgs &A) {
-  return A.tasks ? (int64_t)A.tasks[blockIdx.x] : (int64_t)blockIdx.x;
+  if (!A.eorder) return (int64_t)blockIdx.x;
+  const int64_t b = blockIdx.x, t = (b & 7) * A.per + (b >> 3);
+  if (t >= A.E_loc * A.chunks) return -1;
+  const int64_t c = t / A.E_loc;
+  return (int64_t)A.eorder[t - c * A.E_loc] * A.chunks + c;
 }
 
 // The block partial is stored write-through (sc1), so the edge's last chunk
@@ -409,7 +441,7 @@ __device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64
   if (t == 0) {
     const uint32_t ch = (uint32_t)A.chunks;
     const uint32_t old = __hip_atomic_fetch_add(A.edge_cnt + e_loc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = (old % ch) == ch - 1;
+    last_s = ((old - A.cnt_base) % ch) == ch - 1;
   }
   __syncthreads();
   if (!last_s) return;
@@ -463,6 +495,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   const int64_t c = b - e_loc * A.chunks;
   const int64_t e = A.edge_begin + e_loc;
   const int64_t HW = A.HW;
+  const ResidualParams P = kparams(A);
 
   Sim3f Tij;
   const float *Xs_i, *Xs_j, *Cs_i = nullptr, *Cs_j = nullptr;
@@ -540,7 +573,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
 #pragma unroll
           for (int k = 0; k < 3; k++) X2[k] = f32x2{Xj[2 * h][k], Xj[2 * h + 1][k]};
           act2(Tm, X2, Y2);
-          pixel_contrib2<MODE, NPL>(acc, A.P, in2, Y2);
+          pixel_contrib2<MODE, NPL>(acc, P, in2, Y2);
         }
       } else
 #endif
@@ -549,7 +582,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
         for (int s = 0; s < 4; s++) {
           float Y[3];
           act(Tm, Xj[s], Y);
-          pixel_contrib<MODE>(acc, A.P, in[s], Y);
+          pixel_contrib<MODE>(acc, P, in[s], Y);
         }
       }
       if (WPACK) {
@@ -578,13 +611,13 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
 #pragma unroll
         for (int k = 0; k < 3; k++) X2[k] = f32x2{Xj[k], Xj[k]};
         act2(Tm, X2, Y2);
-        pixel_contrib2<MODE, NPL>(acc, A.P, in2, Y2);
+        pixel_contrib2<MODE, NPL>(acc, P, in2, Y2);
       } else
 #endif
       {
         float Y[3];
         act(Tm, Xj, Y);
-        pixel_contrib<MODE>(acc, A.P, in, Y);
+        pixel_contrib<MODE>(acc, P, in, Y);
       }
       if (WPACK) {
 #pragma unroll
@@ -625,6 +658,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   const int ri = A.rank_i[e], rj = A.rank_j[e];
   const Sim3f Tij = relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj));
   const Sim3Mat Tm = sim3_matrix(Tij);
+  const ResidualParams P = kparams(A);
   const float *__restrict__ Xs_j = A.Xs + (size_t)rj * HW * 3;
   constexpr int NPL = PixIn<MODE>::kPlanes;
   const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
@@ -656,7 +690,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].x, pv[k].y};
       f32x2 Y[3];
       act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL>(acc, A.P, in, Y);
+      pixel_contrib2<MODE, NPL>(acc, P, in, Y);
     }
     __builtin_amdgcn_sched_barrier(0);
     {
@@ -666,7 +700,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].z, pv[k].w};
       f32x2 Y[3];
       act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL>(acc, A.P, in, Y);
+      pixel_contrib2<MODE, NPL>(acc, P, in, Y);
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -681,7 +715,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       for (int k = 0; k < NPL; k++) in.v[k] = pv[k][s];
       float Y[3];
       act(Tm, Xj[s], Y);
-      pixel_contrib<MODE>(acc, A.P, in, Y);
+      pixel_contrib<MODE>(acc, P, in, Y);
       // one pixel at a time: keeps the packed kernel at ~90 VGPRs (5 waves/SIMD)
       if ((s + 1) % 1 == 0) __builtin_amdgcn_sched_barrier(0);
     }
@@ -735,7 +769,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       }
       f32x2 Y[3];
       act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL>(acc, A.P, in, Y);
+      pixel_contrib2<MODE, NPL>(acc, P, in, Y);
       __builtin_amdgcn_sched_barrier(0);
     }
 #else
@@ -3251,6 +3285,147 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
   finish_step(xbuf, dxs, nrm, n, Twc, N, dx_out, info, stop, delta_thresh);
 }
 
+// ------------------------------------------------------ call prologue --
+// The per-call setup of a GN call on the device, so the call's first
+// linearize can be enqueued right behind it and nothing waits for the host:
+// the edge ids are ranked (the reference's torch::_unique(cat(ii, jj), sorted,
+// return_inverse), gn_kernels.cu:1154-1160) by a bitonic sort of the 2E ids in
+// LDS, the ranks and the linearize edge order (edges grouped by KF j,
+// block_task; the order inside a KF bucket is free: partials are indexed by
+// task, so the sums do not depend on it) go to the workspace, flags / edge
+// counters / info /
+// dx_out are initialised, and ii, jj, K are copied into pinned host memory
+// for the host's symbolic analysis, which then runs while the first linearize
+// kernel does (host_finish).
+constexpr int kProThreads = 1024;
+constexpr int kProMaxE = 2048;  // 2E ids sorted in LDS; larger edge sets take the host path
+struct ProArgs {
+  const int64_t *ii, *jj;
+  const float *K;      // calib: 3x3 (else null)
+  int64_t *down_ii, *down_jj;
+  float *down_K;       // host-mapped pinned copies
+  int E, N, P2;        // P2: power of two >= 2E
+  int32_t *flags, *rank_i, *rank_j, *eorder, *info;
+  uint32_t *edge_cnt;
+  float *dx_out;
+  int n_dx;
+};
+
+// exclusive prefix of one int per thread over the block; *total = block sum
+__device__ int block_excl_scan(int v, int *wsum, int *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < nw; w++) {
+      const int t = wsum[w];
+      wsum[w] = acc;
+      acc += t;
+    }
+    wsum[16] = acc;
+  }
+  __syncthreads();
+  const int r = wsum[wave] + x - v;
+  *total = wsum[16];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ int lower_bound_i64(const int64_t *u, int n, int64_t v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (u[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
+  extern __shared__ __attribute__((aligned(16))) int64_t pro_smem[];
+  __shared__ int wsum[17];
+  const int E = A.E, P2 = A.P2, tid = threadIdx.x;
+  constexpr int64_t kPad = 0x7fffffffffffffffLL;
+  int64_t *keys = pro_smem, *uniq = keys + P2;
+  int32_t *cnt = reinterpret_cast<int32_t *>(uniq + P2);  // [P2]: KF bucket counts, then offsets
+  int32_t *erj = cnt + P2;  // [E]
+  for (int q = tid; q < E; q += kProThreads) {
+    const int64_t a = A.ii[q], b = A.jj[q];
+    A.down_ii[q] = a, A.down_jj[q] = b;
+    keys[q] = a, keys[E + q] = b;
+  }
+  for (int q = 2 * E + tid; q < P2; q += kProThreads) keys[q] = kPad;
+  if (A.K && tid < 9) A.down_K[tid] = A.K[tid];
+  for (int q = tid; q <= E; q += kProThreads) A.edge_cnt[q] = 0u;
+  for (int q = tid; q < A.n_dx; q += kProThreads) A.dx_out[q] = 0.0f;
+  if (tid < 64) A.flags[tid] = 0;
+  __syncthreads();
+  for (int k = 2; k <= P2; k <<= 1)  // bitonic sort, ascending
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P2; i += kProThreads) {
+        const int l = i ^ j;
+        if (l > i) {
+          const int64_t x = keys[i], y = keys[l];
+          if ((x > y) == ((i & k) == 0)) keys[i] = y, keys[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+  // the sorted unique ids, in order (each thread a run of <= 4 sorted keys)
+  const int seg = (P2 + kProThreads - 1) / kProThreads;
+  auto first = [&](int i) { return i < P2 && keys[i] != kPad && (i == 0 || keys[i] != keys[i - 1]); };
+  int nf = 0;
+  for (int q = 0; q < seg; q++) nf += first(tid * seg + q) ? 1 : 0;
+  int nu = 0;
+  int at_ = block_excl_scan(nf, wsum, &nu);
+  for (int q = 0; q < seg; q++)
+    if (first(tid * seg + q)) uniq[at_++] = keys[tid * seg + q];
+  __syncthreads();
+  for (int e = tid; e < E; e += kProThreads) {
+    const int ri = lower_bound_i64(uniq, nu, A.ii[e]), rj = lower_bound_i64(uniq, nu, A.jj[e]);
+    A.rank_i[e] = ri, A.rank_j[e] = rj;
+    erj[e] = rj;
+  }
+  const bool bad = nu > A.N;
+  if (tid < 8) A.info[tid] = tid == M3S_INFO_N_UNIQUE ? nu : (tid == M3S_INFO_BAD_EDGE && bad) ? 1 : 0;
+  if (tid == 0 && bad) A.flags[kFlagStop] = 1;  // every launch of the call is a no-op
+  if (bad || E == 0) return;                     // (uniform)
+  for (int q = tid; q < nu; q += kProThreads) cnt[q] = 0;
+  __syncthreads();
+  for (int e = tid; e < E; e += kProThreads) atomicAdd(&cnt[erj[e]], 1);
+  __syncthreads();
+  const int segn = (nu + kProThreads - 1) / kProThreads;  // <= 4
+  int cl[4] = {0, 0, 0, 0}, sum = 0;
+  for (int q = 0; q < segn; q++) {
+    const int i = tid * segn + q;
+    cl[q] = i < nu ? cnt[i] : 0;
+    sum += cl[q];
+  }
+  int tot = 0;
+  int off = block_excl_scan(sum, wsum, &tot);
+  for (int q = 0; q < segn; q++) {
+    const int i = tid * segn + q;
+    if (i < nu) cnt[i] = off, off += cl[q];
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += kProThreads) A.eorder[atomicAdd(&cnt[erj[e]], 1)] = e;
+}
+inline size_t prologue_lds(int E, int P2) {
+  return sizeof(int64_t) * 2 * (size_t)P2 + sizeof(int32_t) * ((size_t)P2 + (size_t)E);
+}
+inline int prologue_p2(int64_t E) {
+  int p = 2;
+  while (p < 2 * E) p <<= 1;
+  return p;
+}
+
 // ---------------------------------------------------------------- host --
 inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -3366,6 +3541,7 @@ struct Knobs {
   std::atomic<int> tail_mfma{1};       // M3S_TAIL_MFMA: 0 = the dense tail in sparse_llt_kernel (A/B)
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel (A/B)
   std::atomic<int> track_persistent{1};  // M3S_TRACK_PERSISTENT: 0 = one tracker launch per iteration
+  std::atomic<int> prologue{1};        // M3S_PROLOGUE: 0 = host prepare (ids read back, then the uploads)
   std::atomic<int> debug_drop_item{-1};  // test hook only (m3s_set_knob): drop one LLT dispatch item
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -3380,6 +3556,7 @@ struct Knobs {
     env("M3S_TAIL_MFMA", tail_mfma);
     env("M3S_BORDER_SPLIT", border_split);
     env("M3S_TRACK_PERSISTENT", track_persistent);
+    env("M3S_PROLOGUE", prologue);
   }
 };
 Knobs &knobs() {
@@ -3409,17 +3586,20 @@ struct PlanMeta {
   std::vector<int32_t> h_plan;     // flattened plan (host copy of the upload)
   int32_t h_info[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int32_t h_flags[64] = {0};
-  int64_t n_blocks_full = 0;       // task-table length of the full edge range
-  std::vector<int32_t> tasks_r;    // task table of a sharded rank's edge range
   bool has_K = false;
   float K4[4] = {0.f, 0.f, 0.f, 0.f};  // fx, fy, cx, cy (calib; read once per call)
-  int64_t range_b = -1, range_e = -1, n_blocks = 0;
+  int64_t range_b = -1, range_e = -1;  // the edge range last linearized
+  bool order_ok = false;               // its edge order is in the workspace (Layout::eorder)
   bool planes_ok = false;
-  std::vector<int32_t> tasks;
+  std::vector<int32_t> eorder;         // host copy of the full range's order (host prepare)
   // the symbolic plan of this call is built by its first solve (cache miss at
   // prepare): the host analysis then overlaps the first linearize kernel
   bool plan_pending = false;
   bool force_dense = false;
+  // the ids of this call are still on their way to the host (device prologue,
+  // gn_prepare_async): host_finish reads them from pinned slot `slot`
+  bool host_pending = false;
+  int slot = -1;
 };
 
 // What a solve launch reads of the registry entry: the scalars and plan
@@ -3444,11 +3624,22 @@ std::unordered_map<const void *, PlanMeta> g_reg;
 // table). Pageable copies were one staged, host-synchronous transfer each
 // (~7 per call); an event per buffer guards it until the copy that reads it
 // has left. The registry entries own no memory a queued copy still reads.
+// Pinned slot the device prologue writes a call's ii, jj and K into (host-
+// mapped); busy from the prepare until the host has read it (host_finish or
+// release), its event marks the prologue's completion.
+struct DownSlot {
+  char *p = nullptr, *dp = nullptr;  // host / device view
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool busy = false, used = false;
+};
 struct Staging {
   char *down = nullptr, *up = nullptr, *plan_up = nullptr, *tasks_up = nullptr;
   size_t down_cap = 0, up_cap = 0, plan_cap = 0, tasks_cap = 0;
   hipEvent_t ev = nullptr, plan_ev = nullptr, tasks_ev = nullptr;
   bool pending = false, plan_pending = false, tasks_pending = false;
+  hipStream_t side = nullptr;  // plan uploads that must not queue behind a running linearize
+  std::vector<DownSlot> slots;
 };
 // One staging set per device: an event recorded on one device's stream cannot
 // guard another device's copies (a process may drive GN on several GPUs).
@@ -3469,33 +3660,49 @@ Staging *stage_for_device() {  // caller holds g_stage_mu
   Staging &S = g_stages[dev];
   for (hipEvent_t *e : {&S.ev, &S.plan_ev, &S.tasks_ev})
     if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (!S.side && hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking) != hipSuccess) return nullptr;
   return &S;
 }
-
-// Task table: the E_loc x chunks (edge, chunk) tasks sorted by (chunk, KF j),
-// cut into 8 contiguous runs, run x dealt to blocks x, x+8, x+16, ... so the
-// edges that stream the same Xj chunk run back to back on one XCD (blocks b
-// and b+8 share an XCD under round-robin placement; speed only).
-void build_tasks(const std::vector<int32_t> &rj, int64_t eb, int64_t E_loc, int64_t chunks,
-                 std::vector<int32_t> &out) {
-  const int64_t T = E_loc * chunks;
-  std::vector<int64_t> order(T);
-  for (int64_t t = 0; t < T; t++) order[t] = t;
-  auto key = [&](int64_t t) {
-    const int64_t e = t / chunks, c = t - e * chunks;
-    return std::make_tuple(c, rj[eb + e], e);
-  };
-  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return key(x) < key(y); });
-  const int64_t per = (T + 7) / 8;
-  out.assign(8 * per, -1);
-  for (int64_t t = 0; t < T; t++) {
-    const int64_t x = t / per, pos = t - x * per;
-    out[8 * pos + x] = (int32_t)order[t];
+// A free pinned slot of at least `need` bytes (caller holds g_stage_mu).
+int acquire_slot(Staging &SG, size_t need) {
+  int k = -1;
+  for (int q = 0; q < (int)SG.slots.size(); q++)
+    if (!SG.slots[q].busy) {
+      k = q;
+      break;
+    }
+  if (k < 0) {
+    SG.slots.emplace_back();
+    k = (int)SG.slots.size() - 1;
   }
+  DownSlot &D = SG.slots[k];
+  if (D.used && hipEventSynchronize(D.ev) != hipSuccess) return -1;  // its last prologue has finished writing
+  if (!D.ev && hipEventCreateWithFlags(&D.ev, hipEventDisableTiming) != hipSuccess) return -1;
+  if (need > D.cap) {
+    if (D.p) (void)hipHostFree(D.p);
+    D.p = D.dp = nullptr, D.cap = 0;
+    const size_t n = std::max<size_t>(need + need / 2, 1 << 16);
+    if (hipHostMalloc(reinterpret_cast<void **>(&D.p), n, hipHostMallocDefault) != hipSuccess) return -1;
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, D.p, 0) != hipSuccess) return -1;
+    D.dp = static_cast<char *>(dp), D.cap = n;
+  }
+  D.busy = true, D.used = true;
+  return k;
 }
 
+// Linearize edge order of an edge range: its edges (local indices) sorted by
+// KF j (block_task deals the (chunk, KF j)-sorted tasks over the XCDs).
+void build_eorder(const std::vector<int32_t> &rj, int64_t eb, int64_t E_loc, std::vector<int32_t> &out) {
+  out.resize((size_t)E_loc);
+  for (int64_t e = 0; e < E_loc; e++) out[e] = (int32_t)e;
+  std::stable_sort(out.begin(), out.end(), [&](int32_t x, int32_t y) { return rj[eb + x] < rj[eb + y]; });
+}
+
+int host_finish(const m3s_gn_args *a, hipStream_t st);
+
 int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb, int64_t ee,
-                      double *edge_sums, hipStream_t st, bool fuse_fin = false) {
+                      double *edge_sums, hipStream_t st, bool fuse_fin = false, int64_t *chunks_used = nullptr) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
   const int64_t E_loc = ee - eb;
@@ -3515,21 +3722,26 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
   L.partials = at<float>(ws, Ly.partials);
   L.planes = at<float>(ws, Ly.planes);
-  L.tasks = nullptr;
+  L.eorder = nullptr;
+  L.cnt_base = 0;
   // fused finalize only over the whole edge set (single-GPU solve)
   L.edge_cnt = (fuse_fin && eb == 0 && ee == a->E) ? at<uint32_t>(ws, Ly.edge_cnt) : nullptr;
   L.fin = at<double>(ws, Ly.fin);
   L.HW = a->HW;
   L.edge_begin = eb;
-  L.chunks = chunks_for(a->HW, E_loc);
-  L.chunk_pix = chunk_pixels(a->HW, L.chunks);
+  L.E_loc = E_loc;
   L.P = P;
+  L.Kd = a->mode == M3S_MODE_CALIB ? a->K : nullptr;
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xs, 16) && vec_ok(a->Cs, 16) && vec_ok(a->Q, 16) &&
                    vec_ok(a->idx_ii2jj, 16) && vec_ok(a->valid_match, 4);
   const bool can_pack = vec &&
                         (a->mode != M3S_MODE_CALIB || (a->width < 65536 && a->height < 32768));
-  int64_t blocks = E_loc * L.chunks;
   int pack = 0;
+  bool ordered = false;
+  if (eb != 0 || ee != a->E) {  // a sharded rank's range: its edge order is built from the host ranks
+    const int rc = host_finish(a, st);
+    if (rc) return rc;
+  }
   {
     std::lock_guard<std::mutex> stage_lock(g_stage_mu);  // (lock order: staging, then registry)
     std::lock_guard<std::mutex> g(g_reg_mu);
@@ -3537,37 +3749,47 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
     if (it == g_reg.end()) return M3S_EINVAL;  // m3s_gn_prepare not called on this workspace
     PlanMeta &M = it->second;
     if (M.range_b != eb || M.range_e != ee) {  // a sharded rank's own edge range
-      M.range_b = eb, M.range_e = ee, M.planes_ok = false;
-      M.n_blocks = 0;
+      M.range_b = eb, M.range_e = ee, M.planes_ok = false, M.order_ok = false;
       if ((int64_t)M.rj.size() >= ee) {
-        M.tasks_r.clear();
-        build_tasks(M.rj, eb, E_loc, L.chunks, M.tasks_r);
+        std::vector<int32_t> order;
+        build_eorder(M.rj, eb, E_loc, order);
         // uploaded from pinned staging guarded by an event, so the registry
         // entry owns no host memory a queued copy still reads (m3s_gn_release
         // need not synchronise)
         Staging *SG = stage_for_device();
-        const size_t nb = sizeof(int32_t) * M.tasks_r.size();
+        const size_t nb = sizeof(int32_t) * order.size();
         if (!SG) return M3S_ELAUNCH;
         if (SG->tasks_pending && hipEventSynchronize(SG->tasks_ev) != hipSuccess) return M3S_ELAUNCH;
         SG->tasks_pending = false;
         if (!pinned_reserve(SG->tasks_up, SG->tasks_cap, nb)) return M3S_ELAUNCH;
-        memcpy(SG->tasks_up, M.tasks_r.data(), nb);
-        if (hipMemcpyAsync(at<int32_t>(ws, Ly.tasks), SG->tasks_up, nb, hipMemcpyHostToDevice, st) != hipSuccess ||
+        memcpy(SG->tasks_up, order.data(), nb);
+        if (hipMemcpyAsync(at<int32_t>(ws, Ly.eorder), SG->tasks_up, nb, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipEventRecord(SG->tasks_ev, st) != hipSuccess)
           return M3S_ELAUNCH;
         SG->tasks_pending = true;
-        M.n_blocks = (int64_t)M.tasks_r.size();
+        M.order_ok = true;
       }
     }
-    if (M.n_blocks > 0) {
-      L.tasks = at<int32_t>(ws, Ly.tasks);
-      blocks = M.n_blocks;
-    }
+    ordered = M.order_ok;
     if (can_pack) {
       pack = M.planes_ok ? 2 : 1;
       M.planes_ok = true;
     }
   }
+  // chunking: the gathering kernel's own (smaller chunks); the packed kernel
+  // counts its arrivals after the first iteration's (edge_tail)
+  const int64_t c_gather = chunks_for(a->HW, E_loc, kGatherBlocks);
+  L.chunks = pack == 2 ? chunks_for(a->HW, E_loc) : c_gather;
+  L.chunk_pix = chunk_pixels(a->HW, L.chunks);
+  L.cnt_base = pack == 2 ? (uint32_t)c_gather : 0u;
+  const int64_t T = E_loc * L.chunks;
+  L.per = (T + 7) / 8;
+  int64_t blocks = T;
+  if (ordered) {
+    L.eorder = at<int32_t>(ws, Ly.eorder);
+    blocks = 8 * L.per;
+  }
+  if (chunks_used) *chunks_used = L.chunks;
   int rc = dispatch_linearize<false>(a->mode, L, blocks, vec, pack, st);
   if (rc || !edge_sums) return rc;  // NULL edge_sums: partials only (kernel timing)
   edge_reduce_kernel<<<dim3((unsigned)E_loc), dim3(64), 0, st>>>(L.partials, L.chunks, edge_sums, L.stop);
@@ -3587,7 +3809,9 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
   int32_t *stop = flags + kFlagStop;
   const int64_t n = Ly.n, ld = Ly.ld;
   if (a->N <= 1) return M3S_OK;
-  int rc0 = finish_plan(a, Ly, st);
+  int rc0 = host_finish(a, st);
+  if (rc0) return rc0;
+  rc0 = finish_plan(a, Ly, st);
   if (rc0) return rc0;
   PlanMeta meta;
   {
@@ -3847,6 +4071,8 @@ void set_lds_attributes_once() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(sparse_llt_kernel<2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gn_prologue_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
   });
 }
 
@@ -3942,6 +4168,24 @@ bool reset_plan_flags(const PlanMeta &M, const Layout &Ly, void *ws, hipStream_t
   return ok;
 }
 
+// Upload a plan on the device's side stream and make `st` wait for it: the
+// copy runs while the first linearize kernel does instead of queueing behind
+// it. Callers have waited for every earlier launch on `st` (the prologue's
+// event or a stream sync), so nothing still running there reads `dst`.
+bool upload_plan(Staging *SG, PlanMeta &M, char *dst, hipStream_t st) {
+  if (!(M.sparse && !M.h_plan.empty())) return true;
+  const size_t nb = sizeof(int32_t) * M.h_plan.size();
+  if (SG->plan_pending && hipEventSynchronize(SG->plan_ev) != hipSuccess) return false;
+  SG->plan_pending = false;
+  if (!pinned_reserve(SG->plan_up, SG->plan_cap, nb)) return false;
+  memcpy(SG->plan_up, M.h_plan.data(), nb);
+  bool ok = hipMemcpyAsync(dst, SG->plan_up, nb, hipMemcpyHostToDevice, SG->side) == hipSuccess;
+  ok &= hipEventRecord(SG->plan_ev, SG->side) == hipSuccess;
+  ok &= hipStreamWaitEvent(st, SG->plan_ev, 0) == hipSuccess;
+  SG->plan_pending = ok;
+  return ok;
+}
+
 // Test hook for the bounded waits (tests/test_gpu_backend.py, knob
 // debug_drop_item): drop one item of sparse_llt_kernel's dispatch list, so the
 // items that read its blocks wait on a flag that is never set; the waits time
@@ -4009,16 +4253,14 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       }
     }
   }
+  if (hit && E > 0 && meta.eorder.empty()) build_eorder(meta.rj, 0, E, meta.eorder);  // cached by the prologue path
   if (!hit) {
     // ranks and the full-range task table now (the first linearize needs
     // them); the symbolic plan is built by the first solve of this call,
     // while the first linearize kernel runs (finish_plan)
     meta.h_ri = ri;
     meta.rj = rj;
-    if (E > 0) {
-      build_tasks(meta.rj, 0, E, chunks_for(a->HW, E), meta.tasks);
-      meta.n_blocks_full = (int64_t)meta.tasks.size();
-    }
+    if (E > 0) build_eorder(meta.rj, 0, E, meta.eorder);
     meta.sparse = !bad && !force_dense && a->N > 1;  // the expected outcome (the dense path reads partials either way)
     meta.plan_pending = !bad && a->N > 1;
     meta.force_dense = force_dense;
@@ -4032,11 +4274,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
     meta.K4[0] = hK[0], meta.K4[1] = hK[4], meta.K4[2] = hK[2], meta.K4[3] = hK[5];
   }
   meta.planes_ok = false;
-  if (meta.n_blocks_full > 0) {
-    meta.range_b = 0, meta.range_e = E, meta.n_blocks = meta.n_blocks_full;
-  } else {
-    meta.range_b = meta.range_e = -1, meta.n_blocks = 0;
-  }
+  meta.range_b = 0, meta.range_e = E, meta.order_ok = E > 0;
   if (meta.sparse && !meta.plan_pending && meta.lds_bytes > 64 * 1024) set_lds_attributes_once();
   std::lock_guard<std::mutex> g(g_reg_mu);
   PlanMeta &M = g_reg[ws];
@@ -4045,13 +4283,13 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   if (!M.plan_pending) ok &= reset_plan_flags(M, Ly, ws, st);
   M.epoch = 0;
   if (!M.plan_pending) apply_drop_item(M);
-  // one upload: flags | rank_i | rank_j | edge counters | tasks [| plan] (the
+  // one upload: flags | rank_i | rank_j | edge counters | edge order [| plan] (the
   // layout keeps them in this order), then info (the caller's tensor) from
   // the same buffer
   const bool with_plan = M.sparse && !M.plan_pending && !M.h_plan.empty();
-  const bool with_tasks = M.n_blocks > 0;
+  const bool with_tasks = E > 0;
   size_t n_up = with_plan ? Ly.plan - Ly.flags + sizeof(int32_t) * M.h_plan.size()
-                          : with_tasks ? Ly.tasks - Ly.flags + sizeof(int32_t) * M.tasks.size()
+                          : with_tasks ? Ly.eorder - Ly.flags + sizeof(int32_t) * M.eorder.size()
                                        : Ly.edge_cnt - Ly.flags + edge_cnt_bytes(E);
   n_up = align_up(n_up, 16);
   if (!pinned_reserve(SG->up, SG->up_cap, n_up + sizeof M.h_info)) return M3S_ELAUNCH;
@@ -4062,7 +4300,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
     memcpy(up + (Ly.rank_i - Ly.flags), M.h_ri.data(), sizeof(int32_t) * E);
     memcpy(up + (Ly.rank_j - Ly.flags), M.rj.data(), sizeof(int32_t) * E);
   }
-  if (with_tasks) memcpy(up + (Ly.tasks - Ly.flags), M.tasks.data(), sizeof(int32_t) * M.tasks.size());
+  if (with_tasks) memcpy(up + (Ly.eorder - Ly.flags), M.eorder.data(), sizeof(int32_t) * M.eorder.size());
   if (with_plan) memcpy(up + (Ly.plan - Ly.flags), M.h_plan.data(), sizeof(int32_t) * M.h_plan.size());
   memcpy(up + n_up, M.h_info, sizeof M.h_info);
   ok &= hipMemcpyAsync(at<char>(ws, Ly.flags), up, n_up, hipMemcpyHostToDevice, st) == hipSuccess;
@@ -4110,22 +4348,147 @@ int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st) {
     C.N = a->N, C.HW = a->HW, C.E = a->E, C.dense = force_dense, C.ri = ri, C.rj = rj;
     C.tail_min = dense_tail_min();
     C.meta = M;
-    C.meta.tasks_r.clear();
     std::lock_guard<std::mutex> gc(g_cache_mu);
     g_cache.insert(g_cache.begin(), std::move(C));
     if (g_cache.size() > kPlanCacheSize) g_cache.pop_back();
   }
   bool ok = reset_plan_flags(M, Ly, ws, st);
   apply_drop_item(M);
-  if (M.sparse && !M.h_plan.empty()) {
-    const size_t nb = sizeof(int32_t) * M.h_plan.size();
-    if (!pinned_reserve(SG->plan_up, SG->plan_cap, nb)) return M3S_ELAUNCH;
-    memcpy(SG->plan_up, M.h_plan.data(), nb);
-    ok &= hipMemcpyAsync(at<char>(ws, Ly.plan), SG->plan_up, nb, hipMemcpyHostToDevice, st) == hipSuccess;
-    ok &= hipEventRecord(SG->plan_ev, st) == hipSuccess;
-    SG->plan_pending = ok;
-  }
+  ok &= upload_plan(SG, M, at<char>(ws, Ly.plan), st);
   return ok ? M3S_OK : M3S_ELAUNCH;
+}
+
+// The host half of an async prepare (gn_prepare_async), at the first point a
+// call needs its ids on the host (its first solve, or a sharded rank's edge
+// range): wait for the prologue (normally long done: the first linearize is
+// queued behind it), read ii / jj / K from the pinned slot, rank the ids on
+// the host (the plan and its cache key need them), and fetch the cached plan;
+// a miss leaves the plan to finish_plan. The linearize state of the entry
+// (range, task table, planes) is the prologue's and stays.
+int host_finish(const m3s_gn_args *a, hipStream_t st) {
+  void *ws = a->workspace;
+  int slot = -1;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(ws);
+    if (it == g_reg.end()) return M3S_EINVAL;
+    if (!it->second.host_pending) return M3S_OK;
+    slot = it->second.slot;
+  }
+  const int64_t E = a->E;
+  std::vector<int64_t> hii((size_t)E), hjj((size_t)E);
+  float hK[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    std::lock_guard<std::mutex> stage_lock(g_stage_mu);
+    Staging *SG = stage_for_device();
+    if (!SG || slot < 0 || slot >= (int)SG->slots.size()) return M3S_ELAUNCH;
+    DownSlot &D = SG->slots[slot];
+    if (hipEventSynchronize(D.ev) != hipSuccess) return M3S_ELAUNCH;
+    if (a->mode == M3S_MODE_CALIB) memcpy(hK, D.p, sizeof hK);
+    if (E > 0) {
+      memcpy(hii.data(), D.p + 64, sizeof(int64_t) * (size_t)E);
+      memcpy(hjj.data(), D.p + 64 + sizeof(int64_t) * (size_t)E, sizeof(int64_t) * (size_t)E);
+    }
+    D.busy = false;
+  }
+  std::vector<int32_t> ri, rj;
+  const int nu = host_remap(hii.data(), hjj.data(), E, ri, rj);
+  const bool bad = nu > a->N;  // the prologue has stopped the call (flags, info)
+  const Layout Ly = gn_layout(a->N, a->HW, a->E);
+  bool force_dense;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    force_dense = g_reg.at(ws).force_dense;
+  }
+  PlanMeta hitm;
+  bool hit = false;
+  if (!bad && plan_cache_enabled()) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    for (size_t q = 0; q < g_cache.size(); q++) {
+      const PlanCacheEntry &C = g_cache[q];
+      if (C.N == a->N && C.HW == a->HW && C.E == E && C.dense == force_dense &&
+          C.tail_min == dense_tail_min() && C.ri == ri && C.rj == rj) {
+        hitm = C.meta;
+        std::rotate(g_cache.begin(), g_cache.begin() + q, g_cache.begin() + q + 1);
+        hit = true;
+        break;
+      }
+    }
+  }
+  if (hit && hitm.sparse && hitm.lds_bytes > 64 * 1024) set_lds_attributes_once();
+  std::lock_guard<std::mutex> stage_lock(g_stage_mu);
+  Staging *SG = stage_for_device();
+  if (!SG) return M3S_ELAUNCH;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  PlanMeta &M = g_reg[ws];
+  M.host_pending = false, M.slot = -1;
+  M.h_ri = std::move(ri), M.rj = std::move(rj);
+  M.K4[0] = hK[0], M.K4[1] = hK[4], M.K4[2] = hK[2], M.K4[3] = hK[5];
+  if (bad) {
+    M.sparse = false, M.plan_pending = false;
+    return M3S_OK;
+  }
+  if (!hit) return M3S_OK;  // plan_pending: finish_plan builds it
+  M.sparse = hitm.sparse, M.store = hitm.store, M.asm_lds = hitm.asm_lds, M.lds_bytes = hitm.lds_bytes;
+  M.m = hitm.m, M.S = hitm.S, M.levels = hitm.levels, M.plan_len = hitm.plan_len;
+  M.n_items = hitm.n_items, M.n_tasks = hitm.n_tasks, M.n_parts = hitm.n_parts, M.nc = hitm.nc;
+  M.off_dfitems = hitm.off_dfitems, M.n_dfitems = hitm.n_dfitems;
+  M.img = hitm.img;
+  M.h_plan = std::move(hitm.h_plan);
+  M.plan_pending = false;
+  bool ok = reset_plan_flags(M, Ly, ws, st);
+  apply_drop_item(M);
+  ok &= upload_plan(SG, M, at<char>(ws, Ly.plan), st);
+  return ok ? M3S_OK : M3S_ELAUNCH;
+}
+
+// Prepare a call without a host round trip: one prologue kernel on the stream
+// (ranks, task table, flags, info, dx_out; the ids to pinned memory) and the
+// registry entry; the host reads the ids later (host_finish), while the first
+// linearize runs. Large edge sets (> kProMaxE) take the synchronous prepare.
+int gn_prepare_async(const m3s_gn_args *a, hipStream_t st) {
+  const int64_t E = a->E;
+  if (E > kProMaxE || a->N > (int64_t)1 << 30 || knobs().prologue == 0) return gn_prepare_impl(a, st);
+  const Layout Ly = gn_layout(a->N, a->HW, E);
+  void *ws = a->workspace;
+  std::lock_guard<std::mutex> stage_lock(g_stage_mu);
+  Staging *SG = stage_for_device();
+  if (!SG) return M3S_ELAUNCH;
+  const int slot = acquire_slot(*SG, 64 + 2 * sizeof(int64_t) * (size_t)E);
+  if (slot < 0) return M3S_ELAUNCH;
+  DownSlot &D = SG->slots[slot];
+  ProArgs P;
+  P.ii = a->ii, P.jj = a->jj;
+  P.K = a->mode == M3S_MODE_CALIB ? a->K : nullptr;
+  P.down_K = reinterpret_cast<float *>(D.dp);
+  P.down_ii = reinterpret_cast<int64_t *>(D.dp + 64);
+  P.down_jj = P.down_ii + E;
+  P.E = (int)E, P.N = (int)a->N, P.P2 = prologue_p2(E);
+  P.flags = at<int32_t>(ws, Ly.flags), P.rank_i = at<int32_t>(ws, Ly.rank_i), P.rank_j = at<int32_t>(ws, Ly.rank_j);
+  P.eorder = at<int32_t>(ws, Ly.eorder), P.info = a->info, P.edge_cnt = at<uint32_t>(ws, Ly.edge_cnt);
+  P.dx_out = a->dx_out;
+  P.n_dx = (a->N > 1 && a->dx_out) ? (int)(7 * (a->N - 1)) : 0;
+  const size_t lds = prologue_lds(P.E, P.P2);
+  if (lds > 64 * 1024) set_lds_attributes_once();
+  gn_prologue_kernel<<<1, kProThreads, lds, st>>>(P);
+  if (launch_ok() != M3S_OK || hipEventRecord(D.ev, st) != hipSuccess) {
+    D.busy = false;
+    return M3S_ELAUNCH;
+  }
+  PlanMeta meta;
+  meta.host_pending = true, meta.slot = slot;
+  meta.has_K = a->mode == M3S_MODE_CALIB;
+  meta.force_dense = knobs().dense == 1;
+  meta.sparse = !meta.force_dense && a->N > 1;  // the expected outcome (the dense path reads partials either way)
+  meta.plan_pending = a->N > 1;
+  meta.range_b = 0, meta.range_e = E, meta.order_ok = E > 0;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  PlanMeta &M = g_reg[ws];
+  if (M.host_pending && M.slot >= 0 && M.slot < (int)SG->slots.size() && M.slot != slot)
+    SG->slots[M.slot].busy = false;  // a re-prepare of a workspace whose ids were never read
+  M = std::move(meta);
+  M.epoch = 0;
+  return M3S_OK;
 }
 
 int gn_full(const m3s_gn_args *a, int mode, void *stream) {
@@ -4134,16 +4497,10 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   if (a->mode != mode) return M3S_EINVAL;
   if (gn_layout(a->N, a->HW, a->E).ld > kMaxLd) return M3S_ETOOLARGE;
   hipStream_t st = S(stream);
-  ResidualParams P = make_params(a);
-  if ((rc = gn_prepare_impl(a, st))) return rc;
-  if (mode == M3S_MODE_CALIB) {
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    const PlanMeta &M = g_reg.at(a->workspace);
-    P.fx = M.K4[0], P.fy = M.K4[1], P.cx = M.K4[2], P.cy = M.K4[3];
-  }
+  const ResidualParams P = make_params(a);  // calib intrinsics: read by the kernels (LinArgs::Kd)
+  if ((rc = gn_prepare_async(a, st))) return rc;
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   const float *partials = at<float>(a->workspace, Ly.partials);
-  const int64_t chunks = chunks_for(a->HW, a->E);
   bool sparse;
   {
     std::lock_guard<std::mutex> g(g_reg_mu);
@@ -4151,7 +4508,8 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   }
   // sparse solve: the linearize kernels finalize each edge themselves
   for (int it = 0; it < a->max_iter; it++) {
-    if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse))) return rc;
+    int64_t chunks = 0;  // of this iteration's linearize launch (the dense path reduces its partials)
+    if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse, &chunks))) return rc;
     if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st, sparse))) return rc;
   }
   return M3S_OK;
@@ -4575,6 +4933,7 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   L.chunks = chunks_for(a->HW, 1);
   L.chunk_pix = chunk_pixels(a->HW, L.chunks);
   L.P = P;
+  L.Kd = nullptr;  // the tracker passes its intrinsics in P
   L.track = ts;  // one launch per iteration: the last chunk runs the solve
   L.info = a->info;
   L.T_WCf_out = a->T_WCf_out, L.T_CkCf_out = a->T_CkCf_out;
@@ -4666,7 +5025,7 @@ int m3s_gauss_newton_calib(const m3s_gn_args *a, void *stream) { return gn_full(
 int m3s_gn_prepare(const m3s_gn_args *a, void *stream) {
   int rc = check_args(a);
   if (rc) return rc;
-  return gn_prepare_impl(a, S(stream));
+  return gn_prepare_async(a, S(stream));
 }
 
 int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end, double *edge_sums,
@@ -4674,13 +5033,7 @@ int m3s_gn_linearize(const m3s_gn_args *a, int64_t edge_begin, int64_t edge_end,
   int rc = check_args(a);
   if (rc) return rc;
   if (edge_begin < 0 || edge_end > a->E || edge_begin > edge_end) return M3S_EINVAL;
-  ResidualParams P = make_params(a);
-  if (a->mode == M3S_MODE_CALIB) {  // intrinsics read once by m3s_gn_prepare (no sync here)
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    auto it = g_reg.find(a->workspace);
-    if (it == g_reg.end() || !it->second.has_K) return M3S_EINVAL;
-    P.fx = it->second.K4[0], P.fy = it->second.K4[1], P.cx = it->second.K4[2], P.cy = it->second.K4[3];
-  }
+  const ResidualParams P = make_params(a);  // calib intrinsics: read by the kernels (LinArgs::Kd)
   return gn_linearize_impl(a, P, edge_begin, edge_end, edge_sums, S(stream));
 }
 
@@ -4695,8 +5048,15 @@ int m3s_gn_solve(const m3s_gn_args *a, const double *edge_sums, void *stream) {
 int m3s_gn_release(const m3s_gn_args *a, void *stream) {
   if (!a || !a->workspace) return M3S_EINVAL;
   (void)stream;  // no sync: every queued upload reads pinned staging, not the entry
+  std::lock_guard<std::mutex> stage_lock(g_stage_mu);  // (lock order: staging, then registry)
   std::lock_guard<std::mutex> g(g_reg_mu);
-  g_reg.erase(a->workspace);
+  auto it = g_reg.find(a->workspace);
+  if (it == g_reg.end()) return M3S_OK;
+  if (it->second.host_pending && it->second.slot >= 0) {  // ids never read: free the slot (its
+    Staging *SG = stage_for_device();                      // event guards the reuse)
+    if (SG && it->second.slot < (int)SG->slots.size()) SG->slots[it->second.slot].busy = false;
+  }
+  g_reg.erase(it);
   return M3S_OK;
 }
 
@@ -4764,7 +5124,7 @@ int m3s_set_knob(const char *name, int value) {
     std::atomic<int> *v;
   } tab[] = {{"plan_cache", &k.plan_cache}, {"dense", &k.dense}, {"dense_tail_min", &k.dense_tail_min},
              {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc}, {"tail_mfma", &k.tail_mfma},
-             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent},
+             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent}, {"prologue", &k.prologue},
              {"debug_drop_item", &k.debug_drop_item}};
   for (const auto &t : tab)
     if (std::strcmp(t.n, name) == 0) {
@@ -4793,7 +5153,7 @@ int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n
 size_t m3s_gn_layout_debug(int64_t N, int64_t HW, int64_t E, size_t *offs) {
   const Layout L = gn_layout(N, HW, E);
   const size_t o[15] = {L.flags, L.rank_i, L.rank_j, L.first, L.partials, L.edge_sums, L.A, L.fin,
-                        L.plan,  L.Lblk,   L.Dinv,   L.tail,  L.tasks,    L.planes,    L.total};
+                        L.plan,  L.Lblk,   L.Dinv,   L.tail,  L.eorder,   L.planes,    L.total};
   if (offs) std::copy(o, o + 15, offs);
   return L.total;
 }

@@ -191,7 +191,7 @@ PLAN_SECTIONS = ("perm", "col_ptr", "col_row", "col_slot", "lev_ptr", "lev_col",
 
 
 LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums", "A", "fin",
-                   "plan", "Lblk", "Dinv", "tail", "tasks", "planes", "total")
+                   "plan", "Lblk", "Dinv", "tail", "eorder", "planes", "total")
 
 
 SIM3_OPS = {"exp": (0, 7, None, 8), "retract": (1, 7, 8, 8), "compose": (2, 8, 8, 8), "inverse": (3, 8, None, 8),

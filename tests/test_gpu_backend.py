@@ -161,6 +161,68 @@ def test_gn_global_ids_are_remapped(be):
     np.testing.assert_allclose(T_gpu, T_ref, atol=1e-4)
 
 
+@pytest.mark.parametrize("mode,N,ids", [("rays", 6, [-5, 0, 9, 1 << 40, 77, 78]), ("calib", 32, None),
+                                        ("points", 12, "spread"), ("rays", 140, "spread")])
+def test_device_prologue_matches_host_prepare_bitwise(be, knobs, mode, N, ids):
+    """The call prologue on the device (the ids ranked by a bitonic sort in LDS,
+    the task table, flags / info / dx init; gn_prepare_async) against the host
+    prepare (knob prologue = 0): poses, dx and info agree bitwise, for global
+    ids that are negative, far apart or unsorted, on the one-workgroup and the
+    chip-wide solver paths, with a cold and a cached plan."""
+    from mast3r_slam_amd import synthetic
+
+    if ids == "spread":
+        ids = sorted(np.random.default_rng(N).choice(1 << 20, size=N, replace=False).tolist())
+    H, W = (24, 32) if N < 64 else (12, 16)
+    g = synthetic.make_graph(N, H, W, seed=700 + N, kf_ids=ids)
+    Xs = constrained(g) if mode == "calib" else None
+    res = []
+    for pro in (1, 0, 1):  # the last call hits the plan cached by the first two
+        knobs("prologue", pro)
+        res.append(run_gpu(be, mode, g, 3, 0.0, Xs=Xs))
+    for T, dx, info in res[1:]:
+        np.testing.assert_array_equal(info, res[0][2])
+        np.testing.assert_array_equal(dx, res[0][1])
+        np.testing.assert_array_equal(T, res[0][0])
+    assert res[0][2][be.INFO_N_UNIQUE] == N and res[0][2][be.INFO_ITERS] == 3
+
+
+@pytest.mark.parametrize("N,ids", [(5, [40, -3, 1 << 45, 7, 8]), (32, None), (256, "spread")])
+def test_device_prologue_ranks_and_edge_order(be, N, ids):
+    """gn_prologue_kernel's outputs in the workspace after m3s_gn_prepare:
+    ranks = the sorted-unique inverse of cat(ii, jj) (gn_kernels.cu:1154-1160),
+    the edge order a permutation of the edges grouped by KF j, info's
+    N_UNIQUE, zeroed dx_out; the ids copied to the host are those passed."""
+    from mast3r_slam_amd import synthetic
+    from mast3r_slam_amd.distributed import HipOps
+
+    if ids == "spread":
+        ids = sorted(np.random.default_rng(N).choice(1 << 40, size=N, replace=False).tolist())
+    g = synthetic.make_graph(N, 8, 8, seed=800 + N, kf_ids=ids)
+    E = g.n_edges
+    ii, jj = g.ii.to(DEV).contiguous(), g.jj.to(DEV).contiguous()
+    ops = HipOps(be.MODE_RAYS, g.T_init.data.clone().to(DEV).contiguous(), g.Xs.to(DEV).contiguous(),
+                 g.Cs.to(DEV).contiguous(), ii, jj, g.idx_ii2jj.to(DEV).contiguous(),
+                 g.valid_match.to(DEV).contiguous(), g.Q.to(DEV).contiguous(), E, sigma_a=0.003, sigma_b=10.0)
+    ops.dx.fill_(7.0)
+    ops.prepare(0.0)
+    torch.cuda.synchronize()
+    lay = be.workspace_layout(N, 64, E)
+    ws = ops.ws.cpu().numpy()
+    rank_i = ws[lay["rank_i"]:lay["rank_i"] + 4 * E].view(np.int32)
+    rank_j = ws[lay["rank_j"]:lay["rank_j"] + 4 * E].view(np.int32)
+    order = ws[lay["eorder"]:lay["eorder"] + 4 * E].view(np.int32)
+    u, inv = np.unique(np.concatenate([g.ii.numpy(), g.jj.numpy()]), return_inverse=True)
+    np.testing.assert_array_equal(rank_i, inv[:E])
+    np.testing.assert_array_equal(rank_j, inv[E:])
+    np.testing.assert_array_equal(np.sort(order), np.arange(E))
+    assert np.all(np.diff(rank_j[order]) >= 0)
+    info = ops.info.cpu().numpy()
+    assert info[be.INFO_N_UNIQUE] == len(u) == N and info[be.INFO_BAD_EDGE] == 0
+    assert np.all(ops.dx.cpu().numpy() == 0)
+    ops.close()
+
+
 def test_gn_singular_system_zero_dx(be):
     """No valid residual -> LLT fails -> dx = 0, poses untouched (gn_kernels.cu:147-150)."""
     from mast3r_slam_amd import synthetic

@@ -1672,6 +1672,19 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
   }
 }
 
+#ifdef M3S_LLT_STAMPS  // per-item shader-clock stamps of sparse_llt_kernel<1> (tools/llt_stamps.py)
+__device__ int64_t g_llt_stamp[2048][4];  // per dispatch slot: ticket, inputs summed, published, fwd done
+__device__ int32_t g_llt_item[2048][2];   // item, wave
+__device__ int64_t g_llt_phase[8];        // start, assembled, factored, back-substituted, end
+#define M3S_LSTAMP(it, i) \
+  if (STORE == 1 && lane == 0 && (it) < 2048) g_llt_stamp[it][i] = (int64_t)__builtin_readcyclecounter();
+#define M3S_LPHASE(i) \
+  if (STORE == 1 && tid == 0) g_llt_phase[i] = (int64_t)__builtin_readcyclecounter();
+#else
+#define M3S_LSTAMP(it, i)
+#define M3S_LPHASE(i)
+#endif
+
 // STORE: 1 = factor, plan and flags in LDS (small graphs); 2 = factor and
 // flags in LDS, plan in global memory; 0 = factor in global memory, flags and
 // the per-wave stage areas in LDS (large graphs).
@@ -1690,16 +1703,13 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   const int m = D.m, S = D.S;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   constexpr int NW = 16;
+  M3S_LPHASE(0);
   double *Lb = IN_LDS ? smem : D.L;
   double *Di = IN_LDS ? smem + (size_t)S * 49 : D.Dinv;
   double *y = IN_LDS ? smem + (size_t)(S + m) * 49 : smem;
   int32_t *after_y = reinterpret_cast<int32_t *>(y + (size_t)m * 7);
   // index arrays: LDS copy (STORE 1) or global
-  const int32_t *pl = D.plan;
-  if (STORE == 1) {
-    for (int q = tid; q < D.plan_len; q += 1024) after_y[q] = D.plan[q];
-    pl = after_y;
-  }
+  const int32_t *pl = STORE == 1 ? after_y : D.plan;
   const int32_t *perm = pl + D.off[0], *col_ptr = pl + D.off[1], *col_row = pl + D.off[2],
                 *col_slot = pl + D.off[3], *lev_col = pl + D.off[5], *dtr_ptr = pl + D.off[6],
                 *dtr_slot = pl + D.off[7], *dtr_p = pl + D.off[8], *task_dst = pl + D.off[10],
@@ -1718,8 +1728,40 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   int32_t *pdone = done2 + m;  // PART items
   const int n_flags = S + 2 * m + D.n_parts;
   double *stg = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1)) + (size_t)wave * kStageDoubles;
+  // the plan (STORE 1) and the per-edge blocks of the in-LDS assembly, every
+  // load of both in flight at once (a loop of dependent load -> LDS store
+  // rounds cost a memory latency each: ~5 us at C3)
+  const bool asm_in = IN_LDS && D.asm_lds && phase != 2;
+  double *fl = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1));  // staged fin (asm_in)
+  {
+    const int np_ = STORE == 1 ? D.plan_len : 0, nf_ = asm_in ? D.E * kFin : 0;
+    for (int r = 0; r * 4096 < np_ || r * 8192 < nf_; r++) {
+      int32_t pv[4];
+      double fv[8];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = r * 4096 + u * 1024 + tid;
+        if (i < np_) pv[u] = D.plan[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = r * 8192 + u * 1024 + tid;
+        if (i < nf_) fv[u] = D.fin[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = r * 4096 + u * 1024 + tid;
+        if (i < np_) after_y[i] = pv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = r * 8192 + u * 1024 + tid;
+        if (i < nf_) fl[i] = fv[u];
+      }
+    }
+  }
   for (int q = tid; q < n_flags; q += 1024) sdone[q] = 0;
-  __syncthreads();  // plan copy complete
+  __syncthreads();  // plan copy and fin staging complete
   const int r = lane / 7, c = lane % 7;
   const bool act49 = lane < 49;
   // clamped row offsets: lanes >= 49 (>= 7) load valid entries and discard them
@@ -1736,10 +1778,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // in LDS with coalesced loads, then summed per slot in edge order (the sums
   // of assemble_slots_kernel); otherwise that kernel assembled into the global
   // factor array, copied in here.
-  if (IN_LDS && D.asm_lds) {
-    double *fl = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1));
-    for (int idx = tid; idx < D.E * kFin; idx += 1024) fl[idx] = D.fin[idx];
-    __syncthreads();
+  if (asm_in) {
     for (int idx = tid; idx < S * 49; idx += 1024) {
       const int sl = idx / 49, t = idx - sl * 49;
       double v = 0.0;
@@ -1763,6 +1802,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   }
   if (tid == 0) fail_s = 0, next_item = 0, next_col = 0, next_b0 = 0;
   __syncthreads();
+  M3S_LPHASE(1);
 #if defined(M3S_LLT_EXIT) && M3S_LLT_EXIT == 1  // phase-timing builds only (tools/llt_phase_ab.py)
   return;
 #endif
@@ -1781,6 +1821,10 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     const int it = wave_ticket(&next_item);
     if (it >= n_disp) break;
     const int item = witems[it];
+    M3S_LSTAMP(it, 0);
+#ifdef M3S_LLT_STAMPS
+    if (STORE == 1 && lane == 0 && it < 2048) g_llt_item[it][0] = item, g_llt_item[it][1] = wave;
+#endif
     if (item >= n_tasks) {  // PART: partial sum of the head of a long update list
       const int pi = item - n_tasks, tg = part_tgt[pi];
       const int q0 = part_q0[pi], q1 = part_q1[pi];
@@ -1805,11 +1849,13 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       double v = Lb[(size_t)k * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
+      M3S_LSTAMP(it, 1);
       double wcol[7];
       const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_LSTAMP(it, 2);
       // forward step, off the factorisation's critical path:
       // y_k = L_kk^-1 (b_k - sum_p L_kp y_p)
       double bb = y[k * 7 + lane7];
@@ -1818,6 +1864,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       fwd_solve_store(bb, wcol, scr, y + (size_t)k * 7, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&ydone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_LSTAMP(it, 3);
     } else {  // OFF: L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
       const int t2 = item;
       const int dst = task_dst[t2], k = task_col[t2];
@@ -1829,7 +1876,9 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       double v = Lb[(size_t)dst * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[tr_a[q]]) && flag_set(&sdone[tr_b[q]]), (v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, qa, qb, r7, c7, lane49, lane, stg)));
+      M3S_LSTAMP(it, 1);
       wait_flag(&sdone[k], &fail_s);  // W_k
+      M3S_LSTAMP(it, 3);
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -1839,9 +1888,11 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       wave_lds_fence();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[dst], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      M3S_LSTAMP(it, 2);
     }
   }
   __syncthreads();
+  M3S_LPHASE(2);
 #if defined(M3S_LLT_EXIT) && M3S_LLT_EXIT == 2
   return;
 #endif
@@ -2050,6 +2101,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     if (lane == 0) __hip_atomic_store(&done2[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
+  M3S_LPHASE(3);
 
   // 3. dx = -x in the original variable order, retraction, ||dx||; dx also
   // to LDS (the per-wave scratch, free now) when it fits, so the retraction
@@ -2084,6 +2136,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       D.flags[kFlagStop] = 1;
     }
   }
+  M3S_LPHASE(4);
 }
 
 // ------------------------------------- column tasks over many workgroups --
@@ -5110,6 +5163,17 @@ int m3s_debug_stamps(int which, int64_t *out) {
 #ifdef M3S_COL_STAMPS
   if (which == 1)
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_col_stamp), sizeof(g_col_stamp)) == hipSuccess ? 1 : M3S_ELAUNCH;
+#endif
+#ifdef M3S_LLT_STAMPS
+  if (which == 2) {  // [2048][4] stamps, then [2048][2] items (as int64), then [8] phases
+    int32_t items[2048][2];
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_llt_stamp), sizeof(g_llt_stamp)) != hipSuccess ||
+        hipMemcpyFromSymbol(items, HIP_SYMBOL(g_llt_item), sizeof(items)) != hipSuccess ||
+        hipMemcpyFromSymbol(out + 2048 * 4 + 2048 * 2, HIP_SYMBOL(g_llt_phase), sizeof(g_llt_phase)) != hipSuccess)
+      return M3S_ELAUNCH;
+    for (int q = 0; q < 2048; q++) out[2048 * 4 + 2 * q] = items[q][0], out[2048 * 4 + 2 * q + 1] = items[q][1];
+    return 1;
+  }
 #endif
   (void)which;
   (void)out;

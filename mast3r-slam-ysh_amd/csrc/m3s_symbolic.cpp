@@ -167,6 +167,7 @@ std::pair<int, int64_t> etree_shape(int m, const BitRows &adj, const std::vector
 constexpr double kCostDiag0 = 3500.0, kCostOff0 = 900.0, kCostUpd = 250.0;
 constexpr double kCostPart0 = 150.0, kCostPartUpd = 60.0, kCostPartIn = 120.0;
 constexpr double kCostFwd0 = 1000.0, kCostFwdUpd = 200.0, kHop = 400.0;
+constexpr double kSlack = 300.0;  // start-time tolerance of the rank choice (small plans)
 
 static void schedule_items(SparsePlan &P) {
   const int n = (int)P.items.size();
@@ -220,7 +221,6 @@ static void schedule_items(SparsePlan &P) {
     d.erase(std::unique(d.begin(), d.end()), d.end());
     for (int x : d) succ[x].push_back(it);
   }
-  (void)T;
   // upward rank: items are listed in a topological order (level order)
   std::vector<double> rank(n, 0.0);
   for (int it = n - 1; it >= 0; it--) {
@@ -242,26 +242,82 @@ static void schedule_items(SparsePlan &P) {
   // a mispredicted cost while ready work waits in another wave's queue. The
   // list is topological: every dependency of item i is dispatched before i,
   // so the lowest unfinished dispatched item can always run (progress).
+  // Small plans (the one-workgroup LDS kernel): the free wave takes the item
+  // that can START first (its inputs' predicted publish times), the highest
+  // rank among those within kSlack of it. Taking the top-rank item instead
+  // parked waves on items whose inputs were far off while ready work queued
+  // behind them in the list (C3: one OFF item waited ~14k cycles for a wave;
+  // profiles/r03/llt_stamps_r3k.txt). Large plans keep the rank heap.
   std::vector<double> free_at(kLltWaves, 0.0);
   P.witems.clear();
-  while (!ready.empty()) {
-    const int it = -ready.top().second;
-    ready.pop();
+  std::vector<int> cand;  // ready candidates (small plans)
+  std::vector<double> pub_at(n, 0.0);  // simulated publish time of each item
+  const bool est_first = n <= 1024;
+  if (est_first)
+    while (!ready.empty()) cand.push_back(-ready.top().second), ready.pop();
+  while (est_first ? !cand.empty() : !ready.empty()) {
     int w = 0;
     for (int x = 1; x < kLltWaves; x++)
       if (free_at[x] < free_at[w]) w = x;
+    int it;
+    if (est_first) {
+      double best_est = 1e300;
+      for (int c : cand) best_est = std::min(best_est, std::max(free_at[w], ready_at[c]));
+      int bi = -1;
+      for (int q = 0; q < (int)cand.size(); q++) {
+        const int c = cand[q];
+        if (std::max(free_at[w], ready_at[c]) > best_est + kSlack) continue;
+        if (bi < 0 || rank[c] > rank[cand[bi]] || (rank[c] == rank[cand[bi]] && c < cand[bi])) bi = q;
+      }
+      it = cand[bi];
+      cand[bi] = cand.back();
+      cand.pop_back();
+    } else {
+      it = -ready.top().second;
+      ready.pop();
+    }
     const double start = std::max(free_at[w], ready_at[it]);
     free_at[w] = start + cost[it];
     const double published = start + pub[it] + kHop;
+    pub_at[it] = published;
     P.witems.push_back(P.items[it]);
     for (int s2 : succ[it]) {
       ready_at[s2] = std::max(ready_at[s2], published);
-      if (--missing[s2] == 0) ready.push({rank[s2], -s2});
+      if (--missing[s2] == 0) {
+        if (est_first) cand.push_back(s2);
+        else ready.push({rank[s2], -s2});
+      }
     }
   }
   // wave_ptr = {0, n}: one dispatch list shared by all waves
   P.wave_ptr.assign(1, 0);
   P.wave_ptr.push_back((int32_t)P.witems.size());
+  if (split || !est_first) return;
+  // Update lists of the dataflow items in the order their blocks are expected
+  // to be published: the kernel applies the updates of a list as they arrive,
+  // in list order, so the block that lands last should be the last product
+  // (ascending p put it anywhere; what followed it waited for it). Dense-tail
+  // lists keep ascending p (their border prefixes, clq's bend, rely on it).
+  const int c0 = P.m - P.nc;
+  std::vector<int> idx;
+  auto reorder = [&](int q0, int q1, auto key, std::initializer_list<std::vector<int32_t> *> arrs) {
+    idx.resize(q1 - q0);
+    for (int q = q0; q < q1; q++) idx[q - q0] = q;
+    std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return key(x) < key(y); });
+    for (std::vector<int32_t> *a : arrs) {
+      std::vector<int32_t> tmp(q1 - q0);
+      for (int q = q0; q < q1; q++) tmp[q - q0] = (*a)[idx[q - q0]];
+      std::copy(tmp.begin(), tmp.end(), a->begin() + q0);
+    }
+  };
+  for (int k = 0; k < c0; k++)
+    reorder(P.dtr_ptr[k], P.dtr_ptr[k + 1], [&](int q) { return pub_at[item_of_slot[P.dtr_slot[q]]]; },
+            {&P.dtr_slot, &P.dtr_p});
+  for (int t = 0; t < T; t++)
+    if (P.task_col[t] < c0)
+      reorder(P.task_tr_ptr[t], P.task_tr_ptr[t + 1],
+              [&](int q) { return std::max(pub_at[item_of_slot[P.tr_a[q]]], pub_at[item_of_slot[P.tr_b[q]]]); },
+              {&P.tr_a, &P.tr_b});
 }
 
 void schedule_plan_items(SparsePlan &P) { schedule_items(P); }

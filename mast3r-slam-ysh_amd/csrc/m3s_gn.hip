@@ -62,6 +62,9 @@ namespace {
 #ifndef M3S_PP_LDS  // PP: operands read from the LDS slot per pixel pair
 #define M3S_PP_LDS 1
 #endif
+#ifndef M3S_PK_DEPTH  // packed linearize: trips prefetched ahead through LDS (1 or 2)
+#define M3S_PK_DEPTH 1
+#endif
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
@@ -726,29 +729,39 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   // global_load_lds_dwordx4 into the wave's own LDS slot while the wave
   // computes the current trip from registers. Lane l's 16 B land at slot +
   // 16 l (lane-linear), so every lane reads back exactly what it loaded.
-  __shared__ __attribute__((aligned(16))) f32x4 stage[kThreads / 64][NPL + 3][64];
+  // M3S_PK_DEPTH slots per wave: trip t lands in slot t % DEPTH
+  constexpr int DEPTH = M3S_PK_DEPTH;
+  __shared__ __attribute__((aligned(16))) f32x4 stage[DEPTH][kThreads / 64][NPL + 3][64];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  auto issue = [&](int64_t q) {
+  auto issue = [&](int64_t q, int sl_) {
 #pragma unroll
     for (int k = 0; k < NPL; k++)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(pl + (size_t)k * HW + q),
-                                       (__attribute__((address_space(3))) void *)(&stage[wv][k][0]),
+                                       (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]),
                                        16, 0, 1 ? 2 : 0);
 #pragma unroll
     for (int k = 0; k < 3; k++)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(Xs_j + 3 * q + 4 * k),
-                                       (__attribute__((address_space(3))) void *)(&stage[wv][NPL + k][0]),
+                                       (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]),
                                        16, 0, 0);
   };
   int64_t p0 = p_begin + kPixPerThread * threadIdx.x;
-  if (p0 < p_end) issue(p0);
-  for (; p0 < p_end; p0 += kBlockPix) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p0 < p_end) issue(p0, 0);
+  if (DEPTH > 1 && p0 + kBlockPix < p_end) issue(p0 + kBlockPix, 1 % DEPTH);
+  for (int trip = 0; p0 < p_end; p0 += kBlockPix, trip++) {
+    const int cur = DEPTH > 1 ? (trip & 1) : 0;
+    if (DEPTH > 1 && p0 + kBlockPix < p_end) {
+      // this trip's loads are done once at most the next trip's NPL + 3 are in flight
+      if constexpr (NPL == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #if M3S_PP && M3S_PP_LDS
     // each pixel pair's operands are read from the LDS slot just before its
     // math (8-B reads: 2 NPL + 6 VGPRs live instead of 4 (NPL + 3)); the slot
     // is refilled once the second pair's operands are in registers
-    const float *sl = reinterpret_cast<const float *>(&stage[wv][0][ln]);
+    const float *sl = reinterpret_cast<const float *>(&stage[cur][wv][0][ln]);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       f32x2 in[NPL], X[3];
@@ -765,7 +778,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       X[0] = f32x2{xf[0], xf[3]}, X[1] = f32x2{xf[1], xf[4]}, X[2] = f32x2{xf[2], xf[5]};
       if (h == 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
-        if (p0 + kBlockPix < p_end) issue(p0 + kBlockPix);
+        if (p0 + DEPTH * kBlockPix < p_end) issue(p0 + DEPTH * kBlockPix, cur);
       }
       f32x2 Y[3];
       act2(Tm, X, Y);
@@ -775,11 +788,11 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 #else
     f32x4 pv[NPL], xv[3];
 #pragma unroll
-    for (int k = 0; k < NPL; k++) pv[k] = stage[wv][k][ln];
+    for (int k = 0; k < NPL; k++) pv[k] = stage[cur][wv][k][ln];
 #pragma unroll
-    for (int k = 0; k < 3; k++) xv[k] = stage[wv][NPL + k][ln];
+    for (int k = 0; k < 3; k++) xv[k] = stage[cur][wv][NPL + k][ln];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
-    if (p0 + kBlockPix < p_end) issue(p0 + kBlockPix);
+    if (p0 + DEPTH * kBlockPix < p_end) issue(p0 + DEPTH * kBlockPix, cur);
     do_trip(pv, xv);
 #endif
   }
@@ -3391,6 +3404,22 @@ __device__ int block_excl_scan(int v, int *wsum, int *total) {
   return r;
 }
 
+// minimum of one int64 per thread over the block (every thread gets it)
+__device__ int64_t block_min_i64(int64_t v, int64_t *red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int64_t y = __shfl_xor(v, o, 64);
+    v = y < v ? y : v;
+  }
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  int64_t r = red[0];
+  for (int w = 1; w < nw; w++) r = red[w] < r ? red[w] : r;
+  __syncthreads();
+  return r;
+}
+
 __device__ __forceinline__ int lower_bound_i64(const int64_t *u, int n, int64_t v) {
   int lo = 0, hi = n;
   while (lo < hi) {
@@ -3404,6 +3433,7 @@ __device__ __forceinline__ int lower_bound_i64(const int64_t *u, int n, int64_t 
 __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
   extern __shared__ __attribute__((aligned(16))) int64_t pro_smem[];
   __shared__ int wsum[17];
+  __shared__ int64_t red64[16];
   const int E = A.E, P2 = A.P2, tid = threadIdx.x;
   constexpr int64_t kPad = 0x7fffffffffffffffLL;
   int64_t *keys = pro_smem, *uniq = keys + P2;
@@ -3419,32 +3449,77 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
   for (int q = tid; q <= E; q += kProThreads) A.edge_cnt[q] = 0u;
   for (int q = tid; q < A.n_dx; q += kProThreads) A.dx_out[q] = 0.0f;
   if (tid < 64) A.flags[tid] = 0;
-  __syncthreads();
-  for (int k = 2; k <= P2; k <<= 1)  // bitonic sort, ascending
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P2; i += kProThreads) {
-        const int l = i ^ j;
-        if (l > i) {
-          const int64_t x = keys[i], y = keys[l];
-          if ((x > y) == ((i & k) == 0)) keys[i] = y, keys[l] = x;
-        }
-      }
-      __syncthreads();
-    }
-  // the sorted unique ids, in order (each thread a run of <= 4 sorted keys)
-  const int seg = (P2 + kProThreads - 1) / kProThreads;
-  auto first = [&](int i) { return i < P2 && keys[i] != kPad && (i == 0 || keys[i] != keys[i - 1]); };
-  int nf = 0;
-  for (int q = 0; q < seg; q++) nf += first(tid * seg + q) ? 1 : 0;
+  // id range (keyframe ids are small non-negative integers in practice)
+  int64_t lo = kPad, hi = -kPad - 1;
+  for (int q = tid; q < 2 * E; q += kProThreads) {
+    const int64_t v = q < E ? A.ii[q] : A.jj[q - E];
+    lo = v < lo ? v : lo, hi = v > hi ? v : hi;
+  }
+  lo = block_min_i64(lo, red64), hi = -block_min_i64(-hi, red64);
+  // bitmap of 64 P2 bits in the uniq region (P2 int64), its word prefix in the keys region
   int nu = 0;
-  int at_ = block_excl_scan(nf, wsum, &nu);
-  for (int q = 0; q < seg; q++)
-    if (first(tid * seg + q)) uniq[at_++] = keys[tid * seg + q];
-  __syncthreads();
-  for (int e = tid; e < E; e += kProThreads) {
-    const int ri = lower_bound_i64(uniq, nu, A.ii[e]), rj = lower_bound_i64(uniq, nu, A.jj[e]);
-    A.rank_i[e] = ri, A.rank_j[e] = rj;
-    erj[e] = rj;
+  if (E > 0 && (uint64_t)hi - (uint64_t)lo < (uint64_t)64 * P2) {
+    // rank = number of distinct ids below: a presence bitmap over [lo, hi] and
+    // a prefix of its word popcounts (4 barriers instead of the sort's
+    // log2(P2)(log2(P2)+1)/2)
+    uint32_t *bm = reinterpret_cast<uint32_t *>(uniq);
+    int32_t *pre = reinterpret_cast<int32_t *>(keys);
+    const int nwu = (int)(((uint64_t)hi - (uint64_t)lo) >> 5) + 1;
+    for (int q = tid; q < nwu; q += kProThreads) bm[q] = 0u;
+    __syncthreads();
+    for (int q = tid; q < 2 * E; q += kProThreads) {
+      const uint64_t d = (uint64_t)(q < E ? A.ii[q] : A.jj[q - E]) - (uint64_t)lo;
+      atomicOr(&bm[d >> 5], 1u << (d & 31));
+    }
+    __syncthreads();
+    const int segw = (nwu + kProThreads - 1) / kProThreads;
+    int pc = 0;
+    for (int q = 0; q < segw; q++) {
+      const int w = tid * segw + q;
+      pc += w < nwu ? __builtin_popcount(bm[w]) : 0;
+    }
+    int off0 = block_excl_scan(pc, wsum, &nu);
+    for (int q = 0; q < segw; q++) {
+      const int w = tid * segw + q;
+      if (w < nwu) pre[w] = off0, off0 += __builtin_popcount(bm[w]);
+    }
+    __syncthreads();
+    auto rank = [&](int64_t v) {
+      const uint64_t d = (uint64_t)v - (uint64_t)lo;
+      return pre[d >> 5] + __builtin_popcount(bm[d >> 5] & ((1u << (d & 31)) - 1u));
+    };
+    for (int e = tid; e < E; e += kProThreads) {
+      const int ri = rank(A.ii[e]), rj = rank(A.jj[e]);
+      A.rank_i[e] = ri, A.rank_j[e] = rj;
+      erj[e] = rj;
+    }
+  } else {
+    __syncthreads();
+    for (int k = 2; k <= P2; k <<= 1)  // bitonic sort, ascending
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < P2; i += kProThreads) {
+          const int l = i ^ j;
+          if (l > i) {
+            const int64_t x = keys[i], y = keys[l];
+            if ((x > y) == ((i & k) == 0)) keys[i] = y, keys[l] = x;
+          }
+        }
+        __syncthreads();
+      }
+    // the sorted unique ids, in order (each thread a run of <= 4 sorted keys)
+    const int seg = (P2 + kProThreads - 1) / kProThreads;
+    auto first = [&](int i) { return i < P2 && keys[i] != kPad && (i == 0 || keys[i] != keys[i - 1]); };
+    int nf = 0;
+    for (int q = 0; q < seg; q++) nf += first(tid * seg + q) ? 1 : 0;
+    int at_ = block_excl_scan(nf, wsum, &nu);
+    for (int q = 0; q < seg; q++)
+      if (first(tid * seg + q)) uniq[at_++] = keys[tid * seg + q];
+    __syncthreads();
+    for (int e = tid; e < E; e += kProThreads) {
+      const int ri = lower_bound_i64(uniq, nu, A.ii[e]), rj = lower_bound_i64(uniq, nu, A.jj[e]);
+      A.rank_i[e] = ri, A.rank_j[e] = rj;
+      erj[e] = rj;
+    }
   }
   const bool bad = nu > A.N;
   if (tid < 8) A.info[tid] = tid == M3S_INFO_N_UNIQUE ? nu : (tid == M3S_INFO_BAD_EDGE && bad) ? 1 : 0;
@@ -3630,6 +3705,7 @@ struct PlanMeta {
   bool asm_lds = false;  // LDS factor with room for the staged fin blocks: assembly in the LLT kernel
   size_t lds_bytes = 0;
   int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0, nc = 0;
+  int nnz = 0;  // off-diagonal blocks (col_ptr[m])
   int off_dfitems = 0, n_dfitems = 0;  // df_factor_kernel dispatch list (appended to the plan image)
   PlanImage img;  // offsets (data vector cleared after upload)
   // linearize state of this solve call: edge ranks, the task table of the
@@ -3664,6 +3740,7 @@ PlanMeta solve_view(const PlanMeta &M) {
   v.m = M.m, v.S = M.S, v.levels = M.levels, v.plan_len = M.plan_len, v.n_items = M.n_items;
   v.n_tasks = M.n_tasks, v.n_parts = M.n_parts, v.nc = M.nc, v.off_dfitems = M.off_dfitems;
   v.n_dfitems = M.n_dfitems;
+  v.nnz = M.nnz;
   v.img = M.img;  // offsets (its data vector is empty in the registry)
   v.plan_pending = M.plan_pending;
   return v;
@@ -3851,6 +3928,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;
 int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st);
+void set_lds_attributes_once();
 
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
@@ -4169,6 +4247,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       meta.n_tasks = (int)P.task_dst.size();
       meta.n_parts = (int)P.part_q0.size();
       meta.nc = P.nc;
+      meta.nnz = P.col_ptr.empty() ? 0 : P.col_ptr[P.m];
       // LDS plan of sparse_llt_kernel<STORE>: flags always, factor + W + y if
       // they fit, the plan too if it fits as well; else global factor with
       // per-wave stage areas
@@ -4392,7 +4471,7 @@ int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st) {
   M.sparse = built.sparse, M.store = built.store, M.asm_lds = built.asm_lds, M.lds_bytes = built.lds_bytes;
   M.m = built.m, M.S = built.S, M.levels = built.levels, M.plan_len = built.plan_len;
   M.n_items = built.n_items, M.n_tasks = built.n_tasks, M.n_parts = built.n_parts, M.nc = built.nc;
-  M.off_dfitems = built.off_dfitems, M.n_dfitems = built.n_dfitems;
+  M.off_dfitems = built.off_dfitems, M.n_dfitems = built.n_dfitems, M.nnz = built.nnz;
   M.img = built.img;
   M.h_plan = std::move(built.h_plan);
   M.plan_pending = false;
@@ -4485,7 +4564,7 @@ int host_finish(const m3s_gn_args *a, hipStream_t st) {
   M.sparse = hitm.sparse, M.store = hitm.store, M.asm_lds = hitm.asm_lds, M.lds_bytes = hitm.lds_bytes;
   M.m = hitm.m, M.S = hitm.S, M.levels = hitm.levels, M.plan_len = hitm.plan_len;
   M.n_items = hitm.n_items, M.n_tasks = hitm.n_tasks, M.n_parts = hitm.n_parts, M.nc = hitm.nc;
-  M.off_dfitems = hitm.off_dfitems, M.n_dfitems = hitm.n_dfitems;
+  M.off_dfitems = hitm.off_dfitems, M.n_dfitems = hitm.n_dfitems, M.nnz = hitm.nnz;
   M.img = hitm.img;
   M.h_plan = std::move(hitm.h_plan);
   M.plan_pending = false;

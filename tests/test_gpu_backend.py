@@ -503,3 +503,4 @@ def test_tail_over_workgroups_matches_one_workgroup(be, N, knobs):
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)
+

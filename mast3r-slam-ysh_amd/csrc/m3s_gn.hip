@@ -2223,6 +2223,7 @@ __device__ __forceinline__ bool wait_flags(const int32_t *flag, const int32_t *i
   return true;
 }
 
+#ifdef M3S_TEST_PATHS  // the column-task factor (A/B reference of df_factor_kernel)
 __global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
   if (C.flags[kFlagStop]) return;
   __shared__ int tk_s;
@@ -2290,6 +2291,7 @@ __global__ void __launch_bounds__(256) col_factor_kernel(ColArgs C) {
   }
 }
 
+#endif  // M3S_TEST_PATHS
 // ------------------------------------ wave-level dataflow factorisation --
 // Large graphs: every block of the sparse columns' factor is its own work
 // item on one wave, dispatched over the whole chip from one ticket counter in
@@ -3365,6 +3367,7 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
 // kernel does (host_finish).
 constexpr int kProThreads = 1024;
 constexpr int kProMaxE = 2048;  // 2E ids sorted in LDS; larger edge sets take the host path
+static_assert(kProMaxE % kProThreads == 0, "prologue: whole edges per thread");
 struct ProArgs {
   const int64_t *ii, *jj;
   const float *K;      // calib: 3x3 (else null)
@@ -3439,22 +3442,30 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
   int64_t *keys = pro_smem, *uniq = keys + P2;
   int32_t *cnt = reinterpret_cast<int32_t *>(uniq + P2);  // [P2]: KF bucket counts, then offsets
   int32_t *erj = cnt + P2;  // [E]
-  for (int q = tid; q < E; q += kProThreads) {
-    const int64_t a = A.ii[q], b = A.jj[q];
-    A.down_ii[q] = a, A.down_jj[q] = b;
-    keys[q] = a, keys[E + q] = b;
+  // this thread's edges e = tid, tid + 1024 (E <= kProMaxE): their ids stay in registers
+  constexpr int kPer = kProMaxE / kProThreads;
+  int64_t ei[kPer], ej[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int e = tid + u * kProThreads;
+    ei[u] = e < E ? A.ii[e] : 0, ej[u] = e < E ? A.jj[e] : 0;
+  }
+  int64_t lo = kPad, hi = -kPad - 1;  // id range (keyframe ids: small non-negative integers in practice)
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int e = tid + u * kProThreads;
+    if (e < E) {
+      A.down_ii[e] = ei[u], A.down_jj[e] = ej[u];
+      keys[e] = ei[u], keys[E + e] = ej[u];
+      lo = ei[u] < lo ? ei[u] : lo, hi = ei[u] > hi ? ei[u] : hi;
+      lo = ej[u] < lo ? ej[u] : lo, hi = ej[u] > hi ? ej[u] : hi;
+    }
   }
   for (int q = 2 * E + tid; q < P2; q += kProThreads) keys[q] = kPad;
   if (A.K && tid < 9) A.down_K[tid] = A.K[tid];
   for (int q = tid; q <= E; q += kProThreads) A.edge_cnt[q] = 0u;
   for (int q = tid; q < A.n_dx; q += kProThreads) A.dx_out[q] = 0.0f;
   if (tid < 64) A.flags[tid] = 0;
-  // id range (keyframe ids are small non-negative integers in practice)
-  int64_t lo = kPad, hi = -kPad - 1;
-  for (int q = tid; q < 2 * E; q += kProThreads) {
-    const int64_t v = q < E ? A.ii[q] : A.jj[q - E];
-    lo = v < lo ? v : lo, hi = v > hi ? v : hi;
-  }
   lo = block_min_i64(lo, red64), hi = -block_min_i64(-hi, red64);
   // bitmap of 64 P2 bits in the uniq region (P2 int64), its word prefix in the keys region
   int nu = 0;
@@ -3467,9 +3478,13 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
     const int nwu = (int)(((uint64_t)hi - (uint64_t)lo) >> 5) + 1;
     for (int q = tid; q < nwu; q += kProThreads) bm[q] = 0u;
     __syncthreads();
-    for (int q = tid; q < 2 * E; q += kProThreads) {
-      const uint64_t d = (uint64_t)(q < E ? A.ii[q] : A.jj[q - E]) - (uint64_t)lo;
-      atomicOr(&bm[d >> 5], 1u << (d & 31));
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      if (tid + u * kProThreads < E) {
+        const uint64_t di = (uint64_t)ei[u] - (uint64_t)lo, dj = (uint64_t)ej[u] - (uint64_t)lo;
+        atomicOr(&bm[di >> 5], 1u << (di & 31));
+        atomicOr(&bm[dj >> 5], 1u << (dj & 31));
+      }
     }
     __syncthreads();
     const int segw = (nwu + kProThreads - 1) / kProThreads;
@@ -3488,10 +3503,14 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
       const uint64_t d = (uint64_t)v - (uint64_t)lo;
       return pre[d >> 5] + __builtin_popcount(bm[d >> 5] & ((1u << (d & 31)) - 1u));
     };
-    for (int e = tid; e < E; e += kProThreads) {
-      const int ri = rank(A.ii[e]), rj = rank(A.jj[e]);
-      A.rank_i[e] = ri, A.rank_j[e] = rj;
-      erj[e] = rj;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int e = tid + u * kProThreads;
+      if (e < E) {
+        const int ri = rank(ei[u]), rj = rank(ej[u]);
+        A.rank_i[e] = ri, A.rank_j[e] = rj;
+        erj[e] = rj;
+      }
     }
   } else {
     __syncthreads();
@@ -3515,10 +3534,14 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
     for (int q = 0; q < seg; q++)
       if (first(tid * seg + q)) uniq[at_++] = keys[tid * seg + q];
     __syncthreads();
-    for (int e = tid; e < E; e += kProThreads) {
-      const int ri = lower_bound_i64(uniq, nu, A.ii[e]), rj = lower_bound_i64(uniq, nu, A.jj[e]);
-      A.rank_i[e] = ri, A.rank_j[e] = rj;
-      erj[e] = rj;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int e = tid + u * kProThreads;
+      if (e < E) {
+        const int ri = lower_bound_i64(uniq, nu, ei[u]), rj = lower_bound_i64(uniq, nu, ej[u]);
+        A.rank_i[e] = ri, A.rank_j[e] = rj;
+        erj[e] = rj;
+      }
     }
   }
   const bool bad = nu > A.N;
@@ -3658,44 +3681,64 @@ __global__ void __launch_bounds__(64 * kBorderWaves) border_kernel(SparseDev D) 
 
 // Solver knobs: the measured-best defaults, overridable per process by the
 // environment (read ONCE, at the first solve) and at run time by
-// m3s_set_knob (tests and bench legs that A/B a path in one process).
+// m3s_set_knob (bench legs and tests that A/B a path in one process). The
+// product library carries the knobs of its own paths only; the A/B reference
+// paths (column-task factor, one-workgroup tail, forced dense / one-workgroup
+// solves) and the bounded-wait test hook exist in the test build
+// (-DM3S_TEST_PATHS: libm3s_gn_test.so, tests/conftest.py `test_lib`).
 struct Knobs {
   std::atomic<int> plan_cache{1};      // M3S_PLAN_CACHE: 0 = symbolic analysis every call (cold calls)
-  std::atomic<int> dense{0};           // M3S_DENSE: 1 = dense fallback LLT
   std::atomic<int> dense_tail_min{kDenseTailMin};  // M3S_DENSE_TAIL_MIN: smallest dense tail (0: never)
-  std::atomic<int> cols{1};            // M3S_COLS: 0 = large graphs on sparse_llt_kernel's one workgroup (A/B)
-  std::atomic<int> df{1};              // M3S_DF: 0 = column tasks + border_kernel instead of the dataflow (A/B)
-  std::atomic<int> tail_cyc{1};        // M3S_TAIL_CYC: 0 = the dense tail on one workgroup (A/B)
-  std::atomic<int> tail_mfma{1};       // M3S_TAIL_MFMA: 0 = the dense tail in sparse_llt_kernel (A/B)
-  std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel (A/B)
   std::atomic<int> track_persistent{1};  // M3S_TRACK_PERSISTENT: 0 = one tracker launch per iteration
   std::atomic<int> prologue{1};        // M3S_PROLOGUE: 0 = host prepare (ids read back, then the uploads)
-  std::atomic<int> debug_drop_item{-1};  // test hook only (m3s_set_knob): drop one LLT dispatch item
+#ifdef M3S_TEST_PATHS
+  std::atomic<int> dense{0};           // M3S_DENSE: 1 = dense fallback LLT
+  std::atomic<int> cols{1};            // M3S_COLS: 0 = large graphs on sparse_llt_kernel's one workgroup
+  std::atomic<int> df{1};              // M3S_DF: 0 = column tasks + border_kernel instead of the dataflow
+  std::atomic<int> tail_cyc{1};        // M3S_TAIL_CYC: 0 = the dense tail on one workgroup
+  std::atomic<int> tail_mfma{1};       // M3S_TAIL_MFMA: 0 = the dense tail in sparse_llt_kernel
+  std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel
+  std::atomic<int> debug_drop_item{-1};  // drop one LLT dispatch item (bounded-wait test)
+#endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
       if (const char *e = std::getenv(name)) v = std::atoi(e);
     };
     env("M3S_PLAN_CACHE", plan_cache);
-    env("M3S_DENSE", dense);
     env("M3S_DENSE_TAIL_MIN", dense_tail_min);
+    env("M3S_TRACK_PERSISTENT", track_persistent);
+    env("M3S_PROLOGUE", prologue);
+#ifdef M3S_TEST_PATHS
+    env("M3S_DENSE", dense);
     env("M3S_COLS", cols);
     env("M3S_DF", df);
     env("M3S_TAIL_CYC", tail_cyc);
     env("M3S_TAIL_MFMA", tail_mfma);
     env("M3S_BORDER_SPLIT", border_split);
-    env("M3S_TRACK_PERSISTENT", track_persistent);
-    env("M3S_PROLOGUE", prologue);
+#endif
   }
 };
 Knobs &knobs() {
   static Knobs k;  // thread-safe one-time initialisation
   return k;
 }
+#ifdef M3S_TEST_PATHS
 inline bool cols_path() { return knobs().cols != 0; }
 inline bool df_path() { return knobs().df != 0; }
 inline bool tail_cyc() { return knobs().tail_cyc != 0; }
 inline bool tail_mfma() { return knobs().tail_mfma != 0; }
 inline bool border_split() { return knobs().border_split != 0; }
+inline bool force_dense_knob() { return knobs().dense == 1; }
+inline int drop_item_knob() { return knobs().debug_drop_item; }
+#else
+constexpr bool cols_path() { return true; }
+constexpr bool df_path() { return true; }
+constexpr bool tail_cyc() { return true; }
+constexpr bool tail_mfma() { return true; }
+constexpr bool border_split() { return true; }
+constexpr bool force_dense_knob() { return false; }
+constexpr int drop_item_knob() { return -1; }
+#endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
 struct PlanMeta {
@@ -4053,8 +4096,10 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         const int nw = std::max(1, std::min(F.n_items, 1024));
         df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
       } else {
+#ifdef M3S_TEST_PATHS
         const int g1 = std::max(1, std::min(C.ncols, 256));
         col_factor_kernel<<<g1, 256, 0, st>>>(C);
+#endif
       }
       if (meta.nc > 0) {
         D.tail_A = tail;
@@ -4325,7 +4370,7 @@ bool upload_plan(Staging *SG, PlanMeta &M, char *dst, hipStream_t st) {
 // On the chip-wide path (global factor) the item is dropped from
 // df_factor_kernel's dispatch list instead.
 void apply_drop_item(PlanMeta &M) {
-  const int d = knobs().debug_drop_item;
+  const int d = drop_item_knob();
   if (d < 0 || !M.sparse || M.h_plan.empty()) return;
   if (M.store == 0 && M.n_dfitems > 0) {
     int32_t *di = M.h_plan.data() + M.off_dfitems;
@@ -4369,7 +4414,7 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
   std::vector<int32_t> ri, rj;
   const int nu = host_remap(hii, hjj, E, ri, rj);
   const bool bad = nu > a->N;
-  const bool force_dense = knobs().dense == 1;
+  const bool force_dense = force_dense_knob();
   PlanMeta meta;
   bool hit = false;
   if (!bad && plan_cache_enabled()) {
@@ -4610,7 +4655,7 @@ int gn_prepare_async(const m3s_gn_args *a, hipStream_t st) {
   PlanMeta meta;
   meta.host_pending = true, meta.slot = slot;
   meta.has_K = a->mode == M3S_MODE_CALIB;
-  meta.force_dense = knobs().dense == 1;
+  meta.force_dense = force_dense_knob();
   meta.sparse = !meta.force_dense && a->N > 1;  // the expected outcome (the dense path reads partials either way)
   meta.plan_pending = a->N > 1;
   meta.range_b = 0, meta.range_e = E, meta.order_ok = E > 0;
@@ -5265,10 +5310,13 @@ int m3s_set_knob(const char *name, int value) {
   const struct {
     const char *n;
     std::atomic<int> *v;
-  } tab[] = {{"plan_cache", &k.plan_cache}, {"dense", &k.dense}, {"dense_tail_min", &k.dense_tail_min},
-             {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc}, {"tail_mfma", &k.tail_mfma},
-             {"border_split", &k.border_split}, {"track_persistent", &k.track_persistent}, {"prologue", &k.prologue},
-             {"debug_drop_item", &k.debug_drop_item}};
+  } tab[] = {{"plan_cache", &k.plan_cache}, {"dense_tail_min", &k.dense_tail_min},
+             {"track_persistent", &k.track_persistent}, {"prologue", &k.prologue},
+#ifdef M3S_TEST_PATHS
+             {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
+             {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item}
+#endif
+  };
   for (const auto &t : tab)
     if (std::strcmp(t.n, name) == 0) {
       const int old = t.v->exchange(value);

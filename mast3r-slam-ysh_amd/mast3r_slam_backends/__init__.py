@@ -30,6 +30,9 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libm3s_gn.so"
 LIB_PATH = os.environ.get("M3S_LIB") or os.path.join(_HERE, LIB_NAME)  # override: experiments only
+# the same sources built with -DM3S_TEST_PATHS: the A/B reference solver paths
+# and test hooks, for the tests that compare against them (never the product)
+TEST_LIB_PATH = os.path.join(_HERE, "libm3s_gn_test.so")
 
 M3S_OK, M3S_EINVAL, M3S_ELAUNCH, M3S_ETOOLARGE = 0, 1, 2, 3
 MODE_POINTS, MODE_RAYS, MODE_CALIB = 0, 1, 2
@@ -178,6 +181,11 @@ def _load(path=LIB_PATH):
 
 
 _lib = _load()
+
+
+def load_test_library():
+    """The test build of the library (A/B reference paths, test hooks)."""
+    return _load(TEST_LIB_PATH)
 
 
 def version() -> str:

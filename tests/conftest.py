@@ -30,8 +30,21 @@ def knobs():
     saved = []
 
     def set_(name, value):
-        saved.append((name, be.set_knob(name, int(value))))
+        saved.append((be._lib, name, be.set_knob(name, int(value))))
 
     yield set_
-    for name, old in reversed(saved):
-        be.set_knob(name, old)
+    for lib, name, old in reversed(saved):  # on the library it was set on (see test_lib)
+        lib.m3s_set_knob(name.encode(), int(old))
+
+
+@pytest.fixture
+def test_lib():
+    """Run this test on the test build of the library (libm3s_gn_test.so:
+    -DM3S_TEST_PATHS, the A/B reference solver paths and the bounded-wait
+    hook); the product library is restored afterwards."""
+    import mast3r_slam_backends as be
+
+    prod = be._lib
+    be._lib = be.load_test_library()
+    yield be._lib
+    be._lib = prod

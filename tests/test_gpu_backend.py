@@ -236,7 +236,7 @@ def test_gn_singular_system_zero_dx(be):
 
 
 @pytest.mark.parametrize("N,tail", [(12, None), (140, 8)])
-def test_gn_broken_plan_times_out_as_solve_failure(be, knobs, N, tail):
+def test_gn_broken_plan_times_out_as_solve_failure(test_lib, be, knobs, N, tail):
     """A plan bug must end as a solve failure, never a hang (the LLT's flag
     waits are bounded). The debug_drop_item knob removes the first item of the
     dispatch list (a leaf DIAG): the items reading its blocks time out, the
@@ -403,7 +403,7 @@ def test_gn_tiled_cholesky_singular_zero_dx(be):
 
 
 @pytest.mark.parametrize("N,tail", [(6, "8"), (32, "8"), (70, "8"), (32, "3"), (70, "0"), (140, "8"), (256, "24")])
-def test_sparse_llt_matches_dense_llt(be, N, tail, knobs):
+def test_sparse_llt_matches_dense_llt(test_lib, be, N, tail, knobs):
     """Block-sparse LLT (default; LDS-resident for small plans, global for
     N >= 70; the top clique as a dense right-looking tail when it has at least
     M3S_DENSE_TAIL_MIN columns, 0 = never) against the dense fallback
@@ -421,7 +421,7 @@ def test_sparse_llt_matches_dense_llt(be, N, tail, knobs):
     np.testing.assert_allclose(T_s, T_d, atol=1e-5)
 
 
-def test_mfma_tail_matches_block_tail_and_is_deterministic(be, knobs):
+def test_mfma_tail_matches_block_tail_and_is_deterministic(test_lib, be, knobs):
     """Global factor with a dense tail: tail_llt_kernel (the top clique on the
     f64 MFMA, 16x16 tiles, the default) against the 7x7-block tail of
     sparse_llt_kernel (M3S_TAIL_MFMA=0) on identical inputs; the MFMA path is
@@ -465,7 +465,7 @@ def test_mfma_tail_one_step_matches_oracle(be, N):
 
 
 @pytest.mark.parametrize("N", [90, 140, 256])
-def test_block_dataflow_matches_column_tasks_bitwise(be, N, knobs):
+def test_block_dataflow_matches_column_tasks_bitwise(test_lib, be, N, knobs):
     """Large graphs: the wave-level block dataflow (df_factor_kernel, the
     default: DIAG / OFF / tail-border items over the chip) sums every block's
     update list in the same order as the column tasks + border_kernel path
@@ -483,7 +483,7 @@ def test_block_dataflow_matches_column_tasks_bitwise(be, N, knobs):
 
 
 @pytest.mark.parametrize("N", [140, 256, 400])
-def test_tail_over_workgroups_matches_one_workgroup(be, N, knobs):
+def test_tail_over_workgroups_matches_one_workgroup(test_lib, be, N, knobs):
     """The dense tail with one workgroup per tile column (tail_cyc_kernel, the
     default) applies every tile update of the factor in the single-workgroup
     kernel's order (tail_llt_kernel, M3S_TAIL_CYC=0); its back-substitution

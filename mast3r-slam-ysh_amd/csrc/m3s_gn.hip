@@ -2468,6 +2468,7 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBsCap = 40;  // L_ik blocks of a column prefetched into LDS (the rest staged)
 __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
   if (C.flags[kFlagStop]) return;
@@ -2878,7 +2879,6 @@ __device__ __forceinline__ void st_sc1_f64x4(double *p, f64x4 v) {
 // entry is one 16-B write-through store {value, epoch tag}, read back by a
 // 16-B sc1 buffer load; the consumer checks the tags, so there is no flag, no
 // producer drain and no second round trip (flag, then payload).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct GranTile {
   u32x4 v[4];
 };
@@ -3407,20 +3407,20 @@ __device__ int block_excl_scan(int v, int *wsum, int *total) {
   return r;
 }
 
-// minimum of one int64 per thread over the block (every thread gets it)
-__device__ int64_t block_min_i64(int64_t v, int64_t *red) {
+// minimum and maximum of one int64 pair per thread over the block (every
+// thread gets both)
+__device__ void block_minmax_i64(int64_t &lo, int64_t &hi, int64_t *red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
-    const int64_t y = __shfl_xor(v, o, 64);
-    v = y < v ? y : v;
+    const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+    lo = a < lo ? a : lo, hi = b > hi ? b : hi;
   }
-  if (lane == 0) red[wave] = v;
+  if (lane == 0) red[wave] = lo, red[16 + wave] = hi;
   __syncthreads();
-  int64_t r = red[0];
-  for (int w = 1; w < nw; w++) r = red[w] < r ? red[w] : r;
+  lo = red[0], hi = red[16];
+  for (int w = 1; w < nw; w++) lo = red[w] < lo ? red[w] : lo, hi = red[16 + w] > hi ? red[16 + w] : hi;
   __syncthreads();
-  return r;
 }
 
 __device__ __forceinline__ int lower_bound_i64(const int64_t *u, int n, int64_t v) {
@@ -3436,7 +3436,7 @@ __device__ __forceinline__ int lower_bound_i64(const int64_t *u, int n, int64_t 
 __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
   extern __shared__ __attribute__((aligned(16))) int64_t pro_smem[];
   __shared__ int wsum[17];
-  __shared__ int64_t red64[16];
+  __shared__ int64_t red64[32];
   const int E = A.E, P2 = A.P2, tid = threadIdx.x;
   constexpr int64_t kPad = 0x7fffffffffffffffLL;
   int64_t *keys = pro_smem, *uniq = keys + P2;
@@ -3466,7 +3466,7 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
   for (int q = tid; q <= E; q += kProThreads) A.edge_cnt[q] = 0u;
   for (int q = tid; q < A.n_dx; q += kProThreads) A.dx_out[q] = 0.0f;
   if (tid < 64) A.flags[tid] = 0;
-  lo = block_min_i64(lo, red64), hi = -block_min_i64(-hi, red64);
+  block_minmax_i64(lo, hi, red64);  // threads without edges hold (max, min): neutral
   // bitmap of 64 P2 bits in the uniq region (P2 int64), its word prefix in the keys region
   int nu = 0;
   if (E > 0 && (uint64_t)hi - (uint64_t)lo < (uint64_t)64 * P2) {

@@ -651,8 +651,10 @@ struct AccumPP {
 #pragma unroll
     for (int k = 0; k < kNP; k++) acc[k] += s[k].x + s[k].y;
   }
-  // one residual row (non-zero columns M, a[p] = the p-th entry) of both pixels
-  template <unsigned M, int K>
+  // one residual row (non-zero columns M, a[p] = the p-th entry) of both pixels;
+  // COST false: no cost sum (the backend's solve never reads it; the tracker's
+  // convergence rule does)
+  template <unsigned M, int K, bool COST = true>
   __device__ __forceinline__ void add(const f32x2 (&a)[K], f32x2 w, f32x2 e) {
     f32x2 wa[K];
 #pragma unroll
@@ -667,7 +669,7 @@ struct AccumPP {
     const f32x2 we = w * e;
 #pragma unroll
     for (int p = 0; p < K; p++) s[kG + nth_col(M, p)] = __builtin_elementwise_fma(we, a[p], s[kG + nth_col(M, p)]);
-    s[kCost] = __builtin_elementwise_fma(we, e, s[kCost]);
+    if (COST) s[kCost] = __builtin_elementwise_fma(we, e, s[kCost]);
   }
 };
 
@@ -699,8 +701,12 @@ __device__ __forceinline__ void act2(const Sim3Mat &M, const f32x2 (&X)[3], f32x
                 fma2(splat2(M.m[3 * r + 1]), X[1], fma2(splat2(M.m[3 * r + 2]), X[2], splat2(M.t[r]))));
 }
 
-// pixel_contrib for two pixels: in[k] = plane k of both, Y = T_ij Xj of both
-template <int MODE, int NPL>
+// pixel_contrib for two pixels: in[k] = plane k of both, Y = T_ij Xj of both.
+// COST false (the backend's packed iterations): no cost sum, and the calib
+// model takes 1/z and log z of max(z, z_floor) instead of selecting them away
+// when z <= z_eps (that pixel's weight is 0 either way; both stay finite), and
+// forms log z_j - log z_i as one fma on log2 z_j
+template <int MODE, int NPL, bool COST = true>
 __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParams &P, const f32x2 (&in)[NPL],
                                                const f32x2 (&Y)[3]) {
   if constexpr (MODE == 1) {  // rays + distance  (ray_align_kernel :924-1089)
@@ -714,11 +720,20 @@ __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParam
     const f32x2 swr = in[3] * P.inv_sig_a, swd = in[3] * P.inv_sig_b;
     const f32x2 kr = swr * swr, kd = swd * swd;
     const f32x2 hk = splat2(P.huber_k);
-    // huber(sw e) sw^2 = min(1, k / |sw e|) sw^2
-    const f32x2 w0 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e0))) * kr;
-    const f32x2 w1 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e1))) * kr;
-    const f32x2 w2 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e2))) * kr;
-    const f32x2 w3 = min2(splat2(1.0f), hk * rcp2(abs2(swd * e3))) * kd;
+    // huber(sw e) sw^2 = min(1, k / |sw e|) sw^2 (= sw min(sw, k / |e|): one
+    // product fewer, the packed backend iterations)
+    f32x2 w0, w1, w2, w3;
+    if (COST) {
+      w0 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e0))) * kr;
+      w1 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e1))) * kr;
+      w2 = min2(splat2(1.0f), hk * rcp2(abs2(swr * e2))) * kr;
+      w3 = min2(splat2(1.0f), hk * rcp2(abs2(swd * e3))) * kd;
+    } else {
+      w0 = swr * min2(swr, hk * rcp2(abs2(e0)));
+      w1 = swr * min2(swr, hk * rcp2(abs2(e1)));
+      w2 = swr * min2(swr, hk * rcp2(abs2(e2)));
+      w3 = swd * min2(swd, hk * rcp2(abs2(e3)));
+    }
     // d r / d P = (I - r r^T) / |P|
     const f32x2 rxi = rx * inj, ryi = ry * inj, rzi = rz * inj;
     const f32x2 dxx = inj - rx * rxi, dyy = inj - ry * ryi, dzz = inj - rz * rzi;
@@ -727,22 +742,32 @@ __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParam
     const f32x2 ay[5] = {dxy, dyy, dyz, -rz, rx};  // kRayY: tau0 tau1 tau2 phi0 phi2
     const f32x2 az[5] = {dxz, dyz, dzz, ry, -rx};  // kRayZ: tau0 tau1 tau2 phi0 phi1
     const f32x2 ad[4] = {rx, ry, rz, nj};          // kRayD: tau0 tau1 tau2 sigma
-    acc.add<kRayX, 5>(ax, w0, e0);
+    acc.add<kRayX, 5, COST>(ax, w0, e0);
     M3S_ROW_BARRIER();
-    acc.add<kRayY, 5>(ay, w1, e1);
+    acc.add<kRayY, 5, COST>(ay, w1, e1);
     M3S_ROW_BARRIER();
-    acc.add<kRayZ, 5>(az, w2, e2);
+    acc.add<kRayZ, 5, COST>(az, w2, e2);
     M3S_ROW_BARRIER();
-    acc.add<kRayD, 4>(ad, w3, e3);
+    acc.add<kRayD, 4, COST>(ad, w3, e3);
     M3S_ROW_BARRIER();
   } else if constexpr (MODE == 2) {  // pinhole pixel + log-depth (calib_proj_kernel :1360-1495)
     // focal-normalised u / v rows as in pixel_contrib
     const bool vzx = Y[2].x > P.z_eps, vzy = Y[2].y > P.z_eps;
-    const f32x2 zr = rcp2(Y[2]);
-    const f32x2 lj = f32x2{flog(Y[2].x), flog(Y[2].y)};
     const f32x2 zero2 = splat2(0.0f);
-    const f32x2 zinv = sel2(vzx, vzy, zr, zero2);
-    const f32x2 e2 = sel2(vzx, vzy, lj - in[2], zero2);
+    f32x2 zinv, e2;
+    if (COST) {
+      const f32x2 zr = rcp2(Y[2]);
+      const f32x2 lj = f32x2{flog(Y[2].x), flog(Y[2].y)};
+      zinv = sel2(vzx, vzy, zr, zero2);
+      e2 = sel2(vzx, vzy, lj - in[2], zero2);
+    } else {
+      // z_floor = max(z_eps, FLT_MIN): z > z_eps leaves z unchanged
+      const float zf = fmaxf(P.z_eps, 1.17549435e-38f);
+      const f32x2 zc = {fmaxf(Y[2].x, zf), fmaxf(Y[2].y, zf)};
+      zinv = rcp2(zc);
+      const f32x2 l2 = {__builtin_amdgcn_logf(zc.x), __builtin_amdgcn_logf(zc.y)};
+      e2 = fma2(l2, splat2(0.693147180559945309f), -in[2]);
+    }
     const int ux = __float_as_int(in[0].x), uy = __float_as_int(in[0].y);
     const f32x2 tu = {(float)(ux & 0xffff), (float)(uy & 0xffff)};
     const f32x2 tv = {(float)(ux >> 16), (float)(uy >> 16)};
@@ -755,38 +780,52 @@ __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParam
     const f32x2 etu = (u - tu) * (1.0f / P.fx), etv = (v - tv) * (1.0f / P.fy);
     const f32x2 swu = sq * (P.inv_sig_a * P.fx), swv = sq * (P.inv_sig_a * P.fy);
     const f32x2 hk = splat2(P.huber_k);
-    const f32x2 Wu = min2(swu * swu, (swu * hk) * rcp2(abs2(etu)));
-    const f32x2 Wv = min2(swv * swv, (swv * hk) * rcp2(abs2(etv)));
     const f32x2 swz = sq * P.inv_sig_b;
-    const f32x2 Wz = min2(swz * swz, (swz * hk) * rcp2(abs2(e2)));
+    f32x2 Wu, Wv, Wz;
+    if (COST) {
+      Wu = min2(swu * swu, (swu * hk) * rcp2(abs2(etu)));
+      Wv = min2(swv * swv, (swv * hk) * rcp2(abs2(etv)));
+      Wz = min2(swz * swz, (swz * hk) * rcp2(abs2(e2)));
+    } else {  // the same weights as sw min(sw, k / |e|): two products instead of three
+      Wu = swu * min2(swu, hk * rcp2(abs2(etu)));
+      Wv = swv * min2(swv, hk * rcp2(abs2(etv)));
+      Wz = swz * min2(swz, hk * rcp2(abs2(e2)));
+    }
     const f32x2 xyp = x * y;
     const f32x2 one = splat2(1.0f);
     const f32x2 au[5] = {zinv, -(x * zinv), -xyp, fma2(x, x, one), -y};  // kCalU: 0 2 3 4 5
     const f32x2 av[5] = {zinv, -(y * zinv), -fma2(y, y, one), xyp, x};  // kCalV: 1 2 3 4 5
     const f32x2 az[4] = {zinv, y, -x, one};                              // kCalZ: 2 3 4 6
-    acc.add<kCalU, 5>(au, Wu, etu);
+    acc.add<kCalU, 5, COST>(au, Wu, etu);
     M3S_ROW_BARRIER();
-    acc.add<kCalV, 5>(av, Wv, etv);
+    acc.add<kCalV, 5, COST>(av, Wv, etv);
     M3S_ROW_BARRIER();
-    acc.add<kCalZ, 4>(az, Wz, e2);
+    acc.add<kCalZ, 4, COST>(az, Wz, e2);
     M3S_ROW_BARRIER();
   } else {  // 3D point (point_align_kernel :564-674)
     const f32x2 e0 = Y[0] - in[0], e1 = Y[1] - in[1], e2 = Y[2] - in[2];
     const f32x2 sw = in[3] * P.inv_sig_a;
     const f32x2 k2 = sw * sw;
     const f32x2 hk = splat2(P.huber_k);
-    const f32x2 w0 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e0))) * k2;
-    const f32x2 w1 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e1))) * k2;
-    const f32x2 w2 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e2))) * k2;
+    f32x2 w0, w1, w2;
+    if (COST) {
+      w0 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e0))) * k2;
+      w1 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e1))) * k2;
+      w2 = min2(splat2(1.0f), hk * rcp2(abs2(sw * e2))) * k2;
+    } else {
+      w0 = sw * min2(sw, hk * rcp2(abs2(e0)));
+      w1 = sw * min2(sw, hk * rcp2(abs2(e1)));
+      w2 = sw * min2(sw, hk * rcp2(abs2(e2)));
+    }
     const f32x2 one = splat2(1.0f);
     const f32x2 ax[4] = {one, Y[2], -Y[1], Y[0]};  // kPtX: 0 4 5 6
     const f32x2 ay[4] = {one, -Y[2], Y[0], Y[1]};  // kPtY: 1 3 5 6
     const f32x2 az[4] = {one, Y[1], -Y[0], Y[2]};  // kPtZ: 2 3 4 6
-    acc.add<kPtX, 4>(ax, w0, e0);
+    acc.add<kPtX, 4, COST>(ax, w0, e0);
     M3S_ROW_BARRIER();
-    acc.add<kPtY, 4>(ay, w1, e1);
+    acc.add<kPtY, 4, COST>(ay, w1, e1);
     M3S_ROW_BARRIER();
-    acc.add<kPtZ, 4>(az, w2, e2);
+    acc.add<kPtZ, 4, COST>(az, w2, e2);
     M3S_ROW_BARRIER();
   }
 }

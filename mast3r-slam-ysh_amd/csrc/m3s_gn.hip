@@ -62,6 +62,12 @@ namespace {
 #ifndef M3S_PP_LDS  // PP: operands read from the LDS slot per pixel pair
 #define M3S_PP_LDS 1
 #endif
+#ifndef M3S_PK_PAIRBAR  // packed linearize: no scheduling across the two pixel pairs of a trip
+#define M3S_PK_PAIRBAR 0
+#endif
+#ifndef M3S_PK_XASM  // packed linearize: Xj floats read one by one into their pair halves
+#define M3S_PK_XASM 1
+#endif
 #ifndef M3S_PK_DEPTH  // packed linearize: trips prefetched ahead through LDS (1 or 2)
 #define M3S_PK_DEPTH 1
 #endif
@@ -642,6 +648,34 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
 // keyframe, which the task table places on one XCD back to back). No gathers.
 // calib / points fit 128 VGPRs (4 waves per SIMD); rays keeps 84 accumulator
 // VGPRs and is left unbounded (164, 3 waves)
+// 16 B per lane from a buffer resource straight into LDS (lane-linear at
+// m0 = lds): wave-uniform soffset, per-lane voffset (nt: streamed once)
+__device__ __forceinline__ void buf_lds16_nt(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
+                                             int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 16, voff, soff, 0, 2);
+}
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
+                                          int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 16, voff, soff, 0, 0);
+}
+// Xj floats 6h .. 6h + 5 of a lane's 12 (its 4 pixels x y z, interleaved over
+// three 16-B LDS rows 1 KB apart, from xs), one ds_read_b32 each straight
+// into the half of the pair that uses it: plain loads merge into 16-B reads
+// whose halves then need 5 v_mov per pair to regroup by pixel. LDS reads
+// complete in order, so the compiler's own counted waits stay correct; ours
+// is explicit.
+__device__ __forceinline__ void lds_xj6(const float *xs, int h, float (&xf)[6]) {
+  const uint32_t xa = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const float *)xs);
+#define M3S_XRD(q_, f_) \
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(xf[q_]) : "v"(xa), "i"(4 * (256 * ((f_) >> 2) + ((f_) & 3))))
+  if (h == 0) {
+    M3S_XRD(0, 0); M3S_XRD(1, 1); M3S_XRD(2, 2); M3S_XRD(3, 3); M3S_XRD(4, 4); M3S_XRD(5, 5);
+  } else {
+    M3S_XRD(0, 6); M3S_XRD(1, 7); M3S_XRD(2, 8); M3S_XRD(3, 9); M3S_XRD(4, 10); M3S_XRD(5, 11);
+  }
+#undef M3S_XRD
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xf[0]), "+v"(xf[1]), "+v"(xf[2]), "+v"(xf[3]), "+v"(xf[4]), "+v"(xf[5]));
+}
 #ifndef M3S_PK_WAVES  // packed linearize: minimum waves per SIMD (register bound 512 / w)
 #define M3S_PK_WAVES (M3S_PP ? 3 : 4)
 #endif
@@ -693,7 +727,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].x, pv[k].y};
       f32x2 Y[3];
       act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL>(acc, P, in, Y);
+      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
     }
     __builtin_amdgcn_sched_barrier(0);
     {
@@ -703,7 +737,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].z, pv[k].w};
       f32x2 Y[3];
       act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL>(acc, P, in, Y);
+      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -726,37 +760,52 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 #endif
   // Prefetch one trip ahead through LDS with no VGPR cost: each wave's next
   // trip (NPL plane vectors + 3 Xj vectors, 16 B per lane each) is loaded by
-  // global_load_lds_dwordx4 into the wave's own LDS slot while the wave
+  // buffer_load_dwordx4 ... lds into the wave's own LDS slot while the wave
   // computes the current trip from registers. Lane l's 16 B land at slot +
   // 16 l (lane-linear), so every lane reads back exactly what it loaded.
+  // Round 3: buffer loads with wave-uniform soffsets (the trip's first pixel)
+  // and per-lane voffsets fixed for the whole kernel, and the LDS slot (m0)
+  // from a wave-uniform wave index: no per-load VALU address arithmetic
+  // (17 VALU per trip before). One resource per plane, sized HW floats.
   // M3S_PK_DEPTH slots per wave: trip t lands in slot t % DEPTH
   constexpr int DEPTH = M3S_PK_DEPTH;
   __shared__ __attribute__((aligned(16))) f32x4 stage[DEPTH][kThreads / 64][NPL + 3][64];
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  auto issue = [&](int64_t q, int sl_) {
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), ln = threadIdx.x & 63;
+  __amdgpu_buffer_rsrc_t Rp[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; k++)
+    Rp[k] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pl + (size_t)k * HW), 0, (int)(4 * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t Rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_j), 0, (int)(12 * HW), 0x00020000);
+  const int vo_p = 16 * ln, vo_x = 48 * ln;
+  // pw: the wave's first pixel of a trip (wave-uniform); lane pixels pw + 4 ln
+  auto issue = [&](int pw, int sl_) {
+#if defined(M3S_PK_FLOOR) && M3S_PK_FLOOR == 2  // compute floor (A/B only): no loads
+    return;
+#endif
 #pragma unroll
     for (int k = 0; k < NPL; k++)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(pl + (size_t)k * HW + q),
-                                       (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]),
-                                       16, 0, 1 ? 2 : 0);
+      buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vo_p, 4 * pw);
 #pragma unroll
     for (int k = 0; k < 3; k++)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(Xs_j + 3 * q + 4 * k),
-                                       (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]),
-                                       16, 0, 0);
+      buf_lds16(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vo_x, 12 * pw + 16 * k);
   };
-  int64_t p0 = p_begin + kPixPerThread * threadIdx.x;
-  if (p0 < p_end) issue(p0, 0);
-  if (DEPTH > 1 && p0 + kBlockPix < p_end) issue(p0 + kBlockPix, 1 % DEPTH);
-  for (int trip = 0; p0 < p_end; p0 += kBlockPix, trip++) {
+  const int pend = (int)p_end;
+  int pw = (int)p_begin + kPixPerThread * 64 * wv;
+  if (pw < pend) issue(pw, 0);
+  if (DEPTH > 1 && pw + kBlockPix < pend) issue(pw + kBlockPix, 1 % DEPTH);
+  for (int trip = 0; pw < pend; pw += kBlockPix, trip++) {
     const int cur = DEPTH > 1 ? (trip & 1) : 0;
-    if (DEPTH > 1 && p0 + kBlockPix < p_end) {
+    if (DEPTH > 1 && pw + kBlockPix < pend) {
       // this trip's loads are done once at most the next trip's NPL + 3 are in flight
       if constexpr (NPL == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    // lanes past the chunk's end (a partial last trip only) read back zeros
+    // from the resources and take no part (their exec bit is off)
+    if (pw + kPixPerThread * ln >= pend) continue;
 #if M3S_PP && M3S_PP_LDS
     // each pixel pair's operands are read from the LDS slot just before its
     // math (8-B reads: 2 NPL + 6 VGPRs live instead of 4 (NPL + 3)); the slot
@@ -770,20 +819,30 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       // Xj of pixels 2h, 2h + 1: floats 6h .. 6h + 5 of the lane's 12
       const float *xs = sl + 256 * NPL;
       float xf[6];
+#if M3S_PK_XASM
+      lds_xj6(xs, h, xf);
+#else
 #pragma unroll
       for (int q = 0; q < 6; q++) {
         const int f = 6 * h + q;
         xf[q] = xs[256 * (f >> 2) + (f & 3)];
       }
+#endif
       X[0] = f32x2{xf[0], xf[3]}, X[1] = f32x2{xf[1], xf[4]}, X[2] = f32x2{xf[2], xf[5]};
       if (h == 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
-        if (p0 + DEPTH * kBlockPix < p_end) issue(p0 + DEPTH * kBlockPix, cur);
+        if (pw + DEPTH * kBlockPix < pend) issue(pw + DEPTH * kBlockPix, cur);
       }
+#if defined(M3S_PK_FLOOR) && M3S_PK_FLOOR == 1  // memory floor (A/B only): no math
+      sink += in[0].x + in[NPL - 1].y + X[0].x + X[2].y;
+#else
       f32x2 Y[3];
       act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL>(acc, P, in, Y);
+      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
+#endif
+#if M3S_PK_PAIRBAR
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 #else
     f32x4 pv[NPL], xv[3];
@@ -792,7 +851,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 #pragma unroll
     for (int k = 0; k < 3; k++) xv[k] = stage[cur][wv][NPL + k][ln];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
-    if (p0 + DEPTH * kBlockPix < p_end) issue(p0 + DEPTH * kBlockPix, cur);
+    if (pw + DEPTH * kBlockPix < pend) issue(pw + DEPTH * kBlockPix, cur);
     do_trip(pv, xv);
 #endif
   }

@@ -50,6 +50,7 @@ using namespace m3s;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef long long i64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -860,6 +861,180 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
   acc.fold(sums);
   sums[0] += sink;
+  store_partial(sums, A.partials + (size_t)b * kNP);
+  if (A.edge_cnt) edge_tail(A, e_loc, e);
+}
+
+// ------------------------------------------ pipelined gathering launch --
+// The first GN iteration of a backend call (round 3). Per trip a lane takes 4
+// pixels; the wave's streamed inputs of the NEXT trip (valid, Q, idx of the
+// edge; Xj, Cj of KF j) go by buffer_load ... lds into the wave's LDS slot
+// while this trip runs, so only the dependent gathers of KF i (z_i or X_i, and
+// C_i, through idx) are exposed per trip, not the stream latency before them.
+// Order per trip: read the slot (inline-asm LDS reads: the compiler adds no
+// vmcnt wait for the DMA), issue the gathers, then the next trip's refill
+// (vmcnt is in order: waiting for the gathers then leaves the refill in
+// flight), the pose-only math, the rest, the plane stores. Same arithmetic per
+// pixel as linearize_kernel<MODE, false, true, true> (gather_pixel +
+// make_pixin + pixel_contrib): bitwise the same planes, partials and sums.
+#ifndef M3S_GATHER_LDS  // pipelined gathering launch (0: linearize_kernel's VGPR-staged loop)
+#define M3S_GATHER_LDS 1
+#endif
+// per-wave slot (bytes): valid u8x4 | Q | idx (int64: two 1-KB rows; int32: one) | Xj (3 rows) | Cj
+constexpr int kGsValid = 0, kGsQ = 256, kGsIdx = 1280, kGsXj = 3328, kGsCj = 6400, kGsBytes = 7424;
+__device__ __forceinline__ void buf_lds4_nt(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
+                                            int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 4, voff, soff, 0, 2);
+}
+struct GSlot {
+  uint32_t vb;
+  f32x4 q, x0, x1, x2, c;
+  u32x4 i0, i1;
+};
+// one lane's trip out of the slot: a = slot + 16 lane, av = slot + 4 lane
+__device__ __forceinline__ void gslot_read(uint32_t a, uint32_t av, bool i64, GSlot &g) {
+  asm volatile("ds_read_b32 %0, %1 offset:0" : "=v"(g.vb) : "v"(av));
+  asm volatile("ds_read_b128 %0, %1 offset:256" : "=v"(g.q) : "v"(a));
+  asm volatile("ds_read_b128 %0, %1 offset:1280" : "=v"(g.i0) : "v"(a));
+  if (i64) asm volatile("ds_read_b128 %0, %1 offset:2304" : "=v"(g.i1) : "v"(a));
+  asm volatile("ds_read_b128 %0, %1 offset:3328" : "=v"(g.x0) : "v"(a));
+  asm volatile("ds_read_b128 %0, %1 offset:4352" : "=v"(g.x1) : "v"(a));
+  asm volatile("ds_read_b128 %0, %1 offset:5376" : "=v"(g.x2) : "v"(a));
+  asm volatile("ds_read_b128 %0, %1 offset:6400" : "=v"(g.c) : "v"(a));
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(g.vb), "+v"(g.q), "+v"(g.i0), "+v"(g.i1), "+v"(g.x0), "+v"(g.x1), "+v"(g.x2), "+v"(g.c));
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
+  if (*A.stop) return;
+  const int64_t b = block_task(A);
+  if (b < 0) return;
+  const int64_t e_loc = b / A.chunks;
+  const int64_t c = b - e_loc * A.chunks;
+  const int64_t e = A.edge_begin + e_loc;
+  const int64_t HW = A.HW;
+  const ResidualParams P = kparams(A);
+  const int ri = A.rank_i[e], rj = A.rank_j[e];
+  const Sim3Mat Tm = sim3_matrix(relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj)));
+  const float *Xs_i = A.Xs + (size_t)ri * HW * 3, *Xs_j = A.Xs + (size_t)rj * HW * 3;
+  const float *Cs_i = A.Cs + (size_t)ri * HW, *Cs_j = A.Cs + (size_t)rj * HW;
+  const size_t eoff = (size_t)e_loc * HW;
+  constexpr int NPL = PixIn<MODE>::kPlanes;
+  float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
+  const bool i64 = A.idx32 == 0;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), ln = threadIdx.x & 63;
+  // streams (ranges: reads past the end return zeros) and the gather sources
+  const __amdgpu_buffer_rsrc_t Rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(A.valid + eoff), 0, (int)HW, 0x00020000);
+  const __amdgpu_buffer_rsrc_t Rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(A.Q + eoff), 0, (int)(4 * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t Ri = __builtin_amdgcn_make_buffer_rsrc(
+      i64 ? (void *)(A.idx + eoff) : (void *)(reinterpret_cast<const int32_t *>(A.idx) + eoff), 0,
+      (int)((i64 ? 8 : 4) * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t Rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_j), 0, (int)(12 * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t Rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Cs_j), 0, (int)(4 * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t RXi = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_i), 0, (int)(12 * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t RCi = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Cs_i), 0, (int)(4 * HW), 0x00020000);
+  __shared__ __attribute__((aligned(16))) uint8_t gstage[kThreads / 64][kGsBytes];
+  uint8_t *slot = gstage[wv];
+  auto L3 = [&](int off) { return (__attribute__((address_space(3))) void *)(slot + off); };
+  // per-lane offsets; kFar (past every resource's range) reads zeros without a
+  // memory access: the refill is issued unconditionally (a fixed count of 8
+  // loads per trip, so the compiler's counted waits for the gathers behind it
+  // stay exact), with kFar when there is no next trip and for the second idx
+  // row of int32 ids
+  constexpr int kFar = 0x7fff0000;
+  const int v4 = 4 * ln, v16 = 16 * ln, v48 = 48 * ln, vi0 = (i64 ? 32 : 16) * ln, vi1 = i64 ? 32 * ln + 16 : kFar;
+  auto issue = [&](int pw, bool far) {  // pw: the wave's first pixel of the trip
+    buf_lds4_nt(Rv, L3(kGsValid), far ? kFar : v4, pw);
+    buf_lds16_nt(Rq, L3(kGsQ), far ? kFar : v16, 4 * pw);
+    buf_lds16_nt(Ri, L3(kGsIdx), far ? kFar : vi0, (i64 ? 8 : 4) * pw);
+    buf_lds16_nt(Ri, L3(kGsIdx + 1024), far ? kFar : vi1, 8 * pw);
+#pragma unroll
+    for (int k = 0; k < 3; k++) buf_lds16(Rx, L3(kGsXj + 1024 * k), far ? kFar : v48, 12 * pw + 16 * k);
+    buf_lds16(Rc, L3(kGsCj), far ? kFar : v16, 4 * pw);
+  };
+  const uint32_t sa = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t *)slot);
+  const uint32_t a16 = sa + 16 * ln, a4 = sa + 4 * ln;
+
+  AccumFlat acc;
+  acc.zero();
+  const int64_t p_begin = c * A.chunk_pix;
+  const int pend = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
+  int pw = (int)p_begin + kPixPerThread * 64 * wv;
+  if (pw < pend) issue(pw, false);
+  for (int trip = 0; pw < pend; pw += kBlockPix, trip++) {
+    // the slot's DMA is done once only the previous trip's NPL plane stores
+    // may still be in flight behind it (stores count in vmcnt, in issue
+    // order); the first trip has no stores behind its loads
+    if (trip == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (NPL == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    const int p0 = pw + kPixPerThread * ln;
+    if (p0 >= pend) continue;  // a partial last trip: lanes past the end take no part
+    GSlot g;
+    gslot_read(a16, a4, i64, g);
+    int64_t ids[4];
+    if (i64) {
+      ids[0] = (int64_t)(((uint64_t)g.i0.y << 32) | g.i0.x), ids[1] = (int64_t)(((uint64_t)g.i0.w << 32) | g.i0.z);
+      ids[2] = (int64_t)(((uint64_t)g.i1.y << 32) | g.i1.x), ids[3] = (int64_t)(((uint64_t)g.i1.w << 32) | g.i1.z);
+    } else {
+      ids[0] = (int32_t)g.i0.x, ids[1] = (int32_t)g.i0.y, ids[2] = (int32_t)g.i0.z, ids[3] = (int32_t)g.i0.w;
+    }
+    // the gathers of this trip (gather_pixel's: id = valid ? idx : 0)
+    bool vm[4];
+    int id[4];
+    float gx[4][3], gc[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) {
+      vm[s4] = ((g.vb >> (8 * s4)) & 0xffu) != 0;
+      id[s4] = vm[s4] ? (int)ids[s4] : 0;
+      if (MODE == M3S_MODE_CALIB) {
+        gx[s4][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, 12 * id[s4] + 8, 0, 0));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+          gx[s4][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, 12 * id[s4] + 4 * k, 0, 0));
+      }
+      gc[s4] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RCi, 4 * id[s4], 0, 0));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the gathers go out before the refill
+    issue(pw + kBlockPix, pw + kBlockPix >= pend);
+    __builtin_amdgcn_sched_barrier(0);
+    const float Xj[4][3] = {{g.x0.x, g.x0.y, g.x0.z}, {g.x0.w, g.x1.x, g.x1.y}, {g.x1.z, g.x1.w, g.x2.x},
+                            {g.x2.y, g.x2.z, g.x2.w}};
+    const float qs[4] = {g.q.x, g.q.y, g.q.z, g.q.w};
+    const float cjs[4] = {g.c.x, g.c.y, g.c.z, g.c.w};
+    PixIn<MODE> in[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) {
+      const bool ok = vm[s4] && (qs[s4] > P.Q_thresh) && (gc[s4] > P.C_thresh) && (cjs[s4] > P.C_thresh);
+      int u_t = 0, v_t = 0;
+      if (MODE == M3S_MODE_CALIB) {  // gather_pixel's ind_Xi % width, ind_Xi / width
+        const int iid = id[s4];
+        int vv = (int)((float)iid * (1.0f / (float)P.width));
+        if (vv * P.width > iid) vv--;
+        if ((vv + 1) * P.width <= iid) vv++;
+        v_t = vv;
+        u_t = iid - vv * P.width;
+      }
+      in[s4] = make_pixin<MODE>(P, gx[s4], ok, qs[s4], u_t, v_t);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) {
+      float Y[3];
+      act(Tm, Xj[s4], Y);
+      pixel_contrib<MODE>(acc, P, in[s4], Y);
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; k++) {
+      const f32x4 v = {in[0].v[k], in[1].v[k], in[2].v[k], in[3].v[k]};
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(pl + (size_t)k * HW + p0));
+    }
+  }
+  float sums[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
+  acc.fold(sums);
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
 }
@@ -2527,7 +2702,6 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBsCap = 40;  // L_ik blocks of a column prefetched into LDS (the rest staged)
 __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
   if (C.flags[kFlagStop]) return;
@@ -3680,7 +3854,9 @@ int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipSt
     else
       linearize_kernel<MODE, TRACK, false, false><<<g, b, 0, st>>>(L);
   } else if (pack == 1) {
-    if (vec)
+    if (vec && M3S_GATHER_LDS)
+      linearize_gather_kernel<MODE><<<g, b, 0, st>>>(L);
+    else if (vec)
       linearize_kernel<MODE, false, true, true><<<g, b, 0, st>>>(L);
     else
       linearize_kernel<MODE, false, false, true><<<g, b, 0, st>>>(L);

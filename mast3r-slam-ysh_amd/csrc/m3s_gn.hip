@@ -1979,6 +1979,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // load of both in flight at once (a loop of dependent load -> LDS store
   // rounds cost a memory latency each: ~5 us at C3)
   const bool asm_in = IN_LDS && D.asm_lds && phase != 2;
+  const bool lazy_asm = asm_in && D.nc == 0 && phase == 0;
   double *fl = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1));  // staged fin (asm_in)
   {
     const int np_ = STORE == 1 ? D.plan_len : 0, nf_ = asm_in ? D.E * kFin : 0;
@@ -2015,6 +2016,22 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
   const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
   double *scr = scratch[wave];
+  // lazy assembly (lazy_asm): slot sl's entry lane49 / the RHS entry lane7 of
+  // column k from the staged fin, the sums of the assembly loops below
+  auto asm_slot = [&](int sl) {
+    double v = 0.0;
+    for (int q = asm_ptr[sl]; q < asm_ptr[sl + 1]; q++) v += fl[asm_edge[q] * kFin + lane49];
+    return (sl < m) ? v : -v;
+  };
+  auto asm_rhs = [&](int k) {
+    double v = 0.0;
+    for (int q = g_ptr[k]; q < g_ptr[k + 1]; q++) {
+      const int ent = g_edge[q];
+      const double gj = fl[(ent >> 1) * kFin + 49 + lane7];
+      v += (ent & 1) ? gj : -gj;
+    }
+    return v;
+  };
 
   if (phase == 2) {  // after border_kernel: y and the failure flag from global memory
     for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
@@ -2025,7 +2042,12 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // in LDS with coalesced loads, then summed per slot in edge order (the sums
   // of assemble_slots_kernel); otherwise that kernel assembled into the global
   // factor array, copied in here.
-  if (asm_in) {
+  // lazy: no assembly phase; each DIAG / OFF item sums its own slot (and
+  // DIAG(k) its RHS) from the staged fin when it starts, in the same order
+  // (bitwise the same values), so the first items start right after the
+  // staging (round 3; graphs without a dense tail, whose border tasks read
+  // assembled slots)
+  if (asm_in && !lazy_asm) {
     for (int idx = tid; idx < S * 49; idx += 1024) {
       const int sl = idx / 49, t = idx - sl * 49;
       double v = 0.0;
@@ -2042,7 +2064,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       }
       y[idx] = v;
     }
-  } else {
+  } else if (!asm_in) {
     if (IN_LDS)
       for (int idx = tid; idx < S * 49; idx += 1024) Lb[idx] = D.L[idx];
     for (int idx = tid; idx < m * 7; idx += 1024) y[idx] = D.rhs[idx];
@@ -2093,7 +2115,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       const int p0 = split ? dpart_ptr[k] : 0, p1 = split ? dpart_ptr[k + 1] : 0;
       const int q0 = (p1 > p0) ? part_q1[p1 - 1] : dtr_ptr[k], q1 = dtr_ptr[k + 1];
       for (int pi = p0; pi < p1; pi++) wait_flag(&pdone[pi], &fail_s);
-      double v = Lb[(size_t)k * 49 + lane49];
+      double v = lazy_asm ? asm_slot(k) : Lb[(size_t)k * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
       M3S_LSTAMP(it, 1);
@@ -2105,7 +2127,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       M3S_LSTAMP(it, 2);
       // forward step, off the factorisation's critical path:
       // y_k = L_kk^-1 (b_k - sum_p L_kp y_p)
-      double bb = y[k * 7 + lane7];
+      double bb = lazy_asm ? asm_rhs(k) : y[k * 7 + lane7];
       for (int pi = p0; pi < p1; pi++) bb += D.parts[(size_t)pi * 56 + 49 + lane7];
       M3S_POLL(q0, q1, flag_set(&ydone[dtr_p[q]]), (bb = sub_matvec<STAGE, false>(bb, Lb, dtr_slot, dtr_p, qa, qb, y, lane7, lane49, lane, stg)));
       fwd_solve_store(bb, wcol, scr, y + (size_t)k * 7, lane);
@@ -2120,7 +2142,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       // the updates first (their inputs L_ip, L_kp are older than DIAG(k)),
       // so only the W_k product waits for DIAG(k)
       for (int pi = p0; pi < p1; pi++) wait_flag(&pdone[pi], &fail_s);
-      double v = Lb[(size_t)dst * 49 + lane49];
+      double v = lazy_asm ? asm_slot(dst) : Lb[(size_t)dst * 49 + lane49];
       for (int pi = p0; pi < p1; pi++) v += D.parts[(size_t)pi * 56 + lane49];
       M3S_POLL(q0, q1, flag_set(&sdone[tr_a[q]]) && flag_set(&sdone[tr_b[q]]), (v = sub_products<STAGE, false>(v, Lb, tr_a, tr_b, qa, qb, r7, c7, lane49, lane, stg)));
       M3S_LSTAMP(it, 1);

@@ -94,3 +94,53 @@ def test_two_processes_gloo_collective_match_in_process_and_single_call(tmp_path
     be.gauss_newton_rays(Twc, g.Xs.to(dev).contiguous(), *args, 0.003, 10.0, 0.0, 1.5, ITERS, 0.0, info=info)
     torch.cuda.synchronize()
     np.testing.assert_allclose(poses[0], Twc.cpu().numpy(), rtol=0, atol=1e-4)
+
+
+def _rccl_main(rank, world, port, out_dir):
+    """One rank over RCCL (backend "nccl"): the product's collective calls on
+    device tensors (bench.py's --gpus N path: init with device_id, the
+    all-gather of per-edge sums, the barrier and the max-over-ranks timing
+    all-reduce). A one-GPU box cannot hold two RCCL ranks; one rank still runs
+    RCCL's own init and kernels."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mast3r-slam-ysh_amd")]
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    from mast3r_slam_amd.distributed import ShardedGN
+
+    g = _graph()
+    E = g.n_edges
+    Twc = g.T_init.data.clone().to(dev).contiguous()
+    gn = ShardedGN(1, Twc, g.Xs.to(dev).contiguous(), g.Cs.to(dev).contiguous(), g.ii.to(dev), g.jj.to(dev),
+                   g.idx_ii2jj.to(dev).contiguous(), g.valid_match.to(dev).contiguous(), g.Q.to(dev).contiguous(),
+                   E, **SIG)
+    gn.ops.prepare(0.0)
+    gn.ops.linearize(0, E, gn.es_loc)
+    es_all = torch.empty_like(gn.es_loc)
+    dist.all_gather_into_tensor(es_all, gn.es_loc)
+    dist.barrier()
+    t = torch.tensor([1.5], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    torch.cuda.synchronize()
+    np.save(os.path.join(out_dir, "rccl_es.npy"), gn.es_loc.cpu().numpy())
+    np.save(os.path.join(out_dir, "rccl_es_all.npy"), es_all.cpu().numpy())
+    np.save(os.path.join(out_dir, "rccl_meta.npy"), np.array([float(t.item()), dist.get_backend() == "nccl"]))
+    gn.ops.close()
+    dist.destroy_process_group()
+
+
+def test_rccl_backend_collectives_on_device_tensors(tmp_path):
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_rccl_main, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    es = np.load(tmp_path / "rccl_es.npy")
+    es_all = np.load(tmp_path / "rccl_es_all.npy")
+    meta = np.load(tmp_path / "rccl_meta.npy")
+    assert meta[1] == 1.0 and meta[0] == 1.5
+    assert np.isfinite(es).all() and np.abs(es).max() > 0
+    np.testing.assert_array_equal(es_all, es)

@@ -384,7 +384,7 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
                   "in the timed region); back_to_back_ms = the same kernel launched back to back",
         "back_to_back_ms": round(b2b_ms, 5),
         "gather_kernel": {
-            "kernel": "linearize_kernel (first GN iteration: gathers Xi/Ci through idx, stores planes)",
+            "kernel": "linearize_gather_kernel (first GN iteration: streams prefetched by LDS-DMA, gathers Xi/Ci through idx, stores planes)",
             "avg_launch_ms": round(first_ms, 5),
             "achieved": round(bytes_alg / (first_ms * 1e-3) / 1e9, 1),
             "frac": round(bytes_alg / (first_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output
 cd $R
 TAG=$TAG/pmc bash tools/pmc_bench.sh || exit 1
 python3 tools/pmc_summary.py $OUT/pmc linearize_packed_kernel pmc/linearize_c3.json 32 || exit 1
-python3 tools/pmc_summary.py $OUT/pmc linearize_kernel pmc/linearize_c3.json 32 gather || exit 1
+python3 tools/pmc_summary.py $OUT/pmc linearize_gather_kernel pmc/linearize_c3.json 32 gather || exit 1
 cp pmc/linearize_c3.json $OUT/
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -5 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json

@@ -3864,6 +3864,8 @@ int check_args(const m3s_gn_args *a) {
   return M3S_OK;
 }
 
+bool gather_lds_path();  // (knobs, below)
+
 // pack: 0 gathering kernel, 1 gathering kernel that stores the planes,
 // 2 packed kernel (reads the planes; VEC layout only)
 template <int MODE, bool TRACK>
@@ -3876,7 +3878,7 @@ int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipSt
     else
       linearize_kernel<MODE, TRACK, false, false><<<g, b, 0, st>>>(L);
   } else if (pack == 1) {
-    if (vec && M3S_GATHER_LDS)
+    if (vec && M3S_GATHER_LDS && gather_lds_path())
       linearize_gather_kernel<MODE><<<g, b, 0, st>>>(L);
     else if (vec)
       linearize_kernel<MODE, false, true, true><<<g, b, 0, st>>>(L);
@@ -3956,6 +3958,7 @@ struct Knobs {
   std::atomic<int> tail_mfma{1};       // M3S_TAIL_MFMA: 0 = the dense tail in sparse_llt_kernel
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel
   std::atomic<int> debug_drop_item{-1};  // drop one LLT dispatch item (bounded-wait test)
+  std::atomic<int> gather_lds{1};      // 0: the round-2 VGPR-staged gathering kernel (bitwise reference)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -3987,6 +3990,7 @@ inline bool tail_mfma() { return knobs().tail_mfma != 0; }
 inline bool border_split() { return knobs().border_split != 0; }
 inline bool force_dense_knob() { return knobs().dense == 1; }
 inline int drop_item_knob() { return knobs().debug_drop_item; }
+bool gather_lds_path() { return knobs().gather_lds != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -3995,6 +3999,7 @@ constexpr bool tail_mfma() { return true; }
 constexpr bool border_split() { return true; }
 constexpr bool force_dense_knob() { return false; }
 constexpr int drop_item_knob() { return -1; }
+bool gather_lds_path() { return true; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -4164,7 +4169,9 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.Kd = a->mode == M3S_MODE_CALIB ? a->K : nullptr;
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xs, 16) && vec_ok(a->Cs, 16) && vec_ok(a->Q, 16) &&
                    vec_ok(a->idx_ii2jj, 16) && vec_ok(a->valid_match, 4);
-  const bool can_pack = vec &&
+  // (the packed and pipelined gathering kernels address a pointmap through
+  // 32-bit buffer offsets: 12 HW bytes must fit a signed int)
+  const bool can_pack = vec && a->HW * 12 < ((int64_t)1 << 31) &&
                         (a->mode != M3S_MODE_CALIB || (a->width < 65536 && a->height < 32768));
   int pack = 0;
   bool ordered = false;
@@ -5571,7 +5578,8 @@ int m3s_set_knob(const char *name, int value) {
              {"track_persistent", &k.track_persistent}, {"prologue", &k.prologue},
 #ifdef M3S_TEST_PATHS
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
-             {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item}
+             {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
+             {"gather_lds", &k.gather_lds}
 #endif
   };
   for (const auto &t : tab)

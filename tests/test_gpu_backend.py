@@ -504,3 +504,53 @@ def test_tail_over_workgroups_matches_one_workgroup(test_lib, be, N, knobs):
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)
 
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib", "points"])
+def test_gn_partial_trip_pixel_count_matches_oracle(be, mode):
+    """HW = 20 x 52 = 1040 pixels: a multiple of 4 (the vector, packed and
+    pipelined gathering paths) but not of a 1024-pixel trip, so the last trip
+    of the last chunk is partial: its lanes past the end take no part and the
+    buffer resources read zeros past HW."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(6, 20, 52, seed=37)
+    Xs = constrained(g) if mode == "calib" else g.Xs
+    T_gpu, dx_gpu, info = run_gpu(be, mode, g, 5, 0.0, Xs=Xs)
+    T_ref, dx_ref, it, failed = run_oracle(mode, g, 5, 0.0, Xs=Xs)
+    assert info[be.INFO_ITERS] == it == 5
+    assert info[be.INFO_SOLVE_FAIL] == failed == 0
+    np.testing.assert_allclose(T_gpu, T_ref, atol=1e-4)
+    np.testing.assert_allclose(dx_gpu, dx_ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode,idx32", [("calib", False), ("rays", False), ("rays", True), ("points", False)])
+def test_pipelined_gathering_launch_matches_round2_kernel_bitwise(test_lib, be, knobs, mode, idx32):
+    """The first GN iteration's pipelined kernel (linearize_gather_kernel:
+    streams by LDS-DMA, gathers before the refill) against the round-2
+    VGPR-staged linearize_kernel it replaced (test-build knob gather_lds=0):
+    the same per-pixel calls in the same order, so poses, dx and info are
+    bitwise equal after several iterations; int64 and int32 ids."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(10, 64, 96, seed=38)
+    Xs = (constrained(g) if mode == "calib" else g.Xs).to(DEV).contiguous()
+    idx = g.idx_ii2jj.to(torch.int32) if idx32 else g.idx_ii2jj
+    out = []
+    for knob in (0, 1):
+        knobs("gather_lds", knob)
+        Twc = g.T_init.data.clone().to(DEV).contiguous()
+        info = torch.zeros(8, dtype=torch.int32, device=DEV)
+        Cs, ii, jj, ix, valid, Q = (t.to(DEV).contiguous() for t in (g.Cs, g.ii, g.jj, idx, g.valid_match, g.Q))
+        if mode == "calib":
+            (dx,) = be.gauss_newton_calib(Twc, Xs, Cs, g.K.to(DEV), ii, jj, ix, valid, Q, g.H, g.W, -10, 1e-6,
+                                          1.0, 10.0, 0.0, 1.5, 4, 0.0, info=info)
+        elif mode == "rays":
+            (dx,) = be.gauss_newton_rays(Twc, Xs, Cs, ii, jj, ix, valid, Q, 0.003, 10.0, 0.0, 1.5, 4, 0.0, info=info)
+        else:
+            (dx,) = be.gauss_newton_points(Twc, Xs, Cs, ii, jj, ix, valid, Q, 0.05, 0.0, 1.5, 4, 0.0, info=info)
+        torch.cuda.synchronize()
+        out.append((Twc.cpu().numpy(), dx.cpu().numpy(), info.cpu().numpy()))
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+    assert int(out[1][2][be.INFO_SOLVE_FAIL]) == 0

@@ -130,7 +130,7 @@ inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cy
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      colsync, tail, eorder, planes, total;
+      colsync, wgran, tail, eorder, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -185,6 +185,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap] (epoch-tagged, zeroed per call)
   off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
+  L.wgran = off;  // df_factor_kernel: W_k of every column as 16-B tagged granules (zeroed with colsync per call)
+  off = align_up(off + (size_t)16 * 49 * (size_t)(m + 1), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
   off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
   // target-side planes of every edge (4 planes = rays / points, the widest modes)
@@ -2579,8 +2581,12 @@ struct DfArgs {
   int32_t *flags;
   double *tail_A;
   int tail_ld;
+  double *Wgr;     // [m][49] W_k as {value, epoch tag} 16-B granules (round 3)
 };
 constexpr int kDfWaves = 4;
+#ifndef M3S_DF_WGRAN  // df_factor_kernel: OFF items take W_k from tagged granules (one round trip)
+#define M3S_DF_WGRAN 1
+#endif
 
 __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
   if (D.flags[kFlagStop]) return;
@@ -2631,6 +2637,18 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       if (lane == 0) M3S_CSTAMP(0, k, 2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (M3S_DF_WGRAN && lane < 7) {
+        // W_k as tagged granules (after the drain: an OFF item that sees a
+        // tag also sees y_k and L_kk): entry qq * 7 + lane of Dinv[k]
+        const __amdgpu_buffer_rsrc_t RG =
+            __builtin_amdgcn_make_buffer_rsrc(D.Wgr, 0, (int)(16 * 49 * (D.m + 1)), 0x00020000);
+#pragma unroll
+        for (int qq = 0; qq < 7; qq++) {
+          const unsigned long long bw = (unsigned long long)__double_as_longlong(wcol[qq]);
+          const u32x4 gw = {(unsigned)(bw & 0xffffffffu), (unsigned)(bw >> 32), (unsigned)want, 0u};
+          __builtin_amdgcn_raw_buffer_store_b128(gw, RG, (k * 49 + qq * 7 + lane) * 16, 0, 16);
+        }
+      }
       if (lane == 0) M3S_CSTAMP(0, k, 3);
     } else if (code < D.n_tasks) {  // OFF(t)
       const int dst = task_dst[code], k = task_col[code];
@@ -2642,10 +2660,32 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       double v = L[(size_t)dst * 49 + lane49];
       v = sub_products<true, false, true>(v, L, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg, D.sdone, want, &ok);
       if (lane == 0) M3S_CSTAMP(3, dst, 1);
+#if M3S_DF_WGRAN
+      {  // W_k from its tagged granules: the poll and the payload are one load
+        const __amdgpu_buffer_rsrc_t RG =
+            __builtin_amdgcn_make_buffer_rsrc(D.Wgr, 0, (int)(16 * 49 * (D.m + 1)), 0x00020000);
+        int spins = 0;
+        for (;;) {
+          const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(RG, (k * 49 + lane49) * 16, 0, 16);
+          if (__ballot(act49 && g.z != (unsigned)want) == 0) {
+            if (act49) W[lane] = __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kColSpins) {
+            ok = false;
+            break;
+          }
+        }
+      }
+      if (!ok && lane == 0) set_fail(D.flags);
+      if (lane == 0) M3S_CSTAMP(3, dst, 2);
+#else
       ok &= wait_flags(D.sdone, task_col, code, code + 1, BIG, want, lane);  // DIAG(k)
       if (!ok && lane == 0) set_fail(D.flags);
       if (lane == 0) M3S_CSTAMP(3, dst, 2);
       if (act49) W[lane] = ld_sc1(D.Dinv + (size_t)k * 49 + lane);
+#endif
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -4357,6 +4397,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         F.flags = flags;
         F.tail_A = tail;
         F.tail_ld = tld;
+        F.Wgr = at<double>(ws, Ly.wgran);
         const int nw = std::max(1, std::min(F.n_items, 1024));
         df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
       } else {

@@ -63,7 +63,7 @@ def analyze(path):
     ours = [(s, e, n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0])
             for s, e, n in seq if "anonymous namespace" in n]
     # calls start at the gathering linearize launch (first GN iteration)
-    starts = [i for i, (_, _, n) in enumerate(ours) if n.startswith("linearize_kernel")]
+    starts = [i for i, (_, _, n) in enumerate(ours) if n.startswith(("linearize_kernel", "linearize_gather_kernel"))]
     b = starts[-1]
     call = ours[b:]
     print(f"between the last two calls: previous call ends, this call's first kernel at "

@@ -6,7 +6,8 @@ time per library per case and whether the final poses / dx / info are bitwise
 equal to the first library's.
 
 usage: python tools/ab_calls.py variants/lib_A.so variants/lib_B.so ...
-  AB_CASES="calib:32:128:128:10:16,rays:140:24:32:3:8"  (mode:N:H:W:iters:dense_tail_min)
+  AB_CASES="calib:32:128:128:10:16,rays:140:24:32:3:8"  (mode:N:H:W:iters:dense_tail_min[:seed])
+  (seed defaults to 4242 + N; bench.py's C3 graph is seed 1003)
 """
 import ctypes
 import os
@@ -39,9 +40,9 @@ def main():
         handles.append(L)
     rounds = int(os.environ.get("AB_ROUNDS", "7"))
     for case in os.environ.get("AB_CASES", DEFAULT).split(","):
-        mode, N, H, W, iters, tail = case.split(":")
+        mode, N, H, W, iters, tail, *sd = case.split(":")
         N, H, W, iters, tail = int(N), int(H), int(W), int(iters), int(tail)
-        g = synthetic.make_graph(N, H, W, seed=4242 + N, device=dev)
+        g = synthetic.make_graph(N, H, W, seed=int(sd[0]) if sd else 4242 + N, device=dev)
         calib = mode == "calib"
         Xs = (g.Xs[..., 2:3] * synthetic.pixel_rays(H, W, g.K)[None]).contiguous() if calib else g.Xs.contiguous()
         mid = be.MODE_CALIB if calib else be.MODE_RAYS

@@ -879,6 +879,9 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 // flight), the pose-only math, the rest, the plane stores. Same arithmetic per
 // pixel as linearize_kernel<MODE, false, true, true> (gather_pixel +
 // make_pixin + pixel_contrib): bitwise the same planes, partials and sums.
+#ifndef M3S_DIAG_RL
+#define M3S_DIAG_RL 1  // sparse_llt_kernel's 7x7 DIAG factor: column broadcast by readlanes (0: through LDS, A/B)
+#endif
 #ifndef M3S_GATHER_LDS  // pipelined gathering launch (0: linearize_kernel's VGPR-staged loop)
 #define M3S_GATHER_LDS 1
 #endif
@@ -1816,7 +1819,7 @@ __device__ __forceinline__ void diag_updates_sc1(double &v, double &bb, const do
 // updates -> L_kk (row-major, upper part 0) into Lb[k], W_k = L_kk^-1
 // (row-major) into Di[k] (and Wl, if given); lane c < 7 keeps column c of W_k
 // in wcol for the forward step. Returns true on a non-positive pivot.
-template <bool SC1 = false>
+template <bool SC1 = false, bool RL = false>
 __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double *Di, double *scr, int lane,
                                             int l7, double (&wcol)[7], double *Wl = nullptr) {
   // entry layout -> row layout through the wave's scratch
@@ -1832,7 +1835,10 @@ __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double 
   // final and s_r (r > j) loses L[r][j] W[j][c]. Column j is scaled on every
   // lane (lane j holds the pivot itself; the lanes above keep finite upper-
   // triangle values that are masked when L_kk is stored). No per-pair
-  // readlanes, no second serial chain for W.
+  // readlanes, no second serial chain for W. RL: the column goes by
+  // constant-lane readlanes instead (sparse_llt_kernel: its one workgroup
+  // has the SIMDs to itself; in df_factor_kernel the readlanes contend with
+  // the other waves' issue and the LDS broadcast measured faster).
   double sw[7];
 #pragma unroll
   for (int r = 0; r < 7; r++) sw[r] = (r == lane) ? 1.0 : 0.0;
@@ -1844,6 +1850,17 @@ __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double 
     const double inv = rsqrt_nr(d);
     a[j] *= inv;
     wcol[j] = sw[j] * inv;
+    if (RL) {
+      // column j of L straight from its lanes (constant-lane readlanes): no
+      // LDS round trip on the pivot chain
+#pragma unroll
+      for (int cc = j + 1; cc < 7; cc++) {
+        const double lcj = readlane_d(a[j], cc);
+        a[cc] -= a[j] * lcj;
+        sw[cc] -= lcj * wcol[j];
+      }
+      continue;
+    }
     if (lane < 7) scr[lane] = a[j];
     wave_lds_fence();
 #pragma unroll
@@ -2122,7 +2139,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
       M3S_LSTAMP(it, 1);
       double wcol[7];
-      const bool bad = diag_factor(v, k, Lb, Di, scr, lane, l7, wcol);
+      const bool bad = diag_factor<false, M3S_DIAG_RL>(v, k, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2205,7 +2222,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     auto tail_diag = [&](int kk) {
       const double v = Lb[(size_t)kk * 49 + lane49];
       double wcol[7];
-      const bool bad = diag_factor(v, kk, Lb, Di, scr, lane, l7, wcol);
+      const bool bad = diag_factor<false, M3S_DIAG_RL>(v, kk, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;
       fwd_solve_store(y[kk * 7 + lane7], wcol, scr, y + (size_t)kk * 7, lane);
     };

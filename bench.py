@@ -78,6 +78,7 @@ def parse(argv=None):
     ap.add_argument("--mode", choices=("calib", "rays"), default="calib")
     ap.add_argument("--lin-reps", type=int, default=30)
     ap.add_argument("--cold-steps", type=int, default=5)
+    ap.add_argument("--natural-steps", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
@@ -205,29 +206,29 @@ def run(args):
                        ops=ops, **sig)
     info = torch.zeros(8, dtype=torch.int32, device=dev)
 
-    def step():
+    def step(delta=0.0):
         Twc.copy_(T_init)
         if world == 1 and not dry:  # the drop-in entry point itself
             if calib_mode:
                 be.gauss_newton_calib(Twc, Xs, Cs, g.K, ii, jj, idx, valid, Q, H, W, -10, 1e-6, 1.0,
-                                      10.0, 0.0, 1.5, args.iters, 0.0, info=info)
+                                      10.0, 0.0, 1.5, args.iters, delta, info=info)
             else:
                 be.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5,
-                                     args.iters, 0.0, info=info)
+                                     args.iters, delta, info=info)
         else:
-            solver.solve(args.iters, 0.0)
+            solver.solve(args.iters, delta)
 
     def sync():
         if not dry:
             torch.cuda.synchronize()
 
-    def timed(nsteps):
+    def timed(nsteps, delta=0.0):
         if world > 1:
             dist.barrier()
         sync()
         t0 = time.perf_counter()
         for _ in range(nsteps):
-            step()
+            step(delta)
         sync()
         if world > 1:
             dist.barrier()
@@ -256,6 +257,23 @@ def run(args):
     else:
         with be.knob("plan_cache", 0):
             cold_el = timed(args.cold_steps) if args.cold_steps > 0 else None
+
+    # natural termination (reported separately): the same calls
+    # with the reference's delta_thresh = 1e-8 (config/base.yaml:49) and
+    # max_iter = 10; the device stop flag ends the loop when a step's norm
+    # falls below delta, and the iterations actually run are counted
+    natural = None
+    if not dry and args.natural_steps > 0:
+        step(1e-8)  # warm-up of the delta path
+        nat_el = timed(args.natural_steps, 1e-8)
+        nat_iters = int(solver.ops.info[0]) if world > 1 else int(info[be.INFO_ITERS])
+        natural = {
+            "delta_thresh": 1e-8, "max_iter": args.iters, "calls": args.natural_steps,
+            "iters_per_call": nat_iters,
+            "ms_per_call": round(nat_el / args.natural_steps * 1e3, 4),
+            "gn_iters_per_s": round(nat_iters * args.natural_steps / nat_el, 2),
+            "note": "config/base.yaml:49 delta; the fp32 steps of this seeded graph stay above 1e-8, so "
+                    "every call runs max_iter iterations (tests/test_gpu_large.py checks the same)"}
 
     out = {
         "metric": METRIC,
@@ -286,6 +304,7 @@ def run(args):
         },
         "gn_iters_per_s": round(gn_iters_per_s, 2),
         "pair_iters_per_s": round(pair_iters_per_s, 1),
+        "natural_termination": natural,
         "cold": {
             "ms_per_step": round(cold_el / args.cold_steps * 1e3, 4) if cold_el else None,
             "gn_iters_per_s": round(args.iters * args.cold_steps / cold_el, 2) if cold_el else None,
@@ -302,7 +321,7 @@ def run(args):
                        "not a scaling measurement" % world)
     else:
         out["roofline"] = roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
-                                       world, dev)
+                                       world, dev, step if world == 1 else None)
 
     if rank == 0 and world == 1 and not dry:
         out["hbm_copy"] = copy_leg(be, dev)
@@ -321,27 +340,46 @@ def run(args):
         dist.destroy_process_group()
 
 
-def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s, world, dev):
+def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s, world, dev, call=None):
     """The dominant kernel: GN iterations 2..10 of a call run
     linearize_packed_kernel (the first runs the gathering kernel that also
-    stores the target-side planes). Timed in the solve's own launch pattern
-    (linearize -> LLT -> ...): a HIP event pair on the launch stream around
-    each linearize and each solve launch of stepwise solves of the same graph
-    (the linearize pair also covers the launch's ~3 us per-edge reduce). The
-    same kernel launched back to back is timed too, for reference."""
+    stores the target-side planes). Timed in the benched call's own launch
+    pattern: at N = 1 the drop-in call itself records HIP timing events on its
+    stream around each iteration's linearize launch and solve launches
+    (m3s_debug_call_timing; nothing else is launched between them); a sharded
+    rank times its stepwise solve's linearize launches (their per-edge reduce
+    included). The same kernel launched back to back is timed too."""
     n_loc = len(ids)
     sel = torch.tensor(ids, dtype=torch.int64, device=ii.device)
     kf_touched = torch.unique(torch.cat([ii[sel], jj[sel]])).numel() if n_loc else 0
     bytes_alg = HW * (13 * n_loc + 16 * kf_touched)  # SURVEY.md §8(d) per (edge, px) and (KF, px)
     stream = torch.cuda.current_stream(dev)
     lin, first, slv = [], [], []
-    for rep in range(4):
-        Twc.copy_(T_init)
-        t_lin, t_slv = solver.solve_timed(args.iters, 0.0, stream)
-        if rep:  # the first call is a warm-up
-            first.append(t_lin[0])
-            lin += t_lin[1:]  # iterations 2.. (packed kernel)
-            slv += t_slv
+    if call is not None:
+        call()  # warm-up
+        torch.cuda.synchronize()
+        be.debug_call_timing(True)
+        for _ in range(5):
+            call()
+        spans = be.debug_call_times()
+        be.debug_call_timing(False)
+        assert len(spans) == 5 * 2 * args.iters, len(spans)
+        first = [ms for k, ms in spans if k == 0]
+        lin = [ms for k, ms in spans if k == 1]
+        slv = [ms for k, ms in spans if k == 2]
+        timing = ("HIP events on the call's stream around each linearize launch inside the drop-in call "
+                  "(m3s_debug_call_timing: its own launch pattern, 5 calls x %d packed launches); "
+                  "back_to_back_ms = the same kernel launched back to back" % (args.iters - 1))
+    else:
+        for rep in range(4):
+            Twc.copy_(T_init)
+            t_lin, t_slv = solver.solve_timed(args.iters, 0.0, stream)
+            if rep:  # the first call is a warm-up
+                first.append(t_lin[0])
+                lin += t_lin[1:]  # iterations 2.. (packed kernel)
+                slv += t_slv
+        timing = ("HIP events around each linearize launch (+ its per-edge reduce) of this rank's "
+                  "stepwise solves; back_to_back_ms = the same kernel launched back to back")
     lin_ms = sum(lin) / len(lin)
     Twc.copy_(T_init)
     be.gn_prepare(solver.args, solver.keep)
@@ -380,8 +418,8 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
         "traffic_note": traffic_note,
         "algorithmic_bytes_per_launch": bytes_alg,
         "avg_launch_ms": round(lin_ms, 5),
-        "timing": "HIP events around each linearize launch of stepwise solves (its launch pattern "
-                  "in the timed region); back_to_back_ms = the same kernel launched back to back",
+        "timing": timing,
+        "in_call_ms_min_max": [round(min(lin), 5), round(max(lin), 5)],
         "back_to_back_ms": round(b2b_ms, 5),
         "gather_kernel": {
             "kernel": "linearize_gather_kernel (first GN iteration: streams prefetched by LDS-DMA, gathers Xi/Ci through idx, stores planes)",
@@ -391,8 +429,8 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
             "traffic": gather_traffic,
         },
         "solve": {
-            "kernels": "fp64 sparse LLT + retraction (sparse_llt_kernel [+ border_kernel]), stepwise "
-                       "path (finalize + assemble launches included)",
+            "kernels": "fp64 block-sparse LLT + retraction: every solve launch of one GN iteration "
+                       "(in-call events at N = 1; the stepwise path's finalize + assemble included at N > 1)",
             "avg_ms": round(sum(slv) / len(slv), 5),
             "bound": "latency (elimination-tree critical path, DESIGN.md §4)",
         },

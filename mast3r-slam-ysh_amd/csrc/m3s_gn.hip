@@ -661,6 +661,9 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t R, __attribute_
                                           int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 16, voff, soff, 0, 0);
 }
+// A buffer offset past every resource's range (num_records < 2^31): the load
+// returns zeros and makes no memory access.
+constexpr int kFarOff = 0x7fff0000;
 // Xj floats 6h .. 6h + 5 of a lane's 12 (its 4 pixels x y z, interleaved over
 // three 16-B LDS rows 1 KB apart, from xs), one ds_read_b32 each straight
 // into the half of the pair that uses it: plain loads merge into 16-B reads
@@ -781,19 +784,30 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   const __amdgpu_buffer_rsrc_t Rx =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_j), 0, (int)(12 * HW), 0x00020000);
   const int vo_p = 16 * ln, vo_x = 48 * ln;
+  const int pend = (int)p_end;
   // pw: the wave's first pixel of a trip (wave-uniform); lane pixels pw + 4 ln
   auto issue = [&](int pw, int sl_) {
 #if defined(M3S_PK_FLOOR) && M3S_PK_FLOOR == 2  // compute floor (A/B only): no loads
     return;
 #endif
+    // A trip that runs past the chunk's end (a partial last trip only): its
+    // lanes past the end take an offset beyond every resource, which reads
+    // zeros with no memory access. The buffer range check covers voffset (+
+    // the instruction offset), not soffset, so the wave-uniform trip base in
+    // soffset alone would let them read past the last plane / pointmap.
+    int vp = vo_p, vx = vo_x;
+    if (pw + kPixPerThread * 64 > pend) {  // wave-uniform: the full trips keep the fixed offsets
+      const bool out = pw + kPixPerThread * ln >= pend;
+      vp = out ? kFarOff : vo_p;
+      vx = out ? kFarOff : vo_x;
+    }
 #pragma unroll
     for (int k = 0; k < NPL; k++)
-      buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vo_p, 4 * pw);
+      buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vp, 4 * pw);
 #pragma unroll
     for (int k = 0; k < 3; k++)
-      buf_lds16(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vo_x, 12 * pw + 16 * k);
+      buf_lds16(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vx, 12 * pw + 16 * k);
   };
-  const int pend = (int)p_end;
   int pw = (int)p_begin + kPixPerThread * 64 * wv;
   if (pw < pend) issue(pw, 0);
   if (DEPTH > 1 && pw + kBlockPix < pend) issue(pw + kBlockPix, 1 % DEPTH);
@@ -947,9 +961,24 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
   // loads per trip, so the compiler's counted waits for the gathers behind it
   // stay exact), with kFar when there is no next trip and for the second idx
   // row of int32 ids
-  constexpr int kFar = 0x7fff0000;
+  constexpr int kFar = kFarOff;
   const int v4 = 4 * ln, v16 = 16 * ln, v48 = 48 * ln, vi0 = (i64 ? 32 : 16) * ln, vi1 = i64 ? 32 * ln + 16 : kFar;
+  const int64_t p_begin = c * A.chunk_pix;
+  const int pend = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
   auto issue = [&](int pw, bool far) {  // pw: the wave's first pixel of the trip
+    // a partial last trip: its lanes past the chunk's end load from kFar too
+    // (the range check covers voffset, not the trip base in soffset)
+    if (!far && pw + kPixPerThread * 64 > pend) {
+      const bool out = pw + kPixPerThread * ln >= pend;
+      buf_lds4_nt(Rv, L3(kGsValid), out ? kFar : v4, pw);
+      buf_lds16_nt(Rq, L3(kGsQ), out ? kFar : v16, 4 * pw);
+      buf_lds16_nt(Ri, L3(kGsIdx), out ? kFar : vi0, (i64 ? 8 : 4) * pw);
+      buf_lds16_nt(Ri, L3(kGsIdx + 1024), out ? kFar : vi1, 8 * pw);
+#pragma unroll
+      for (int k = 0; k < 3; k++) buf_lds16(Rx, L3(kGsXj + 1024 * k), out ? kFar : v48, 12 * pw + 16 * k);
+      buf_lds16(Rc, L3(kGsCj), out ? kFar : v16, 4 * pw);
+      return;
+    }
     buf_lds4_nt(Rv, L3(kGsValid), far ? kFar : v4, pw);
     buf_lds16_nt(Rq, L3(kGsQ), far ? kFar : v16, 4 * pw);
     buf_lds16_nt(Ri, L3(kGsIdx), far ? kFar : vi0, (i64 ? 8 : 4) * pw);
@@ -963,8 +992,6 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
 
   AccumFlat acc;
   acc.zero();
-  const int64_t p_begin = c * A.chunk_pix;
-  const int pend = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
   int pw = (int)p_begin + kPixPerThread * 64 * wv;
   if (pw < pend) issue(pw, false);
   for (int trip = 0; pw < pend; pw += kBlockPix, trip++) {
@@ -2734,6 +2761,172 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
   }
 }
 
+// ---------------------------------------- subtrees in LDS (round 4) --
+// Large graphs: the sparse columns below the dense tail split into subtrees
+// whose update lists stay inside the subtree (every row of struct(k) is an
+// etree ancestor of k; m3s_symbolic.h, build_subtree_image). One 1024-thread
+// workgroup per subtree runs its DIAG / OFF items as a dataflow over LDS
+// completion flags, with W_k, y_k and the blocks that fit in LDS (the rest,
+// border rows first, in global memory), instead of df_factor_kernel's
+// cross-CU hand-offs (~2 per etree level at ~1-3 us each). Every finished
+// block, W_k and y_k also goes to the global factor (write-through stores,
+// drained, then the slot's epoch flag), so the border tasks, the dense tail
+// and the column back-substitution read exactly what df_factor_kernel leaves
+// there. Per block the same products in the same order (the global plan's
+// ascending-p update lists, diag_factor without readlanes): bitwise the same
+// factor as df_factor_kernel. (SimplicialLLT's factor, gn_kernels.cu:132-153.)
+struct SubArgs {
+  const int32_t *sub;  // subtree image (in the plan upload)
+  double *L, *Dinv, *y;  // global factor: slots (assembled values in, L out), W_k, RHS in / y out
+  int32_t *sdone;        // [S] slot epoch flags (diagonal slot k: W_k and y_k)
+  int want;
+  int32_t *flags;
+};
+constexpr int kSubWaves = 16;
+
+// entry e of local block b: LDS (b < nlds) or the global slot (sc1: another
+// wave of this workgroup wrote it write-through; L1 may hold a stale line)
+__device__ __forceinline__ double sub_blk(const double *Bl, const double *Lg, const int32_t *gsl, int nlds, int b,
+                                          int e) {
+  return b < nlds ? Bl[b * 49 + e] : ld_sc1(Lg + (size_t)gsl[b] * 49 + e);
+}
+
+// the update sums of subtree_factor_kernel over the ready entries [qa, qb):
+// DIAG v -= L_kp L_kp^T (entry layout), forward bb -= L_kp y_p (row layout),
+// OFF v -= L_ip L_kp^T; per block the sub_products / sub_matvec sums
+__device__ __forceinline__ double sub_upd_diag(double v, const double *Bl, const double *Lg, const int32_t *gsl,
+                                               int nlds, const int32_t *dlist, int qa, int qb, int r7, int c7) {
+  for (int qq = qa; qq < qb; qq++) {
+    const int b = dlist[2 * qq];
+    double s0 = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) s0 += sub_blk(Bl, Lg, gsl, nlds, b, r7 + mm) * sub_blk(Bl, Lg, gsl, nlds, b, c7 + mm);
+    v -= s0;
+  }
+  return v;
+}
+__device__ __forceinline__ double sub_upd_fwd(double bb, const double *Bl, const double *Lg, const int32_t *gsl,
+                                              int nlds, const int32_t *dlist, const double *yl, int qa, int qb,
+                                              int l7) {
+  for (int qq = qa; qq < qb; qq++) {
+    const int b = dlist[2 * qq], pp = dlist[2 * qq + 1];
+    double t0 = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) t0 += sub_blk(Bl, Lg, gsl, nlds, b, l7 + mm) * yl[pp * 7 + mm];
+    bb -= t0;
+  }
+  return bb;
+}
+__device__ __forceinline__ double sub_upd_off(double v, const double *Bl, const double *Lg, const int32_t *gsl,
+                                              int nlds, const int32_t *tlist, int qa, int qb, int r7, int c7) {
+  for (int qq = qa; qq < qb; qq++) {
+    const int ba = tlist[2 * qq], bb2 = tlist[2 * qq + 1];
+    double s0 = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++)
+      s0 += sub_blk(Bl, Lg, gsl, nlds, ba, r7 + mm) * sub_blk(Bl, Lg, gsl, nlds, bb2, c7 + mm);
+    v -= s0;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs A) {
+  if (A.flags[kFlagStop]) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ double wsc[kSubWaves][64];
+  __shared__ int tk[2], fail_s;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int32_t *rec = A.sub + A.sub[1 + blockIdx.x];
+  const int ncol = rec[0], nblk = rec[1], nlds = rec[2], nA = rec[3], nB = rec[4], nwA = rec[14];
+  const int32_t *cols = A.sub + rec[5], *gsl = A.sub + rec[6], *itA = A.sub + rec[7], *itB = A.sub + rec[8],
+                *dptr = A.sub + rec[9], *dlist = A.sub + rec[10], *tcol = A.sub + rec[11], *tptr = A.sub + rec[12],
+                *tlist = A.sub + rec[13];
+  double *Wl = smem, *yl = Wl + (size_t)ncol * 49;
+  int32_t *bfl = reinterpret_cast<int32_t *>(yl + (size_t)ncol * 7), *wfl = bfl + nblk, *yfl = wfl + ncol;
+  double *Bl = reinterpret_cast<double *>(yfl + ncol + ((nblk + 2 * ncol) & 1));  // 8-B aligned
+  for (int q = tid; q < nblk + 2 * ncol; q += 64 * kSubWaves) bfl[q] = 0;
+  if (tid == 0) tk[0] = 0, tk[1] = 0, fail_s = 0;
+  __syncthreads();
+  const int r = lane / 7, c = lane % 7;
+  const bool act49 = lane < 49;
+  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
+  const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
+  double *scr = wsc[wave];
+  double *L = A.L;
+  // lists: waves [0, nwA) start on A (DIAG + internal OFF), the others on B
+  // (border OFF); an exhausted list sends its waves to the other one. A items
+  // never wait for B items, so A always completes, then B.
+  int lst = wave < nwA ? 0 : 1;
+  bool other_tried = false;
+  for (;;) {
+    const int t = wave_ticket(&tk[lst]);
+    if (t >= (lst ? nB : nA)) {
+      if (other_tried) break;
+      other_tried = true;
+      lst ^= 1;
+      continue;
+    }
+    const int code = lst ? itB[t] : itA[t];
+    if (code < 0) {  // DIAG(c): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
+      const int cc = -1 - code, k = cols[cc];
+      double v = L[(size_t)k * 49 + lane49];  // assembled (assemble_slots_kernel)
+      const int q0 = dptr[cc], q1 = dptr[cc + 1];
+      M3S_POLL(q0, q1, flag_set(&bfl[dlist[2 * q]]), (v = sub_upd_diag(v, Bl, L, gsl, nlds, dlist, qa, qb, r7, c7)));
+      double wcol[7];
+      const bool bad = diag_factor<true>(v, k, L, A.Dinv, scr, lane, l7, wcol, Wl + (size_t)cc * 49);
+      if (bad && lane == 0) set_fail(A.flags);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&wfl[cc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // forward step y_k = W_k (b_k - sum_p L_kp y_p)
+      double bb = A.y[(size_t)k * 7 + lane7];
+      M3S_POLL(q0, q1, flag_set(&yfl[dlist[2 * q + 1]]), (bb = sub_upd_fwd(bb, Bl, L, gsl, nlds, dlist, yl, qa, qb, l7)));
+      // y_k = W_k bb (fwd_solve_store's sums), to LDS and the global RHS
+      if (lane < 7) {
+#pragma unroll
+        for (int rr = 0; rr < 7; rr++) scr[rr * 7 + lane] = wcol[rr] * bb;
+      }
+      wave_lds_fence();
+      if (lane < 7) {
+        double yo = 0.0;
+#pragma unroll
+        for (int q = 0; q < 7; q++) yo += scr[lane * 7 + q];
+        yl[cc * 7 + lane] = yo;
+        st_sc1(A.y + (size_t)k * 7 + lane, yo);
+      }
+      wave_lds_fence();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&yfl[cc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L_kk, W_k, y_k stores have left
+      if (lane == 0) __hip_atomic_store(A.sdone + k, A.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {  // OFF(b): L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
+      const int b = code, cc = tcol[b], dst = gsl[b];
+      double v = L[(size_t)dst * 49 + lane49];  // assembled A_ik
+      const int q0 = tptr[b], q1 = tptr[b + 1];
+      M3S_POLL(q0, q1, flag_set(&bfl[tlist[2 * q]]) && flag_set(&bfl[tlist[2 * q + 1]]),
+               (v = sub_upd_off(v, Bl, L, gsl, nlds, tlist, qa, qb, r7, c7)));
+      wait_flag(&wfl[cc], &fail_s);  // W_k
+      if (act49) scr[lane] = v;
+      wave_lds_fence();
+      double x = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * Wl[cc * 49 + c7 + mm];
+      wave_lds_fence();
+      if (act49) {
+        if (b < nlds) Bl[b * 49 + lane] = x;
+        st_sc1(L + (size_t)dst * 49 + lane, x);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the global copy has left (global-only blocks are read from it)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) {
+        __hip_atomic_store(&bfl[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(A.sdone + dst, A.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && fail_s) set_fail(A.flags);
+}
+
 // dx = -x (original order), retraction, ||dx|| test (one wave; x in y, sc1)
 __device__ void col_finish(const ColArgs &C, int lane) {
   __shared__ float dxs[7 * 512];
@@ -2778,6 +2971,122 @@ __device__ void col_finish(const ColArgs &C, int lane) {
       C.info[M3S_INFO_CONVERGED] = 1;
       C.flags[kFlagStop] = 1;
     }
+  }
+}
+
+// Back-substitution of the subtrees (round 4; replaces col_backsub_kernel on
+// the subtree path): one 1024-thread workgroup per subtree. The tail's x is
+// final (tail_cyc_kernel), so every border term L_ik^T x_i (i in the tail) is
+// formed up front, all in flight at once, together with W_k and the internal
+// blocks into LDS; then the columns run from the subtree's root down as a
+// dataflow over LDS flags (x_k = W_k^T (y_k - sum_i L_ik^T x_i), rows
+// ascending: col_backsub_kernel's per-block sums in its order, bitwise the
+// same x). The workgroup that finishes last writes dx, retracts and tests
+// ||dx|| (col_finish), as col_backsub_kernel's last column did.
+struct SubBsArgs {
+  const int32_t *sub;
+  int ns;
+  int32_t *fin_ctr;  // workgroups finished, epoch-based
+  ColArgs C;
+};
+
+__global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsArgs A) {
+  const ColArgs &C = A.C;
+  if (C.flags[kFlagStop]) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int tk, last_s, fail_s;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int32_t *rec = A.sub + A.sub[1 + blockIdx.x];
+  const int ncol = rec[0], nblk = rec[1], n_int = rec[19], n_li = rec[20], nbd = nblk - n_int;
+  const int32_t *cols = A.sub + rec[5], *gsl = A.sub + rec[6], *ci = A.sub + rec[15], *cb = A.sub + rec[16],
+                *brow = A.sub + rec[17], *corder = A.sub + rec[18];
+  double *Wt = smem, *xl = Wt + (size_t)ncol * 49, *tb = xl + (size_t)ncol * 7, *Li = tb + (size_t)nbd * 7;
+  int32_t *xfl = reinterpret_cast<int32_t *>(Li + (size_t)n_li * 49);
+  const double *L = C.L;
+  // phase 0: W_k and the internal blocks to LDS, the border terms (every load
+  // of a batch in flight); the factor and the tail's x are final (earlier launches)
+  for (int i0 = 0; i0 < ncol * 49; i0 += 4096) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * 1024 + tid;
+      if (i < ncol * 49) v[u] = C.Dinv[(size_t)cols[i / 49] * 49 + i % 49];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * 1024 + tid;
+      if (i < ncol * 49) Wt[i] = v[u];
+    }
+  }
+  for (int i0 = 0; i0 < n_li * 49; i0 += 4096) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * 1024 + tid;
+      if (i < n_li * 49) v[u] = L[(size_t)gsl[i / 49] * 49 + i % 49];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * 1024 + tid;
+      if (i < n_li * 49) Li[i] = v[u];
+    }
+  }
+  for (int i = tid; i < nbd * 7; i += 1024) {  // (border block, entry): L_ik^T x_i, sub_matvec<TRANS>'s sum
+    const int b = n_int + i / 7, l = i % 7;
+    const double *Lb = L + (size_t)gsl[b] * 49;
+    const double *xi = C.y + (size_t)brow[b] * 7;
+    double t0 = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) t0 += Lb[mm * 7 + l] * xi[mm];
+    tb[i] = t0;
+  }
+  for (int q = tid; q < ncol; q += 1024) xfl[q] = 0;
+  if (tid == 0) tk = 0, last_s = 0, fail_s = 0;
+  __syncthreads();
+  const int lane7 = lane < 7 ? lane : 0;
+  for (;;) {
+    const int t = wave_ticket(&tk);
+    if (t >= ncol) break;
+    const int c = corder[ncol - 1 - t], k = cols[c];
+    double rr = C.y[(size_t)k * 7 + lane7];
+    for (int b = ci[c]; b < ci[c + 1]; b++) {
+      const int pc = brow[b];
+      wait_flag(&xfl[pc], &fail_s);
+      double t0 = 0.0;
+      if (b < n_li) {
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) t0 += Li[b * 49 + mm * 7 + lane7] * xl[pc * 7 + mm];
+      } else {
+        const double *Lb = L + (size_t)gsl[b] * 49;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) t0 += Lb[mm * 7 + lane7] * xl[pc * 7 + mm];
+      }
+      rr -= t0;
+    }
+    for (int b = cb[c]; b < cb[c + 1]; b++) rr -= tb[(b - n_int) * 7 + lane7];
+    double xk = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) xk += Wt[c * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
+    if (lane < 7) {
+      xl[c * 7 + lane] = xk;
+      st_sc1(C.y + (size_t)k * 7 + lane, xk);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&xfl[c], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's x stores have left
+  __syncthreads();
+  if (tid == 0 && fail_s) set_fail(C.flags);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the failure flag before the arrival)
+  // the workgroup that finishes last finishes the step
+  if (tid == 0) {
+    const int f = __hip_atomic_fetch_add(A.fin_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = (f - C.epoch * A.ns == A.ns - 1);
+  }
+  __syncthreads();
+  if (last_s && wave == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    col_finish(C, lane);
   }
 }
 
@@ -3543,6 +3852,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
   if (tid == 0) M3S_CSTAMP(2, 511, 0);
 }
 
+#ifdef M3S_TEST_PATHS  // reached only through the dense knob: every graph it fits (m <= 31) has a sparse plan
 // ------------------------------------------------- small dense Cholesky --
 // Thread (tr, tc) of a 16 x 32 grid owns A[lr*16 + tr][lc*32 + tc]. The RHS g
 // is appended as row n, so the factor's row n is y = L^-1 g. After the loop
@@ -3664,6 +3974,7 @@ __global__ void __launch_bounds__(kCholThreads) chol_small_kernel(
   }
   finish_step(xbuf, dxs, nrm, n, Twc, N, dx_out, info, stop, delta_thresh);
 }
+#endif  // M3S_TEST_PATHS (chol_small_kernel)
 
 // ------------------------------------------------------ call prologue --
 // The per-call setup of a GN call on the device, so the call's first
@@ -4016,6 +4327,7 @@ struct Knobs {
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel
   std::atomic<int> debug_drop_item{-1};  // drop one LLT dispatch item (bounded-wait test)
   std::atomic<int> gather_lds{1};      // 0: the round-2 VGPR-staged gathering kernel (bitwise reference)
+  std::atomic<int> subtree{1};         // 0: df_factor_kernel factors the sparse columns too (round-3 path)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -4032,6 +4344,7 @@ struct Knobs {
     env("M3S_TAIL_CYC", tail_cyc);
     env("M3S_TAIL_MFMA", tail_mfma);
     env("M3S_BORDER_SPLIT", border_split);
+    env("M3S_SUBTREE", subtree);
 #endif
   }
 };
@@ -4048,6 +4361,7 @@ inline bool border_split() { return knobs().border_split != 0; }
 inline bool force_dense_knob() { return knobs().dense == 1; }
 inline int drop_item_knob() { return knobs().debug_drop_item; }
 bool gather_lds_path() { return knobs().gather_lds != 0; }
+inline bool subtree_path() { return knobs().subtree != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -4057,6 +4371,7 @@ constexpr bool border_split() { return true; }
 constexpr bool force_dense_knob() { return false; }
 constexpr int drop_item_knob() { return -1; }
 bool gather_lds_path() { return true; }
+constexpr bool subtree_path() { return true; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -4069,6 +4384,9 @@ struct PlanMeta {
   int m = 0, S = 0, levels = 0, plan_len = 0, n_items = 0, n_tasks = 0, n_parts = 0, nc = 0;
   int nnz = 0;  // off-diagonal blocks (col_ptr[m])
   int off_dfitems = 0, n_dfitems = 0;  // df_factor_kernel dispatch list (appended to the plan image)
+  int n_dfsparse = 0;                  // its sparse-column items (the border items follow)
+  int off_sub = 0, n_sub = 0;          // subtree image (appended), subtrees (subtree_factor_kernel)
+  int64_t sub_lds = 0, sub_bs_lds = 0;  // dynamic LDS bytes: subtree factor, back-substitution
   PlanImage img;  // offsets (data vector cleared after upload)
   // linearize state of this solve call: edge ranks, the task table of the
   // edge range last linearized (host copy stays alive for the async upload)
@@ -4102,6 +4420,8 @@ PlanMeta solve_view(const PlanMeta &M) {
   v.m = M.m, v.S = M.S, v.levels = M.levels, v.plan_len = M.plan_len, v.n_items = M.n_items;
   v.n_tasks = M.n_tasks, v.n_parts = M.n_parts, v.nc = M.nc, v.off_dfitems = M.off_dfitems;
   v.n_dfitems = M.n_dfitems;
+  v.n_dfsparse = M.n_dfsparse, v.off_sub = M.off_sub, v.n_sub = M.n_sub, v.sub_lds = M.sub_lds;
+  v.sub_bs_lds = M.sub_bs_lds;
   v.nnz = M.nnz;
   v.img = M.img;  // offsets (its data vector is empty in the registry)
   v.plan_pending = M.plan_pending;
@@ -4291,6 +4611,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 }
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;
+constexpr int64_t kSubLdsCap = 140 * 1024;  // subtree_factor_kernel's dynamic LDS (+ 8.2 KB static)
 int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st);
 void set_lds_attributes_once();
 
@@ -4415,8 +4736,24 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         F.tail_A = tail;
         F.tail_ld = tld;
         F.Wgr = at<double>(ws, Ly.wgran);
+        if (subtree_path() && meta.n_sub > 0) {
+          // the sparse columns: one LDS workgroup per subtree; df_factor_kernel
+          // then runs only the dense tail's border tasks (if any)
+          SubArgs SA;
+          SA.sub = D.plan + meta.off_sub;
+          SA.L = D.L;
+          SA.Dinv = D.Dinv;
+          SA.y = C.y;
+          SA.sdone = F.sdone;
+          SA.want = meta.epoch + 1;
+          SA.flags = flags;
+          set_lds_attributes_once();
+          subtree_factor_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_lds, st>>>(SA);
+          F.items += meta.n_dfsparse;
+          F.n_items -= meta.n_dfsparse;
+        }
         const int nw = std::max(1, std::min(F.n_items, 1024));
-        df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
+        if (F.n_items > 0) df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
       } else {
 #ifdef M3S_TEST_PATHS
         const int g1 = std::max(1, std::min(C.ncols, 256));
@@ -4452,8 +4789,17 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
         }
       }
-      const int g4 = std::max(1, std::min(C.ncols, 256));
-      col_backsub_kernel<<<g4, 64, 0, st>>>(C);
+      if (subtree_path() && meta.n_sub > 0) {
+        SubBsArgs B;
+        B.sub = D.plan + meta.off_sub;
+        B.ns = meta.n_sub;
+        B.fin_ctr = C.ctr + 5;
+        B.C = C;
+        subtree_backsub_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_bs_lds, st>>>(B);
+      } else {
+        const int g4 = std::max(1, std::min(C.ncols, 256));
+        col_backsub_kernel<<<g4, 64, 0, st>>>(C);
+      }
     } else if (meta.store == 1)
       sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.store == 2)
@@ -4502,6 +4848,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       edge_sums, at<int32_t>(ws, Ly.rank_i), at<int32_t>(ws, Ly.rank_j), a->E, a->Twc, n, ld, A, stop);
   if ((rc = launch_ok())) return rc;
   const int np = (int)n + 1;
+#ifdef M3S_TEST_PATHS
   if (np <= kMaxSmallNp) {
     const int nbc = (np + 31) / 32;
 #define M3S_CHOL(NB)                                                                                   \
@@ -4523,6 +4870,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
 #undef M3S_CHOL
     return launch_ok();
   }
+#endif
+  (void)np;
   const int nt = (int)(ld / kTile);
   for (int kb = 0; kb < nt; kb++) {
     if ((int64_t)kb * kTile >= n) break;
@@ -4571,6 +4920,10 @@ void set_lds_attributes_once() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gn_prologue_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(subtree_factor_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSubLdsCap);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(subtree_backsub_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSubLdsCap);
   });
 }
 
@@ -4601,8 +4954,18 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       img.data.push_back(-1 - k);
       for (int q = 0; q < P.col_ptr[k + 1] - P.col_ptr[k]; q++) img.data.push_back(P.ctask0[k] + q);
     }
+    meta.n_dfsparse = (int)img.data.size() - meta.off_dfitems;
     for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
     meta.n_dfitems = (int)img.data.size() - meta.off_dfitems;
+    if (chip_path) {  // the sparse columns' subtrees, one LDS workgroup each (subtree_factor_kernel)
+      SubtreeImage SI;
+      build_subtree_image(P, kSubLdsCap, SI);
+      meta.off_sub = (int)img.data.size();
+      meta.n_sub = SI.ns;
+      meta.sub_lds = SI.lds_bytes;
+      meta.sub_bs_lds = SI.bs_lds_bytes;
+      img.data.insert(img.data.end(), SI.data.begin(), SI.data.end());
+    }
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
     if (fits && !force_dense) {
       meta.sparse = true;
@@ -4694,6 +5057,16 @@ bool upload_plan(Staging *SG, PlanMeta &M, char *dst, hipStream_t st) {
 void apply_drop_item(PlanMeta &M) {
   const int d = drop_item_knob();
   if (d < 0 || !M.sparse || M.h_plan.empty()) return;
+  if (M.store == 0 && M.n_sub > 0 && subtree_path()) {  // list A of the first subtree
+    int32_t *sub = M.h_plan.data() + M.off_sub;
+    int32_t *rec = sub + sub[1];
+    int32_t *ia = sub + rec[7];
+    if (d < rec[3]) {
+      for (int t = d; t + 1 < rec[3]; t++) ia[t] = ia[t + 1];
+      rec[3] -= 1;
+    }
+    return;
+  }
   if (M.store == 0 && M.n_dfitems > 0) {
     int32_t *di = M.h_plan.data() + M.off_dfitems;
     if (d < M.n_dfitems) {
@@ -4990,6 +5363,35 @@ int gn_prepare_async(const m3s_gn_args *a, hipStream_t st) {
   return M3S_OK;
 }
 
+// In-call launch timing (bench.py's roofline leg, m3s_debug_call_timing):
+// when on, a drop-in call records a timing event on its stream before each
+// linearize launch, after it and after the solve launches of that iteration,
+// so the packed kernel is timed in the call's own launch pattern (behind the
+// previous iteration's solve), not back to back. Kinds: 0 first-iteration
+// (gathering) linearize, 1 packed linearize, 2 solve (every launch of it).
+struct CallTiming {
+  std::mutex mu;
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // pool, reused
+  std::vector<int> kind;       // kind of the span from event q to q + 1 (-1: none)
+  size_t used = 0;
+};
+CallTiming &call_timing() {
+  static CallTiming t;
+  return t;
+}
+bool call_mark(hipStream_t st, int kind_next) {  // caller holds the lock
+  CallTiming &T = call_timing();
+  if (T.used == T.ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return false;
+    T.ev.push_back(e);
+    T.kind.push_back(-1);
+  }
+  T.kind[T.used] = kind_next;
+  return hipEventRecord(T.ev[T.used++], st) == hipSuccess;
+}
+
 int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   int rc = check_args(a);
   if (rc) return rc;
@@ -5005,11 +5407,22 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
     std::lock_guard<std::mutex> g(g_reg_mu);
     sparse = g_reg.at(a->workspace).sparse;
   }
+  CallTiming &CT = call_timing();
+  std::unique_lock<std::mutex> tl(CT.mu, std::defer_lock);
+  bool timing = false;
+  {
+    std::lock_guard<std::mutex> g(CT.mu);
+    timing = CT.on;
+  }
+  if (timing) tl.lock();
   // sparse solve: the linearize kernels finalize each edge themselves
   for (int it = 0; it < a->max_iter; it++) {
     int64_t chunks = 0;  // of this iteration's linearize launch (the dense path reduces its partials)
+    if (timing && !call_mark(st, it == 0 ? 0 : 1)) return M3S_ELAUNCH;
     if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse, &chunks))) return rc;
+    if (timing && !call_mark(st, 2)) return M3S_ELAUNCH;
     if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st, sparse))) return rc;
+    if (timing && !call_mark(st, -1)) return M3S_ELAUNCH;
   }
   return M3S_OK;
 }
@@ -5594,6 +6007,19 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
   return n;
 }
 
+int64_t m3s_subtree_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t *out, int64_t cap,
+                               int64_t *meta) {
+  std::vector<int32_t> a(ri, ri + E), b(rj, rj + E);
+  SparsePlan P;
+  build_sparse_plan(N, a, b, P, 0, 0, dense_tail_min(), false);  // as the chip-wide path builds it
+  SubtreeImage SI;
+  build_subtree_image(P, kSubLdsCap, SI);
+  if (meta) meta[0] = SI.ns, meta[1] = SI.lds_bytes, meta[2] = SI.bs_lds_bytes, meta[3] = P.nc;
+  const int64_t n = (int64_t)SI.data.size();
+  if (out && cap >= n) std::copy(SI.data.begin(), SI.data.end(), out);
+  return n;
+}
+
 // Instrumented builds only (tools/trk_stamps.py, tools/col_stamps.py):
 // which = 0: persistent tracker phase stamps [2][16][8] (-DM3S_TRK_STAMPS);
 // which = 1: column-task stamps [4][2048][4] (-DM3S_COL_STAMPS: factor
@@ -5637,15 +6063,56 @@ int m3s_set_knob(const char *name, int value) {
 #ifdef M3S_TEST_PATHS
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
-             {"gather_lds", &k.gather_lds}
+             {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree}
 #endif
   };
   for (const auto &t : tab)
     if (std::strcmp(t.n, name) == 0) {
       const int old = t.v->exchange(value);
+      // knobs that shape a plan (its schedule, split lists, tail, path) are
+      // not all in the plan-cache key: a change drops every cached plan, so
+      // no launch reads a plan built for another path (e.g. a chip-path
+      // plan, cached unscheduled, on the one-workgroup kernel)
+      static const char *const shaping[] = {"dense_tail_min", "dense", "cols", "df", "tail_cyc",
+                                            "tail_mfma", "border_split", "debug_drop_item", "subtree"};
+      if (old != value)
+        for (const char *sn : shaping)
+          if (std::strcmp(sn, name) == 0) {
+            std::lock_guard<std::mutex> g(g_cache_mu);
+            g_cache.clear();
+            break;
+          }
       return old;
     }
   return -(1 << 30);
+}
+
+int m3s_debug_call_timing(int enable) {
+  CallTiming &T = call_timing();
+  std::lock_guard<std::mutex> g(T.mu);
+  T.on = enable != 0;
+  T.used = 0;
+  return M3S_OK;
+}
+
+int m3s_debug_call_times(float *ms, int32_t *kinds, int cap) {
+  CallTiming &T = call_timing();
+  std::lock_guard<std::mutex> g(T.mu);
+  if (T.used == 0) return 0;
+  if (hipEventSynchronize(T.ev[T.used - 1]) != hipSuccess) return M3S_ELAUNCH;
+  int n = 0;
+  for (size_t q = 0; q + 1 < T.used; q++) {
+    if (T.kind[q] < 0) continue;
+    if (n < cap) {
+      float t = 0.0f;
+      if (hipEventElapsedTime(&t, T.ev[q], T.ev[q + 1]) != hipSuccess) return M3S_ELAUNCH;
+      ms[n] = t;
+      kinds[n] = T.kind[q];
+    }
+    n++;
+  }
+  T.used = 0;
+  return n;
 }
 
 int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void *stream) {

@@ -374,13 +374,15 @@ def test_gn_input_checks(be, graph_small):
 
 
 @pytest.mark.parametrize("N", [33, 70])
-def test_gn_tiled_cholesky_path_matches_oracle(be, N):
-    """7(N-1)+1 > 224: the tiled 64x64 fp64 Cholesky + blocked back-substitution.
-    One step from identical inputs is tight; after 3 steps the fp32 H/g noise
-    (x cond(H)) has moved the linearisation point, so poses get the
-    step-scaled tolerance."""
+def test_gn_tiled_cholesky_path_matches_oracle(test_lib, be, knobs, N):
+    """The dense fallback forced on (test build, knob dense=1) at 7(N-1)+1 >
+    224: the tiled 64x64 fp64 Cholesky + blocked back-substitution. One step
+    from identical inputs is tight; after 3 steps the fp32 H/g noise (x
+    cond(H)) has moved the linearisation point, so poses get the step-scaled
+    tolerance."""
     from mast3r_slam_amd import synthetic
 
+    knobs("dense", 1)
     g = synthetic.make_graph(N, 24, 32, seed=40 + N)
     _, dx1_gpu, _ = run_gpu(be, "rays", g, 1, 0.0)
     _, dx1_ref, _, _ = run_oracle("rays", g, 1, 0.0)
@@ -391,7 +393,35 @@ def test_gn_tiled_cholesky_path_matches_oracle(be, N):
     np.testing.assert_allclose(T_gpu, T_ref, atol=1e-5 + 3e-4 * np.abs(dx1_ref).max())
 
 
-def test_gn_tiled_cholesky_singular_zero_dx(be):
+def test_gn_over_capacity_plan_takes_dense_fallback(be):
+    """The product library's own dense fallback: a complete graph of 201
+    keyframes fills all m (m + 1) / 2 = 20100 blocks of its factor, more than
+    the workspace's sparse-slot capacity (64 m + 4096 + 1), so the call solves
+    by the tiled fp64 Cholesky (n = 1400) instead of the block-sparse LLT;
+    against the oracle's dense fp64 solve (gn_kernels.cu:57-159 builds the same
+    system as triplets). One step tight, then 2 iterations at the step-scaled
+    tolerance."""
+    from mast3r_slam_amd import synthetic
+
+    N = 201
+    ii_u = [i for j in range(N) for i in range(j)]
+    jj_u = [j for j in range(N) for i in range(j)]
+    g = synthetic.make_graph(N, 8, 12, seed=45, edges=(ii_u, jj_u))
+    m = N - 1
+    assert m * (m + 1) // 2 > 64 * m + 4096 + 1
+    _, dx1_gpu, info1 = run_gpu(be, "rays", g, 1, 0.0)
+    _, dx1_ref, _, failed = run_oracle("rays", g, 1, 0.0)
+    assert failed == 0 and info1[be.INFO_SOLVE_FAIL] == 0
+    np.testing.assert_allclose(dx1_gpu, dx1_ref, atol=1e-6 + 1e-4 * np.abs(dx1_ref).max())
+    T_gpu, _, info = run_gpu(be, "rays", g, 2, 0.0)
+    T_ref, _, it, _ = run_oracle("rays", g, 2, 0.0)
+    assert info[be.INFO_ITERS] == it == 2
+    np.testing.assert_allclose(T_gpu, T_ref, atol=1e-5 + 3e-4 * np.abs(dx1_ref).max())
+
+
+def test_gn_singular_global_factor_zero_dx(be):
+    """As above at 40 KFs: every iteration's block-sparse LLT fails, dx = 0,
+    poses untouched."""
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(40, 12, 16, seed=77)
@@ -482,6 +512,25 @@ def test_block_dataflow_matches_column_tasks_bitwise(test_lib, be, N, knobs):
     np.testing.assert_array_equal(T_a, T_b)
 
 
+@pytest.mark.parametrize("N", [90, 140, 256, 400])
+def test_subtree_factor_matches_block_dataflow_bitwise(test_lib, be, N, knobs):
+    """Large graphs (round 4): the sparse columns below the dense tail factored
+    as subtrees, one LDS workgroup each (subtree_factor_kernel, the default),
+    against df_factor_kernel's chip-wide dataflow over the same columns (test
+    knob subtree=0). Both run every block's update list in the global plan's
+    order with the same per-block arithmetic: poses and dx agree bitwise."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 12, 16, seed=750 + N)
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    knobs("subtree", "0")
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
+    np.testing.assert_array_equal(dx_a, dx_b)
+    np.testing.assert_array_equal(T_a, T_b)
+
+
 @pytest.mark.parametrize("N", [140, 256, 400])
 def test_tail_over_workgroups_matches_one_workgroup(test_lib, be, N, knobs):
     """The dense tail with one workgroup per tile column (tail_cyc_kernel, the
@@ -510,13 +559,20 @@ def test_tail_over_workgroups_matches_one_workgroup(test_lib, be, N, knobs):
 def test_gn_partial_trip_pixel_count_matches_oracle(be, mode):
     """HW = 20 x 52 = 1040 pixels: a multiple of 4 (the vector, packed and
     pipelined gathering paths) but not of a 1024-pixel trip, so the last trip
-    of the last chunk is partial: its lanes past the end take no part and the
-    buffer resources read zeros past HW."""
+    of the last chunk is partial: its lanes past the end take no part and their
+    LDS-DMA loads take an offset past the buffer range (zeros, no access).
+    The pointmaps sit at the very end of their own allocation (a fresh 12-MiB
+    segment of the caching allocator), so the last keyframe's partial trip
+    has no bytes of the allocation left behind it to read."""
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(6, 20, 52, seed=37)
     Xs = constrained(g) if mode == "calib" else g.Xs
-    T_gpu, dx_gpu, info = run_gpu(be, mode, g, 5, 0.0, Xs=Xs)
+    buf = torch.empty(3 << 20, dtype=torch.float32, device=DEV)
+    Xs_end = buf[buf.numel() - Xs.numel():].view(Xs.shape)
+    Xs_end.copy_(Xs.to(DEV))
+    assert Xs_end.data_ptr() + 4 * Xs.numel() == buf.data_ptr() + 4 * buf.numel()
+    T_gpu, dx_gpu, info = run_gpu(be, mode, g, 5, 0.0, Xs=Xs_end)
     T_ref, dx_ref, it, failed = run_oracle(mode, g, 5, 0.0, Xs=Xs)
     assert info[be.INFO_ITERS] == it == 5
     assert info[be.INFO_SOLVE_FAIL] == failed == 0

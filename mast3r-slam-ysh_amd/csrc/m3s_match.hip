@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "m3s_gn.h"
 #include "m3s_match.h"
@@ -24,6 +25,15 @@ namespace {
 constexpr int kMatchThreads = 256;
 
 inline int launch_status() { return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH; }
+
+// M3S_REFINE_STAGED=0: refine_matches on the round-3 global-read kernel (A/B)
+bool refine_staged_knob() {
+  static const bool on = [] {
+    const char *e = std::getenv("M3S_REFINE_STAGED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 
 // ------------------------------------------------------------ iter_proj --
 #pragma clang fp contract(off)
@@ -199,8 +209,173 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
   A.p1_new[2 * gid + 1] = v_new;
 }
 
+// Round 4: the window rows staged in LDS. A workgroup takes a 16 x 16 tile of
+// query pixels (N = H W, query n = pixel (n % W, n / W) of image 2, whose
+// matches p1 in image 1 move smoothly, so their windows overlap) or 256
+// consecutive queries otherwise. Per dilation d (dilation_max .. 1) the
+// workgroup reduces the bounding box of its current windows (centres +-
+// radius d, clipped to the image), copies those D11 pixels into LDS with
+// coalesced 16-B loads (rows of the box are contiguous in D11), and every
+// lane scores its candidates from LDS; a candidate outside the box (a box too
+// large for LDS is not staged at all) reads D11 directly. Each score is the
+// same fp16 FMA chain in feature order and candidates keep the scan order and
+// strict comparison, so the integer result is bitwise the global kernel's.
+// (matching_kernels.cu:25-81.)
+constexpr int kRefTile = 16;
+constexpr int kRefLdsBytes = 144 * 1024;
+
+template <typename T, int FMAX>
+__global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_args A, int tiles_x, int tiles_per_b,
+                                                                   int tiled) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+  __shared__ int red[4];
+  constexpr int VB = FMAX * (int)sizeof(T);  // bytes per pixel (a multiple of 16)
+  static_assert(VB % 16 == 0, "16-B vectors per pixel");
+  constexpr int NV = VB / 16;
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x / tiles_per_b;
+  const int tb = (int)(blockIdx.x - b * tiles_per_b);
+  const int64_t H = A.H, W = A.W;
+  int64_t n;
+  bool valid;
+  if (tiled) {
+    const int x = (tb % tiles_x) * kRefTile + tid % kRefTile, y = (tb / tiles_x) * kRefTile + tid / kRefTile;
+    valid = x < W && y < H;
+    n = (int64_t)y * W + x;
+  } else {
+    n = (int64_t)tb * kMatchThreads + tid;
+    valid = n < A.N;
+  }
+  const int64_t gid = b * A.N + n;
+  const T *D11 = static_cast<const T *>(A.D11) + b * H * W * FMAX;
+  T q[FMAX];
+  int64_t u0 = 0, v0 = 0;
+  if (valid) {
+    const T *d21 = static_cast<const T *>(A.D21) + gid * FMAX;
+#pragma unroll
+    for (int k = 0; k < FMAX; k++) q[k] = d21[k];
+    u0 = A.p1[2 * gid], v0 = A.p1[2 * gid + 1];
+  }
+  T max_score = min_normal<T>();
+  int64_t u_new = u0, v_new = v0;
+  const int cap_px = kRefLdsBytes / VB;
+  for (int d = A.dilation_max; d > 0; d--) {
+    const int rd = A.radius * d;
+    // the box of this dilation's windows (ints: image coordinates fit)
+    if (tid == 0) red[0] = INT32_MAX, red[1] = INT32_MIN, red[2] = INT32_MAX, red[3] = INT32_MIN;
+    __syncthreads();
+    if (valid) {
+      const int ui = (int)max<int64_t>(min<int64_t>(u0, INT32_MAX / 2), INT32_MIN / 2);
+      const int vi = (int)max<int64_t>(min<int64_t>(v0, INT32_MAX / 2), INT32_MIN / 2);
+      atomicMin(&red[0], ui), atomicMax(&red[1], ui), atomicMin(&red[2], vi), atomicMax(&red[3], vi);
+    }
+    __syncthreads();
+    const int64_t bx0 = max<int64_t>((int64_t)red[0] - rd, 0), bx1 = min<int64_t>((int64_t)red[1] + rd, W - 1);
+    const int64_t by0 = max<int64_t>((int64_t)red[2] - rd, 0), by1 = min<int64_t>((int64_t)red[3] + rd, H - 1);
+    const int64_t bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+    const bool staged = bw > 0 && bh > 0 && bw * bh <= cap_px;
+    __syncthreads();  // red read by every lane before the next dilation rewrites it
+    if (staged) {
+      const int nvec = (int)(bw * bh) * NV;
+      const uint4 *src = reinterpret_cast<const uint4 *>(D11);
+      uint4 *dst = reinterpret_cast<uint4 *>(rsm);
+      for (int i0 = 0; i0 < nvec; i0 += 8 * kMatchThreads) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int i = i0 + u * kMatchThreads + tid;
+          if (i < nvec) {
+            const int px = i / NV, c = i - px * NV;
+            const int64_t yy = by0 + px / bw, xx = bx0 + px % bw;
+            v[u] = src[(yy * W + xx) * NV + c];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int i = i0 + u * kMatchThreads + tid;
+          if (i < nvec) dst[i] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      // candidates in scan order (u offset outer, v inner), four v offsets at a
+      // time: their FMA chains run interleaved, then they are compared in order
+      const int nw = 2 * A.radius + 1;
+      constexpr int G = 4;
+      constexpr int EV = 16 / (int)sizeof(T);  // elements per 16-B vector
+      for (int i = 0; i < nw; i++) {
+        const int64_t u = u0 - rd + (int64_t)i * d;
+        for (int j0 = 0; j0 < nw; j0 += G) {
+          T x[G][FMAX];
+          bool ok[G];
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const int64_t v = v0 - rd + (int64_t)(j0 + g) * d;
+            ok[g] = j0 + g < nw && v >= 0 && v < H && u >= 0 && u < W;
+            const bool in_box = staged && u >= bx0 && u <= bx1 && v >= by0 && v <= by1;
+            const uint4 *pv;
+            if (in_box)
+              pv = reinterpret_cast<const uint4 *>(rsm) + ((v - by0) * bw + (u - bx0)) * NV;
+            else  // (a candidate outside the image reads pixel 0 and is discarded)
+              pv = reinterpret_cast<const uint4 *>(D11 + (ok[g] ? (v * W + u) * FMAX : 0));
+#pragma unroll
+            for (int c = 0; c < NV; c++) *reinterpret_cast<uint4 *>(&x[g][c * EV]) = pv[c];
+          }
+          T score[G];
+#pragma unroll
+          for (int g = 0; g < G; g++) score[g] = (T)0.0f;
+#pragma unroll
+          for (int k = 0; k < FMAX; k++)
+#pragma unroll
+            for (int g = 0; g < G; g++) score[g] = __builtin_elementwise_fma(q[k], x[g][k], score[g]);
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (ok[g] && score[g] > max_score) {
+              max_score = score[g];
+              u_new = u;
+              v_new = v0 - rd + (int64_t)(j0 + g) * d;
+            }
+          }
+        }
+      }
+    }
+    u0 = u_new;
+    v0 = v_new;
+    __syncthreads();  // the box is read before the next dilation restages it
+  }
+  if (valid) {
+    A.p1_new[2 * gid] = u_new;
+    A.p1_new[2 * gid + 1] = v_new;
+  }
+}
+
 template <typename T>
 int launch_refine(const m3s_refine_args &a, hipStream_t st) {
+  // LDS-staged windows for 16-B multiples of descriptor bytes (f16: F = 8k)
+  const bool vec = (a.F * (int64_t)sizeof(T)) % 16 == 0 && (a.F == 16 || a.F == 24 || a.F == 32) &&
+                   reinterpret_cast<uintptr_t>(a.D11) % 16 == 0;
+  if (vec && refine_staged_knob()) {
+    const bool tiled = a.N == a.H * a.W;
+    const int tiles_x = (int)((a.W + kRefTile - 1) / kRefTile);
+    const int tiles_per_b = tiled ? tiles_x * (int)((a.H + kRefTile - 1) / kRefTile)
+                                  : (int)((a.N + kMatchThreads - 1) / kMatchThreads);
+    const unsigned blocks = (unsigned)(a.B * tiles_per_b);
+    static bool attr = false;
+    if (!attr) {
+      for (const void *f : {reinterpret_cast<const void *>(refine_lds_kernel<T, 16>),
+                            reinterpret_cast<const void *>(refine_lds_kernel<T, 24>),
+                            reinterpret_cast<const void *>(refine_lds_kernel<T, 32>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRefLdsBytes);
+      attr = true;
+    }
+    switch (a.F) {
+      case 16: refine_lds_kernel<T, 16><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+      case 24: refine_lds_kernel<T, 24><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+      default: refine_lds_kernel<T, 32><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+    }
+    return launch_status();
+  }
   const unsigned blocks = (unsigned)((a.B * a.N + kMatchThreads - 1) / kMatchThreads);
   switch (a.F) {  // descriptor width in registers for the common sizes
     case 16: refine_kernel<T, 16><<<blocks, kMatchThreads, 0, st>>>(a); break;

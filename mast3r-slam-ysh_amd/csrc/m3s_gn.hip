@@ -1057,6 +1057,10 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
       act(Tm, Xj[s4], Y);
       pixel_contrib<MODE>(acc, P, in[s4], Y);
     }
+    // NPL plane stores after the refill: the loop top's counted vmcnt(NPL)
+    // relies on at least NPL vector-memory operations following the refill's
+    // 8 LDS-DMA loads on every path back to it (tests/test_isa.py checks the
+    // disassembly of the built library)
 #pragma unroll
     for (int k = 0; k < NPL; k++) {
       const f32x4 v = {in[0].v[k], in[1].v[k], in[2].v[k], in[3].v[k]};
@@ -2781,6 +2785,8 @@ struct SubArgs {
   int32_t *sdone;        // [S] slot epoch flags (diagonal slot k: W_k and y_k)
   int want;
   int32_t *flags;
+  double *Wgr;           // [m][49] W_k as tagged granules (df_factor_kernel's border OFF items read them)
+  int m;
 };
 constexpr int kSubWaves = 16;
 
@@ -2846,13 +2852,37 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs 
   double *Bl = reinterpret_cast<double *>(yfl + ncol + ((nblk + 2 * ncol) & 1));  // 8-B aligned
   for (int q = tid; q < nblk + 2 * ncol; q += 64 * kSubWaves) bfl[q] = 0;
   if (tid == 0) tk[0] = 0, tk[1] = 0, fail_s = 0;
+  double *L = A.L;
+  // the assembled values (assemble_slots_kernel) of the LDS blocks, the
+  // diagonal blocks (into the W area, which DIAG(c) overwrites with W_k) and
+  // the RHS (into y), every load of a batch in flight: no item then waits on
+  // a global load of its own input
+  {
+    const int nb49 = nlds * 49, nd49 = ncol * 49, ny = ncol * 7, tot = nb49 + nd49 + ny;
+    for (int i0 = 0; i0 < tot; i0 += 8 * 64 * kSubWaves) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * 64 * kSubWaves + tid;
+        if (i < nb49) v[u] = L[(size_t)gsl[i / 49] * 49 + i % 49];
+        else if (i < nb49 + nd49) v[u] = L[(size_t)cols[(i - nb49) / 49] * 49 + (i - nb49) % 49];
+        else if (i < tot) v[u] = A.y[(size_t)cols[(i - nb49 - nd49) / 7] * 7 + (i - nb49 - nd49) % 7];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * 64 * kSubWaves + tid;
+        if (i < nb49) Bl[i] = v[u];
+        else if (i < nb49 + nd49) Wl[i - nb49] = v[u];
+        else if (i < tot) yl[i - nb49 - nd49] = v[u];
+      }
+    }
+  }
   __syncthreads();
   const int r = lane / 7, c = lane % 7;
   const bool act49 = lane < 49;
   const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
   const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
   double *scr = wsc[wave];
-  double *L = A.L;
   // lists: waves [0, nwA) start on A (DIAG + internal OFF), the others on B
   // (border OFF); an exhausted list sends its waves to the other one. A items
   // never wait for B items, so A always completes, then B.
@@ -2869,16 +2899,19 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs 
     const int code = lst ? itB[t] : itA[t];
     if (code < 0) {  // DIAG(c): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
       const int cc = -1 - code, k = cols[cc];
-      double v = L[(size_t)k * 49 + lane49];  // assembled (assemble_slots_kernel)
+      if (lane == 0) M3S_CSTAMP(0, k, 0);
+      double v = Wl[cc * 49 + lane49];  // assembled D_k (staged)
       const int q0 = dptr[cc], q1 = dptr[cc + 1];
       M3S_POLL(q0, q1, flag_set(&bfl[dlist[2 * q]]), (v = sub_upd_diag(v, Bl, L, gsl, nlds, dlist, qa, qb, r7, c7)));
+      if (lane == 0) M3S_CSTAMP(0, k, 1);
       double wcol[7];
       const bool bad = diag_factor<true>(v, k, L, A.Dinv, scr, lane, l7, wcol, Wl + (size_t)cc * 49);
       if (bad && lane == 0) set_fail(A.flags);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&wfl[cc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) M3S_CSTAMP(0, k, 2);
       // forward step y_k = W_k (b_k - sum_p L_kp y_p)
-      double bb = A.y[(size_t)k * 7 + lane7];
+      double bb = yl[cc * 7 + lane7];  // b_k (staged)
       M3S_POLL(q0, q1, flag_set(&yfl[dlist[2 * q + 1]]), (bb = sub_upd_fwd(bb, Bl, L, gsl, nlds, dlist, yl, qa, qb, l7)));
       // y_k = W_k bb (fwd_solve_store's sums), to LDS and the global RHS
       if (lane < 7) {
@@ -2896,15 +2929,29 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs 
       wave_lds_fence();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&yfl[cc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L_kk, W_k, y_k stores have left
-      if (lane == 0) __hip_atomic_store(A.sdone + k, A.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < 7) {
+        // W_k as tagged granules for the border-row OFF items (df_factor_kernel,
+        // the next launch; the global slot flags are set at this kernel's end)
+        const __amdgpu_buffer_rsrc_t RG =
+            __builtin_amdgcn_make_buffer_rsrc(A.Wgr, 0, (int)(16 * 49 * (A.m + 1)), 0x00020000);
+#pragma unroll
+        for (int qq = 0; qq < 7; qq++) {
+          const unsigned long long bw = (unsigned long long)__double_as_longlong(wcol[qq]);
+          const u32x4 gw = {(unsigned)(bw & 0xffffffffu), (unsigned)(bw >> 32), (unsigned)A.want, 0u};
+          __builtin_amdgcn_raw_buffer_store_b128(gw, RG, (k * 49 + qq * 7 + lane) * 16, 0, 16);
+        }
+      }
+      if (lane == 0) M3S_CSTAMP(0, k, 3);
     } else {  // OFF(b): L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
       const int b = code, cc = tcol[b], dst = gsl[b];
-      double v = L[(size_t)dst * 49 + lane49];  // assembled A_ik
+      if (lane == 0) M3S_CSTAMP(3, dst, 0);
+      double v = b < nlds ? Bl[b * 49 + lane49] : L[(size_t)dst * 49 + lane49];  // assembled A_ik (staged)
       const int q0 = tptr[b], q1 = tptr[b + 1];
       M3S_POLL(q0, q1, flag_set(&bfl[tlist[2 * q]]) && flag_set(&bfl[tlist[2 * q + 1]]),
                (v = sub_upd_off(v, Bl, L, gsl, nlds, tlist, qa, qb, r7, c7)));
+      if (lane == 0) M3S_CSTAMP(3, dst, 1);
       wait_flag(&wfl[cc], &fail_s);  // W_k
+      if (lane == 0) M3S_CSTAMP(3, dst, 2);
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -2915,15 +2962,25 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs 
         if (b < nlds) Bl[b * 49 + lane] = x;
         st_sc1(L + (size_t)dst * 49 + lane, x);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the global copy has left (global-only blocks are read from it)
+      // a block in LDS is published at once; a global-only block once its
+      // write-through copy has left (other waves read it with sc1 loads)
+      if (b >= nlds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) {
         __hip_atomic_store(&bfl[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(A.sdone + dst, A.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        M3S_CSTAMP(3, dst, 3);
       }
     }
   }
+  // every internal block, W_k and y_k of this subtree is final: the global
+  // slot flags that df_factor_kernel's border items poll (next launch; the
+  // border blocks themselves are its items, so their flags stay unset)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  const int n_int = rec[19];
+  for (int b = tid; b < n_int + ncol; b += 64 * kSubWaves)
+    __hip_atomic_store(A.sdone + (b < n_int ? gsl[b] : cols[b - n_int]), A.want, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0 && fail_s) set_fail(A.flags);
 }
 
@@ -3040,6 +3097,7 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsAr
     for (int mm = 0; mm < 7; mm++) t0 += Lb[mm * 7 + l] * xi[mm];
     tb[i] = t0;
   }
+  for (int i = tid; i < ncol * 7; i += 1024) xl[i] = C.y[(size_t)cols[i / 7] * 7 + i % 7];  // y_k (x_k later)
   for (int q = tid; q < ncol; q += 1024) xfl[q] = 0;
   if (tid == 0) tk = 0, last_s = 0, fail_s = 0;
   __syncthreads();
@@ -3048,7 +3106,8 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsAr
     const int t = wave_ticket(&tk);
     if (t >= ncol) break;
     const int c = corder[ncol - 1 - t], k = cols[c];
-    double rr = C.y[(size_t)k * 7 + lane7];
+    if (lane == 0) M3S_CSTAMP(1, k, 0);
+    double rr = xl[c * 7 + lane7];  // y_k (staged)
     for (int b = ci[c]; b < ci[c + 1]; b++) {
       const int pc = brow[b];
       wait_flag(&xfl[pc], &fail_s);
@@ -3063,6 +3122,7 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsAr
       }
       rr -= t0;
     }
+    if (lane == 0) M3S_CSTAMP(1, k, 1);
     for (int b = cb[c]; b < cb[c + 1]; b++) rr -= tb[(b - n_int) * 7 + lane7];
     double xk = 0.0;
 #pragma unroll
@@ -3073,6 +3133,7 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsAr
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(&xfl[c], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) M3S_CSTAMP(1, k, 2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's x stores have left
   __syncthreads();
@@ -3530,6 +3591,162 @@ __device__ __forceinline__ void gran_store(__amdgpu_buffer_rsrc_t R, int tile, i
   }
 }
 
+// The last workgroup of a tail launch: back-substitution L^T x = y' over the
+// published tiles (after every column flag), x of the tail columns to A.rhs.
+__device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSync &S, double *yv, double *xv) {
+  const int n = 7 * A.nc;
+  const int TC = (n + 15) / 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int want = S.epoch + 1;
+  double *Wg = A.Wg;
+  // The last workgroup: back-substitution L^T x = y' over the published tiles
+  // (every column k < J was waited for above). Wave w owns the tile rows
+  // J' = w (mod 4) of y' (it alone updates them); x_K is formed by the owner
+  // of row K as soon as its own updates from x_{K+1..} are in, then handed to
+  // the other waves through LDS with a flag: no workgroup barrier per step.
+  // The same sums in the same order as tail_llt_kernel's loop.
+  __shared__ int xflag[kTailMaxT];
+  if (wave == 0) {  // every column's W, y' and LgT tiles are out (column flags, one per lane)
+    int spins = 0;
+    while (__ballot(lane < TC && __hip_atomic_load(S.tflag + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kColSpins) {
+        if (lane == 0) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) M3S_CSTAMP(2, 698, 0);
+  // every W_K^T to LDS (rows padded to 17: conflict-free column reads)
+  __shared__ double WlT[kTailMaxT * 16 * 17];
+  {  // all loads in flight at once (16-B sc1 buffer loads; out of range past TC reads zeros)
+    constexpr int kWL = kTailMaxT * 256 / (2 * 64 * kTailNW);
+    const __amdgpu_buffer_rsrc_t RW = __builtin_amdgcn_make_buffer_rsrc(Wg, 0, kTailMaxT * 256 * 8, 0x00020000);
+    u32x4 wv[kWL];
+#pragma unroll
+    for (int i = 0; i < kWL; i++) {
+      const int q2 = 2 * (tid + 64 * kTailNW * i);
+      wv[i] = __builtin_amdgcn_raw_buffer_load_b128(RW, q2 < 256 * TC ? q2 * 8 : 0x7fffff00, 0, 16);
+    }
+    double yl[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int q = tid + 64 * kTailNW * i;
+      yl[i] = q < 16 * TC ? ld_sc1(S.ypg + q) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kWL; i++) {
+      const int q2 = 2 * (tid + 64 * kTailNW * i);
+      WlT[(q2 >> 4) * 17 + (q2 & 15)] = __longlong_as_double((long long)(((unsigned long long)wv[i].y << 32) | wv[i].x));
+      WlT[(q2 >> 4) * 17 + (q2 & 15) + 1] =
+          __longlong_as_double((long long)(((unsigned long long)wv[i].w << 32) | wv[i].z));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int q = tid + 64 * kTailNW * i;
+      if (q < 16 * TC) yv[q] = yl[i];
+    }
+  }
+  for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) xv[q] = 0.0;
+  if (tid < kTailMaxT) xflag[tid] = 0;
+  __syncthreads();
+  // y_J -= L(K, J)^T x_K from the LgT tile (operand order: 32 B per lane).
+  // The operands of the next step are in flight while this one runs: every
+  // load is a 16-B sc1 buffer load issued unconditionally (rows a step does
+  // not need read out of range, which returns zeros without a memory access),
+  // so each step issues the same number of loads and the compiler waits for
+  // exactly the older step's (24 per wave, two steps = 48 < the 63 vmcnt).
+  // Per step K the owner of row K - 1 applies x_K to that row first and forms
+  // x_{K-1} at once (the chain per step is one tile update + one 16-term
+  // dot product), then applies x_K to its other rows. Each row still takes
+  // its updates in decreasing K (the same sums).
+  constexpr int kTW = (kTailMaxT + kTailNW - 1) / kTailNW;  // tile rows J' of one wave
+  constexpr int kRing = 3;
+  const __amdgpu_buffer_rsrc_t RT =
+      __builtin_amdgcn_make_buffer_rsrc(S.LgT, 0, kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 8, 0x00020000);
+  constexpr int kFar = 0x7fffff00;  // out of range
+  f64x4 lt[kRing][kTW];
+  auto ld2 = [&](int off, double &x0, double &x1) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(RT, off, 0, 16);
+    x0 = __longlong_as_double((long long)(((unsigned long long)v.y << 32) | v.x));
+    x1 = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
+  };
+  auto bs_load = [&](int K, int slot) {
+#pragma unroll
+    for (int t = 0; t < kTW; t++) {
+      const int Jc = wave + kTailNW * t;
+      const int off = (K >= 0 && Jc < K) ? (tail_tile(K, Jc) * 256 + 4 * lane) * 8 : kFar;
+      double x0, x1, x2, x3;
+      ld2(off, x0, x1);
+      ld2(off + 16, x2, x3);
+      lt[slot][t] = f64x4{x0, x1, x2, x3};
+    }
+  };
+  auto form_x = [&](int K) {  // the owner of row K, all of whose updates are in
+    const int jv = min(16, n - 16 * K);
+    if (lane < 16) {
+      double x = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; i++) x += WlT[(K * 16 + lane) * 17 + i] * yv[16 * K + i];
+      xv[16 * K + lane] = lane < jv ? x : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) M3S_CSTAMP(2, 700 + K, 0);
+  };
+#pragma unroll
+  for (int d = 0; d < kRing; d++) bs_load(TC - 1 - d, d);
+  if (tid == 0) M3S_CSTAMP(2, 699, 0);
+  if ((TC - 1) % kTailNW == wave) form_x(TC - 1);
+  for (int K0 = TC - 1; K0 >= 0; K0 -= kRing) {
+#pragma unroll
+    for (int d = 0; d < kRing; d++) {
+      const int K = K0 - d;
+      if (K >= 0) {
+        if (K % kTailNW != wave) {  // (the owner formed x_K itself, in the step before)
+          int spins = 0;
+          while (__hip_atomic_load(xflag + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
+                 spins < (1 << 22))
+            spins++;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        double xb[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) xb[q] = xv[16 * K + 4 * q + lk];
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+          for (int t = 0; t < kTW; t++) {
+            const int Jc = wave + kTailNW * t;
+            if (pass == 0 ? Jc == K - 1 : Jc < K - 1) {
+              // (L^T x)[m], m = lr: lane l holds L(K,Jc)^T[lr][lk + 4q]; the 4 lanes of
+              // one m add their partial sums (VALU: the MFMA form spent 15/16 of its work
+              // on copies of x)
+              double u = 0.0;
+#pragma unroll
+              for (int q = 0; q < 4; q++) u += lt[d][t][q] * xb[q];
+              u += __shfl_xor(u, 16);
+              u += __shfl_xor(u, 32);
+              if (lane < 16) yv[16 * Jc + lane] -= u;
+              if (pass == 0) {
+                wave_lds_fence();  // row K - 1's y' before this wave reads it
+                form_x(K - 1);
+              }
+            }
+          }
+        }
+        wave_lds_fence();
+      }
+      bs_load(K - kRing, d);
+    }
+  }
+  __syncthreads();  // every x_K
+  for (int j = tid; j < n; j += 64 * kTailNW) A.rhs[7 * A.c0 + j] = xv[j];
+  if (tid == 0) M3S_CSTAMP(2, 511, 0);
+}
+
 // Round 2: the L tiles go from workgroup to workgroup as tagged granules
 // (one hop = one store + one polled load), the panel follows the updates
 // without a workgroup barrier (waves 1..3 wait for W_J on an LDS flag), and
@@ -3705,151 +3922,298 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     M3S_CSTAMP(2, J, 3);
   }
   if (J != TC - 1) return;
-  // The last workgroup: back-substitution L^T x = y' over the published tiles
-  // (every column k < J was waited for above). Wave w owns the tile rows
-  // J' = w (mod 4) of y' (it alone updates them); x_K is formed by the owner
-  // of row K as soon as its own updates from x_{K+1..} are in, then handed to
-  // the other waves through LDS with a flag: no workgroup barrier per step.
-  // The same sums in the same order as tail_llt_kernel's loop.
-  __shared__ int xflag[kTailMaxT];
-  if (wave == 0) {  // every column's W, y' and LgT tiles are out (column flags, one per lane)
+  tail_backsub_wg(A, S, yv, xv);
+}
+
+
+// Round 4: two tile columns per workgroup (J0 = 2 b, J1 = J0 + 1). The
+// chain per tile column of tail_cyc_kernel is a hand-off (~1.3 us) + the
+// diagonal factor (~2.4 us) + a panel tile; here the second column of a pair
+// takes its sub-diagonal panel tile L(J1, J0) and the update of its diagonal
+// from the first column inside the workgroup (wave 0, no hand-off), so the
+// chain has one hand-off per two columns. Wave 0 holds the tiles (J0, J0),
+// (J1, J0), (J1, J1); waves 1..3 the rows below, I = J1 + w + 3 u, for both
+// columns. Per tile the same updates in the same order as tail_cyc_kernel
+// (columns k ascending, then the pair's own first column): bitwise the same
+// factor; the back-substitution is the same code (tail_backsub_wg).
+__global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, TailSync S) {
+  if (A.flags[kFlagStop]) return;
+  __shared__ double Wk[2][16][17];
+  __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
+  __shared__ f64x4 Lsub[64];  // L(J1, J0) in operand order (waves 1..3 update their J1 tiles with it)
+  __shared__ int fail_s, wready[2], lready;
+  const int n = 7 * A.nc;
+  const int TC = (n + 15) / 16, TR = (n + 16) / 16;
+  const int In = n / 16, rn = n - 16 * In;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int J0 = 2 * (int)blockIdx.x, jn = min(2, TC - J0), J1 = J0 + 1, Jl = J0 + jn - 1;
+  const int want = S.epoch + 1;
+  double *Wg = A.Wg;
+  const __amdgpu_buffer_rsrc_t R = gran_rsrc(S.LgG);
+  constexpr int kRC = (kTailMaxT + 2) / 3;
+  auto rowI = [&](int u) { return wave == 0 ? (u < jn ? J0 + u : -1) : Jl + wave + 3 * u; };
+  auto live = [&](int u) {
+    const int I = rowI(u);
+    return I >= 0 && I < TR;
+  };
+  if (tid == 0) fail_s = 0, wready[0] = 0, wready[1] = 0, lready = 0;
+  for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) yv[q] = 0.0;
+  __syncthreads();
+  // acc0[u]: tile (I, J0)^T; acc1[u]: tile (I, J1)^T (rows I >= J1)
+  f64x4 acc0[kRC], acc1[kRC];
+#pragma unroll
+  for (int u = 0; u < kRC; u++) {
+    f64x4 v0 = {0.0, 0.0, 0.0, 0.0}, v1 = {0.0, 0.0, 0.0, 0.0};
+    if (live(u)) {
+      const int I = rowI(u);
+#pragma unroll
+      for (int r = 0; r < 4; r++) v0[r] = tail_entry(A, n, 16 * I + lr, 16 * J0 + lk + 4 * r);
+      if (jn == 2 && I >= J1) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) v1[r] = tail_entry(A, n, 16 * I + lr, 16 * J1 + lk + 4 * r);
+      }
+    }
+    acc0[u] = v0;
+    acc1[u] = v1;
+  }
+  auto poll_tile = [&](int t, GranTile &g) {
     int spins = 0;
-    while (__ballot(lane < TC && __hip_atomic_load(S.tflag + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want)) {
+    for (;;) {
+      gran_load(R, t, lane, g);
+      if (gran_ready(g, want)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > kColSpins) {
-        if (lane == 0) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) fail_s = 1;
         break;
       }
     }
-  }
-  __syncthreads();
-  if (tid == 0) M3S_CSTAMP(2, 698, 0);
-  // every W_K^T to LDS (rows padded to 17: conflict-free column reads)
-  __shared__ double WlT[kTailMaxT * 16 * 17];
-  {  // all loads in flight at once (16-B sc1 buffer loads; out of range past TC reads zeros)
-    constexpr int kWL = kTailMaxT * 256 / (2 * 64 * kTailNW);
-    const __amdgpu_buffer_rsrc_t RW = __builtin_amdgcn_make_buffer_rsrc(Wg, 0, kTailMaxT * 256 * 8, 0x00020000);
-    u32x4 wv[kWL];
-#pragma unroll
-    for (int i = 0; i < kWL; i++) {
-      const int q2 = 2 * (tid + 64 * kTailNW * i);
-      wv[i] = __builtin_amdgcn_raw_buffer_load_b128(RW, q2 < 256 * TC ? q2 * 8 : 0x7fffff00, 0, 16);
-    }
-    double yl[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int q = tid + 64 * kTailNW * i;
-      yl[i] = q < 16 * TC ? ld_sc1(S.ypg + q) : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < kWL; i++) {
-      const int q2 = 2 * (tid + 64 * kTailNW * i);
-      WlT[(q2 >> 4) * 17 + (q2 & 15)] = __longlong_as_double((long long)(((unsigned long long)wv[i].y << 32) | wv[i].x));
-      WlT[(q2 >> 4) * 17 + (q2 & 15) + 1] =
-          __longlong_as_double((long long)(((unsigned long long)wv[i].w << 32) | wv[i].z));
-    }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int q = tid + 64 * kTailNW * i;
-      if (q < 16 * TC) yv[q] = yl[i];
-    }
-  }
-  for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) xv[q] = 0.0;
-  if (tid < kTailMaxT) xflag[tid] = 0;
-  __syncthreads();
-  // y_J -= L(K, J)^T x_K from the LgT tile (operand order: 32 B per lane).
-  // The operands of the next step are in flight while this one runs: every
-  // load is a 16-B sc1 buffer load issued unconditionally (rows a step does
-  // not need read out of range, which returns zeros without a memory access),
-  // so each step issues the same number of loads and the compiler waits for
-  // exactly the older step's (24 per wave, two steps = 48 < the 63 vmcnt).
-  // Per step K the owner of row K - 1 applies x_K to that row first and forms
-  // x_{K-1} at once (the chain per step is one tile update + one 16-term
-  // dot product), then applies x_K to its other rows. Each row still takes
-  // its updates in decreasing K (the same sums).
-  constexpr int kTW = (kTailMaxT + kTailNW - 1) / kTailNW;  // tile rows J' of one wave
-  constexpr int kRing = 3;
-  const __amdgpu_buffer_rsrc_t RT =
-      __builtin_amdgcn_make_buffer_rsrc(S.LgT, 0, kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 8, 0x00020000);
-  constexpr int kFar = 0x7fffff00;  // out of range
-  f64x4 lt[kRing][kTW];
-  auto ld2 = [&](int off, double &x0, double &x1) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(RT, off, 0, 16);
-    x0 = __longlong_as_double((long long)(((unsigned long long)v.y << 32) | v.x));
-    x1 = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
   };
-  auto bs_load = [&](int K, int slot) {
+  auto mma = [&](f64x4 &acc, const f64x4 &key, const f64x4 &ri) {
 #pragma unroll
-    for (int t = 0; t < kTW; t++) {
-      const int Jc = wave + kTailNW * t;
-      const int off = (K >= 0 && Jc < K) ? (tail_tile(K, Jc) * 256 + 4 * lane) * 8 : kFar;
-      double x0, x1, x2, x3;
-      ld2(off, x0, x1);
-      ld2(off + 16, x2, x3);
-      lt[slot][t] = f64x4{x0, x1, x2, x3};
-    }
+    for (int q = 0; q < 4; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-key[q], ri[q], acc, 0, 0, 0);
   };
-  auto form_x = [&](int K) {  // the owner of row K, all of whose updates are in
-    const int jv = min(16, n - 16 * K);
-    if (lane < 16) {
-      double x = 0.0;
-#pragma unroll
-      for (int i = 0; i < 16; i++) x += WlT[(K * 16 + lane) * 17 + i] * yv[16 * K + i];
-      xv[16 * K + lane] = lane < jv ? x : 0.0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (lane == 0) M3S_CSTAMP(2, 700 + K, 0);
-  };
-#pragma unroll
-  for (int d = 0; d < kRing; d++) bs_load(TC - 1 - d, d);
-  if (tid == 0) M3S_CSTAMP(2, 699, 0);
-  if ((TC - 1) % kTailNW == wave) form_x(TC - 1);
-  for (int K0 = TC - 1; K0 >= 0; K0 -= kRing) {
-#pragma unroll
-    for (int d = 0; d < kRing; d++) {
-      const int K = K0 - d;
-      if (K >= 0) {
-        if (K % kTailNW != wave) {  // (the owner formed x_K itself, in the step before)
-          int spins = 0;
-          while (__hip_atomic_load(xflag + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
-                 spins < (1 << 22))
-            spins++;
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  f64x4 rk0_last = {0.0, 0.0, 0.0, 0.0}, rk1_last = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < J0; k++) {
+    // the pair's two key tiles L(J0, k), L(J1, k): both loads in flight, one poll
+    GranTile g0, g1;
+    {
+      int spins = 0;
+      for (;;) {
+        gran_load(R, tail_tile(J0, k), lane, g0);
+        if (jn == 2) gran_load(R, tail_tile(J1, k), lane, g1);
+        if (gran_ready(g0, want) && (jn < 2 || gran_ready(g1, want))) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kColSpins) {
+          if (lane == 0) fail_s = 1;
+          break;
         }
-        double xb[4];
+      }
+    }
+    const f64x4 rk0 = gran_val(g0);
+    f64x4 rk1 = {0.0, 0.0, 0.0, 0.0};
+    if (jn == 2) rk1 = gran_val(g1);
+    if (wave == 0) {
+      mma(acc0[0], rk0, rk0);
+      if (jn == 2) {
+        mma(acc0[1], rk0, rk1);
+        mma(acc1[1], rk1, rk1);
+      }
+    } else if (k + 1 == J0) {
+      rk0_last = rk0, rk1_last = rk1;
+    } else {
+      unsigned pend = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) xb[q] = xv[16 * K + 4 * q + lk];
+      for (int u = 0; u < kRC; u++)
+        if (live(u)) pend |= 1u << u;
+      int spins = 0;
+      while (pend) {
+        GranTile g[kRC];
 #pragma unroll
-        for (int pass = 0; pass < 2; pass++) {
+        for (int u = 0; u < kRC; u++)
+          if (pend & (1u << u)) gran_load(R, tail_tile(rowI(u), k), lane, g[u]);
 #pragma unroll
-          for (int t = 0; t < kTW; t++) {
-            const int Jc = wave + kTailNW * t;
-            if (pass == 0 ? Jc == K - 1 : Jc < K - 1) {
-              // (L^T x)[m], m = lr: lane l holds L(K,Jc)^T[lr][lk + 4q]; the 4 lanes of
-              // one m add their partial sums (VALU: the MFMA form spent 15/16 of its work
-              // on copies of x)
-              double u = 0.0;
-#pragma unroll
-              for (int q = 0; q < 4; q++) u += lt[d][t][q] * xb[q];
-              u += __shfl_xor(u, 16);
-              u += __shfl_xor(u, 32);
-              if (lane < 16) yv[16 * Jc + lane] -= u;
-              if (pass == 0) {
-                wave_lds_fence();  // row K - 1's y' before this wave reads it
-                form_x(K - 1);
-              }
-            }
+        for (int u = 0; u < kRC; u++) {
+          if ((pend & (1u << u)) && gran_ready(g[u], want)) {
+            const f64x4 ri = gran_val(g[u]);
+            mma(acc0[u], rk0, ri);
+            if (jn == 2) mma(acc1[u], rk1, ri);
+            pend &= ~(1u << u);
           }
         }
-        wave_lds_fence();
+        if (pend) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kColSpins) {
+            if (lane == 0) fail_s = 1;
+            break;
+          }
+        }
       }
-      bs_load(K - kRing, d);
     }
   }
-  __syncthreads();  // every x_K
-  for (int j = tid; j < n; j += 64 * kTailNW) A.rhs[7 * A.c0 + j] = xv[j];
-  if (tid == 0) M3S_CSTAMP(2, 511, 0);
+  const __amdgpu_buffer_rsrc_t RT =
+      __builtin_amdgcn_make_buffer_rsrc(S.LgT, 0, kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 8, 0x00020000);
+  // L(I, J) itself (A(I, J) W^T: operands swapped) for the back-substitution
+  auto store_lgt = [&](int I, int J, const f64x4 &a, int slot) {
+    f64x4 dt = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) dt = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], Wk[slot][lr][4 * q + lk], dt, 0, 0, 0);
+    const unsigned long long b0 = __double_as_longlong(dt[0]), b1 = __double_as_longlong(dt[1]),
+                             b2 = __double_as_longlong(dt[2]), b3 = __double_as_longlong(dt[3]);
+    const u32x4 w0 = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
+    const u32x4 w1 = {(unsigned)b2, (unsigned)(b2 >> 32), (unsigned)b3, (unsigned)(b3 >> 32)};
+    const int off = (tail_tile(I, J) * 256 + 4 * lane) * 8;
+    __builtin_amdgcn_raw_buffer_store_b128(w0, RT, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(w1, RT, off + 16, 0, 16);
+  };
+  auto panel = [&](const f64x4 &a, int slot) {  // L(I, J)^T = W_J A(I, J)^T, operand order
+    f64x4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) d = __builtin_amdgcn_mfma_f64_16x16x4f64(Wk[slot][lr][4 * q + lk], a[q], d, 0, 0, 0);
+    return d;
+  };
+  auto wait_lds = [&](int *f) {
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && spins < (1 << 20)) {
+      __builtin_amdgcn_s_sleep(1);
+      spins++;
+    }
+    if (spins >= (1 << 20) && lane == 0) fail_s = 1;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  if (wave == 0) {
+    // diagonal J0, then (jn == 2) the pair's sub-diagonal tile, the second
+    // diagonal's update from it, the second diagonal
+    if (tid == 0) M3S_CSTAMP(2, J0, 1);
+    if (tid == 0) M3S_CSTAMP(2, 600 + J0, 0);
+    if (tail_diag_mfma(acc0[0], Wk[0], yv + 16 * J0, min(16, n - 16 * J0), In == J0 ? rn : -1, lane) && lane == 0)
+      fail_s = 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&wready[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (tid == 0) M3S_CSTAMP(2, J0, 2);
+    if (jn == 2) {
+      const f64x4 d = panel(acc0[1], 0);  // L(J1, J0)^T
+      Lsub[lane] = d;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&lready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (J1 == In && lr == rn) {  // y' of column J0 from the RHS row
+#pragma unroll
+        for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J0 + lk + 4 * r, d[r]);
+      }
+      mma(acc1[1], d, d);
+      if (tid == 0) M3S_CSTAMP(2, J1, 1);
+      if (tid == 0) M3S_CSTAMP(2, 600 + J1, 0);
+      if (tail_diag_mfma(acc1[1], Wk[1], yv + 16 * J1, min(16, n - 16 * J1), In == J1 ? rn : -1, lane) && lane == 0)
+        fail_s = 1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&wready[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (tid == 0) M3S_CSTAMP(2, J1, 2);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < jn; j++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)(J0 + j) * 256 + lane * 16 + r, Wk[j][r][lane]);  // W^T
+        if (In == J0 + j) st_sc1(S.ypg + 16 * (J0 + j) + lane, yv[16 * (J0 + j) + lane]);
+      }
+    }
+    if (jn == 2) store_lgt(J1, J0, acc0[1], 0);
+  } else {
+    // the deferred update from column J0 - 1: every row's tile in flight at
+    // once, applied as they land (while wave 0 factors the diagonal)
+    if (J0 > 0) {
+      unsigned pend = 0;
+#pragma unroll
+      for (int u = 0; u < kRC; u++)
+        if (live(u)) pend |= 1u << u;
+      int spins = 0;
+      while (pend) {
+        GranTile g[kRC];
+#pragma unroll
+        for (int u = 0; u < kRC; u++)
+          if (pend & (1u << u)) gran_load(R, tail_tile(rowI(u), J0 - 1), lane, g[u]);
+#pragma unroll
+        for (int u = 0; u < kRC; u++) {
+          if ((pend & (1u << u)) && gran_ready(g[u], want)) {
+            const f64x4 ri = gran_val(g[u]);
+            mma(acc0[u], rk0_last, ri);
+            if (jn == 2) mma(acc1[u], rk1_last, ri);
+            pend &= ~(1u << u);
+          }
+        }
+        if (pend) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kColSpins) {
+            if (lane == 0) fail_s = 1;
+            break;
+          }
+        }
+      }
+    }
+    // column J0's panel tiles, handed off at once
+    if (tid == 64) M3S_CSTAMP(2, 800 + J0, 0);
+    wait_lds(&wready[0]);
+    if (tid == 64) M3S_CSTAMP(2, 800 + J0, 1);
+    f64x4 d0[kRC];
+#pragma unroll
+    for (int u = 0; u < kRC; u++) {
+      const int I = rowI(u);
+      d0[u] = f64x4{0.0, 0.0, 0.0, 0.0};
+      if (live(u)) {
+        d0[u] = panel(acc0[u], 0);
+        gran_store(R, tail_tile(I, J0), lane, d0[u], want);
+        if (I == In && lr == rn) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J0 + lk + 4 * r, d0[u][r]);
+        }
+      }
+    }
+    if (jn == 2) {
+      // column J1: the update from the pair's first column (L(J1, J0) from
+      // wave 0), then the panel tiles (row J1 + 1, the next pair's chain, is
+      // wave 1's first)
+      if (tid == 64) M3S_CSTAMP(2, 800 + J0, 2);
+      wait_lds(&lready);
+      const f64x4 ls = Lsub[lane];
+#pragma unroll
+      for (int u = 0; u < kRC; u++)
+        if (live(u)) mma(acc1[u], ls, d0[u]);
+      if (tid == 64) M3S_CSTAMP(2, 800 + J0, 3);
+      wait_lds(&wready[1]);
+      if (tid == 64) M3S_CSTAMP(2, 900 + J0, 0);
+#pragma unroll
+      for (int u = 0; u < kRC; u++) {
+        const int I = rowI(u);
+        if (live(u)) {
+          const f64x4 d = panel(acc1[u], 1);
+          gran_store(R, tail_tile(I, J1), lane, d, want);
+          if (I == J1 + 1 && tid == 64) M3S_CSTAMP(2, J1, 0);
+          if (I == In && lr == rn) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J1 + lk + 4 * r, d[r]);
+          }
+        }
+      }
+    }
+    // the L tiles for the back-substitution, after every hand-off
+#pragma unroll
+    for (int u = 0; u < kRC; u++) {
+      const int I = rowI(u);
+      if (live(u) && I < TC) {
+        store_lgt(I, J0, acc0[u], 0);
+        if (jn == 2) store_lgt(I, J1, acc1[u], 1);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave has left
+  __syncthreads();
+  if (tid == 0) {
+    if (fail_s) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < jn; j++) __hip_atomic_store(S.tflag + J0 + j, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < jn; j++) M3S_CSTAMP(2, J0 + j, 3);
+  }
+  if ((int)blockIdx.x != (int)gridDim.x - 1) return;
+  tail_backsub_wg(A, S, yv, xv);
 }
 
 #ifdef M3S_TEST_PATHS  // reached only through the dense knob: every graph it fits (m <= 31) has a sparse plan
@@ -4328,6 +4692,7 @@ struct Knobs {
   std::atomic<int> debug_drop_item{-1};  // drop one LLT dispatch item (bounded-wait test)
   std::atomic<int> gather_lds{1};      // 0: the round-2 VGPR-staged gathering kernel (bitwise reference)
   std::atomic<int> subtree{1};         // 0: df_factor_kernel factors the sparse columns too (round-3 path)
+  std::atomic<int> tail_pair{1};       // 0: tail_cyc_kernel (one tile column per workgroup)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -4345,6 +4710,7 @@ struct Knobs {
     env("M3S_TAIL_MFMA", tail_mfma);
     env("M3S_BORDER_SPLIT", border_split);
     env("M3S_SUBTREE", subtree);
+    env("M3S_TAIL_PAIR", tail_pair);
 #endif
   }
 };
@@ -4362,6 +4728,7 @@ inline bool force_dense_knob() { return knobs().dense == 1; }
 inline int drop_item_knob() { return knobs().debug_drop_item; }
 bool gather_lds_path() { return knobs().gather_lds != 0; }
 inline bool subtree_path() { return knobs().subtree != 0; }
+inline bool tail_pair_path() { return knobs().tail_pair != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -4372,6 +4739,7 @@ constexpr bool force_dense_knob() { return false; }
 constexpr int drop_item_knob() { return -1; }
 bool gather_lds_path() { return true; }
 constexpr bool subtree_path() { return true; }
+constexpr bool tail_pair_path() { return true; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -4385,6 +4753,7 @@ struct PlanMeta {
   int nnz = 0;  // off-diagonal blocks (col_ptr[m])
   int off_dfitems = 0, n_dfitems = 0;  // df_factor_kernel dispatch list (appended to the plan image)
   int n_dfsparse = 0;                  // its sparse-column items (the border items follow)
+  int off_dfb = 0, n_dfb = 0;          // subtree path: border-row OFF tasks + tail border tasks
   int off_sub = 0, n_sub = 0;          // subtree image (appended), subtrees (subtree_factor_kernel)
   int64_t sub_lds = 0, sub_bs_lds = 0;  // dynamic LDS bytes: subtree factor, back-substitution
   PlanImage img;  // offsets (data vector cleared after upload)
@@ -4422,6 +4791,7 @@ PlanMeta solve_view(const PlanMeta &M) {
   v.n_dfitems = M.n_dfitems;
   v.n_dfsparse = M.n_dfsparse, v.off_sub = M.off_sub, v.n_sub = M.n_sub, v.sub_lds = M.sub_lds;
   v.sub_bs_lds = M.sub_bs_lds;
+  v.off_dfb = M.off_dfb, v.n_dfb = M.n_dfb;
   v.nnz = M.nnz;
   v.img = M.img;  // offsets (its data vector is empty in the registry)
   v.plan_pending = M.plan_pending;
@@ -4747,10 +5117,12 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           SA.sdone = F.sdone;
           SA.want = meta.epoch + 1;
           SA.flags = flags;
+          SA.Wgr = F.Wgr;
+          SA.m = meta.m;
           set_lds_attributes_once();
           subtree_factor_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_lds, st>>>(SA);
-          F.items += meta.n_dfsparse;
-          F.n_items -= meta.n_dfsparse;
+          F.items = D.plan + meta.off_dfb;
+          F.n_items = meta.n_dfb;
         }
         const int nw = std::max(1, std::min(F.n_items, 1024));
         if (F.n_items > 0) df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
@@ -4784,7 +5156,10 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.LgT = Y.ypg + 16 * kTailMaxT;
           Y.LgG = tail + tail_gran_offset_doubles();
           const int TC = (7 * meta.nc + 15) / 16;
-          tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
+          if (tail_pair_path())
+            tail_pair_kernel<<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
+          else
+            tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
         } else {
           tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
         }
@@ -4957,7 +5332,18 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
     meta.n_dfsparse = (int)img.data.size() - meta.off_dfitems;
     for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
     meta.n_dfitems = (int)img.data.size() - meta.off_dfitems;
-    if (chip_path) {  // the sparse columns' subtrees, one LDS workgroup each (subtree_factor_kernel)
+    if (chip_path) {
+      // the subtree path's df_factor_kernel list: the OFF tasks of the sparse
+      // columns' border rows (rows in the dense tail) in level order, then the
+      // dense-tail border tasks; the subtrees' internal blocks are
+      // subtree_factor_kernel's (one LDS workgroup per subtree)
+      const int c0 = P.m - P.nc;
+      meta.off_dfb = (int)img.data.size();
+      for (int32_t k : P.corder)
+        for (int q = 0; q < P.col_ptr[k + 1] - P.col_ptr[k]; q++)
+          if (P.col_row[P.col_ptr[k] + q] >= c0) img.data.push_back(P.ctask0[k] + q);
+      for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
+      meta.n_dfb = (int)img.data.size() - meta.off_dfb;
       SubtreeImage SI;
       build_subtree_image(P, kSubLdsCap, SI);
       meta.off_sub = (int)img.data.size();
@@ -5212,6 +5598,9 @@ int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st) {
   M.m = built.m, M.S = built.S, M.levels = built.levels, M.plan_len = built.plan_len;
   M.n_items = built.n_items, M.n_tasks = built.n_tasks, M.n_parts = built.n_parts, M.nc = built.nc;
   M.off_dfitems = built.off_dfitems, M.n_dfitems = built.n_dfitems, M.nnz = built.nnz;
+  M.n_dfsparse = built.n_dfsparse, M.off_sub = built.off_sub, M.n_sub = built.n_sub, M.sub_lds = built.sub_lds;
+  M.off_dfb = built.off_dfb, M.n_dfb = built.n_dfb;
+  M.sub_bs_lds = built.sub_bs_lds;
   M.img = built.img;
   M.h_plan = std::move(built.h_plan);
   M.plan_pending = false;
@@ -5305,6 +5694,9 @@ int host_finish(const m3s_gn_args *a, hipStream_t st) {
   M.m = hitm.m, M.S = hitm.S, M.levels = hitm.levels, M.plan_len = hitm.plan_len;
   M.n_items = hitm.n_items, M.n_tasks = hitm.n_tasks, M.n_parts = hitm.n_parts, M.nc = hitm.nc;
   M.off_dfitems = hitm.off_dfitems, M.n_dfitems = hitm.n_dfitems, M.nnz = hitm.nnz;
+  M.n_dfsparse = hitm.n_dfsparse, M.off_sub = hitm.off_sub, M.n_sub = hitm.n_sub, M.sub_lds = hitm.sub_lds;
+  M.off_dfb = hitm.off_dfb, M.n_dfb = hitm.n_dfb;
+  M.sub_bs_lds = hitm.sub_bs_lds;
   M.img = hitm.img;
   M.h_plan = std::move(hitm.h_plan);
   M.plan_pending = false;
@@ -6063,7 +6455,8 @@ int m3s_set_knob(const char *name, int value) {
 #ifdef M3S_TEST_PATHS
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
-             {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree}
+             {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
+             {"tail_pair", &k.tail_pair}
 #endif
   };
   for (const auto &t : tab)
@@ -6074,7 +6467,7 @@ int m3s_set_knob(const char *name, int value) {
       // no launch reads a plan built for another path (e.g. a chip-path
       // plan, cached unscheduled, on the one-workgroup kernel)
       static const char *const shaping[] = {"dense_tail_min", "dense", "cols", "df", "tail_cyc",
-                                            "tail_mfma", "border_split", "debug_drop_item", "subtree"};
+                                            "tail_mfma", "border_split", "debug_drop_item"};
       if (old != value)
         for (const char *sn : shaping)
           if (std::strcmp(sn, name) == 0) {

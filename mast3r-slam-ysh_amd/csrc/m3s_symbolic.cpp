@@ -593,7 +593,7 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   }
 }
 
-void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImage &out) {
+void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImage &out, bool with_border) {
   out = SubtreeImage();
   const int m = P.m, c0 = m - P.nc;
   std::vector<int> parent(m, -1), root(m, -1), level(m, 0);
@@ -637,7 +637,7 @@ void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImag
     // LDS: W (49) + y (7) doubles per column, flags (nblk + 2 ncol + 4 ints), then blocks
     const int64_t fixed = 8 * (int64_t)ncol * 56 + 4 * ((int64_t)nblk + 2 * ncol + 4);
     const int64_t room = lds_cap_bytes - fixed;
-    const int n_lds = (int)std::max<int64_t>(0, std::min<int64_t>(nblk, room / (8 * 49)));
+    const int n_lds = (int)std::max<int64_t>(0, std::min<int64_t>(with_border ? nblk : n_int, room / (8 * 49)));
     out.lds_bytes = std::max(out.lds_bytes, fixed + 8 * 49 * (int64_t)n_lds);
     // per-block column and the global OFF task it is
     std::vector<int32_t> tcol(nblk), tptr(1, 0), tlist, dptr(1, 0), dlist, itA, itB;
@@ -682,8 +682,9 @@ void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImag
           for (int b = 0; b < n_int; b++)
             if (tcol[b] == c) itA.push_back(b);
         }
-      for (int b = n_int; b < nblk; b++)
-        if (level[cols[tcol[b]]] == l) itB.push_back(b);
+      if (with_border)
+        for (int b = n_int; b < nblk; b++)
+          if (level[cols[tcol[b]]] == l) itB.push_back(b);
     }
     // waves on list A: enough for its width, the rest start on the border list
     const int nwA = itB.empty() ? 16 : std::max(8, std::min(14, 16 * (int)itA.size() / (int)(itA.size() + itB.size()) + 2));

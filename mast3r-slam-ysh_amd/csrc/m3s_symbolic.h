@@ -107,7 +107,10 @@ struct SubtreeImage {
   int64_t lds_bytes = 0;     // largest subtree's dynamic LDS (factor)
   int64_t bs_lds_bytes = 0;  // (back-substitution)
 };
-void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImage &out);
+// with_border = false: the border blocks (rows in the dense tail) are not
+// the subtree workgroup's items (list B empty, only internal blocks in LDS):
+// df_factor_kernel computes them over the chip (subtree path, round 4)
+void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImage &out, bool with_border = false);
 
 // Flattened int32 image of the plan (offsets of each array into it).
 struct PlanImage {

@@ -287,6 +287,15 @@ def run_subtree_plan(p, subs, Hjj, gj):
                 assert fdone[k]
                 L[gsl[blk]] = A @ W[k].T
                 fdone[gsl[blk]] = True
+        assert d["nB"] == 0  # border rows are df_factor_kernel's (level order over the chip)
+        for blk in range(d["n_int"], d["nblk"]):  # column order: a topological order of the border blocks
+            k = cols[d["tcol"][blk]]
+            A = L[gsl[blk]].copy()
+            for ba, bb in d["tlist"][d["tptr"][blk]:d["tptr"][blk + 1]]:
+                assert fdone[gsl[ba]] and fdone[gsl[bb]]
+                A -= L[gsl[ba]] @ L[gsl[bb]].T
+            L[gsl[blk]] = A @ W[k].T
+            fdone[gsl[blk]] = True
         assert all(fdone[g_] for g_ in gsl) and all(fdone[k] for k in cols)
     assert seen == set(range(c0))  # every sparse column in exactly one subtree
     assert sum(len(d["cols"]) for d in subs) == c0

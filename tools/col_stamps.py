@@ -93,6 +93,12 @@ if TC:
         e = (T[J, 0] - tt0) / 100.0 if J + 1 < TC else float("nan")
         dg = (T[J, 2] - T[600 + J, 0]) / 100.0 if T[600 + J, 0] else float("nan")
         print(f"  J={J:2d} {a:8.2f} {b:8.2f} {e:8.2f} {c:8.2f}   (diagonal factor alone {dg:5.2f})")
+    if T[800, 1]:
+        print("  pair kernel, wave 1 per pair (J0): deferred update done / W_J0 seen / J0 panels stored / "
+              "J1 updates done / W_J1 seen")
+        for J0 in range(0, TC - 1, 2):
+            v = [(T[800 + J0, i] - tt0) / 100.0 for i in range(4)] + [(T[900 + J0, 0] - tt0) / 100.0]
+            print(f"  J0={J0:2d} " + " ".join(f"{x:8.2f}" for x in v))
     print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")
     if T[699, 0]:
         print(f"  back-substitution: flags seen {(T[698, 0] - tt0) / 100.0:.2f}, loop start {(T[699, 0] - tt0) / 100.0:.2f}; "

@@ -2765,6 +2765,7 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
   }
 }
 
+#ifdef M3S_TEST_PATHS  // A/B path (M3S_SUBTREE=1): measured slower than df_factor_kernel
 // ---------------------------------------- subtrees in LDS (round 4) --
 // Large graphs: the sparse columns below the dense tail split into subtrees
 // whose update lists stay inside the subtree (every row of struct(k) is an
@@ -2983,6 +2984,7 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs 
                        __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0 && fail_s) set_fail(A.flags);
 }
+#endif  // M3S_TEST_PATHS
 
 // dx = -x (original order), retraction, ||dx|| test (one wave; x in y, sc1)
 __device__ void col_finish(const ColArgs &C, int lane) {
@@ -3031,6 +3033,7 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
 }
 
+#ifdef M3S_TEST_PATHS
 // Back-substitution of the subtrees (round 4; replaces col_backsub_kernel on
 // the subtree path): one 1024-thread workgroup per subtree. The tail's x is
 // final (tail_cyc_kernel), so every border term L_ik^T x_i (i in the tail) is
@@ -3150,6 +3153,7 @@ __global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsAr
     col_finish(C, lane);
   }
 }
+#endif  // M3S_TEST_PATHS
 
 constexpr int kBsCap = 40;  // L_ik blocks of a column prefetched into LDS (the rest staged)
 __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
@@ -4119,72 +4123,51 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     }
     if (jn == 2) store_lgt(J1, J0, acc0[1], 0);
   } else {
-    // the deferred update from column J0 - 1: every row's tile in flight at
-    // once, applied as they land (while wave 0 factors the diagonal)
-    if (J0 > 0) {
-      unsigned pend = 0;
-#pragma unroll
-      for (int u = 0; u < kRC; u++)
-        if (live(u)) pend |= 1u << u;
-      int spins = 0;
-      while (pend) {
-        GranTile g[kRC];
-#pragma unroll
-        for (int u = 0; u < kRC; u++)
-          if (pend & (1u << u)) gran_load(R, tail_tile(rowI(u), J0 - 1), lane, g[u]);
-#pragma unroll
-        for (int u = 0; u < kRC; u++) {
-          if ((pend & (1u << u)) && gran_ready(g[u], want)) {
-            const f64x4 ri = gran_val(g[u]);
-            mma(acc0[u], rk0_last, ri);
-            if (jn == 2) mma(acc1[u], rk1_last, ri);
-            pend &= ~(1u << u);
-          }
-        }
-        if (pend) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > kColSpins) {
-            if (lane == 0) fail_s = 1;
-            break;
-          }
-        }
-      }
-    }
-    // column J0's panel tiles, handed off at once
-    if (tid == 64) M3S_CSTAMP(2, 800 + J0, 0);
-    wait_lds(&wready[0]);
-    if (tid == 64) M3S_CSTAMP(2, 800 + J0, 1);
-    f64x4 d0[kRC];
+    // row by row (the first row of waves 1 and 2 carries the next pair's
+    // chain: its two tiles go out before any other row's work): the deferred
+    // update from column J0 - 1 as the row's tile lands, the panel tile
+    // L(I, J0), the update of (I, J1) from the pair's first column
+    // (L(J1, J0) from wave 0), the panel tile L(I, J1); each tile handed off
+    // at once. (Per tile the same updates in the same order.)
+    bool have_w0 = false, have_l = false, have_w1 = false;
+    f64x4 ls = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int u = 0; u < kRC; u++) {
       const int I = rowI(u);
-      d0[u] = f64x4{0.0, 0.0, 0.0, 0.0};
       if (live(u)) {
-        d0[u] = panel(acc0[u], 0);
-        gran_store(R, tail_tile(I, J0), lane, d0[u], want);
+        if (J0 > 0) {
+          GranTile g;
+          poll_tile(tail_tile(I, J0 - 1), g);
+          const f64x4 ri = gran_val(g);
+          mma(acc0[u], rk0_last, ri);
+          if (jn == 2) mma(acc1[u], rk1_last, ri);
+        }
+        if (!have_w0) {
+          if (tid == 64) M3S_CSTAMP(2, 800 + J0, 0);
+          wait_lds(&wready[0]);
+          have_w0 = true;
+          if (tid == 64) M3S_CSTAMP(2, 800 + J0, 1);
+        }
+        const f64x4 d0 = panel(acc0[u], 0);
+        gran_store(R, tail_tile(I, J0), lane, d0, want);
         if (I == In && lr == rn) {
 #pragma unroll
-          for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J0 + lk + 4 * r, d0[u][r]);
+          for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J0 + lk + 4 * r, d0[r]);
         }
-      }
-    }
-    if (jn == 2) {
-      // column J1: the update from the pair's first column (L(J1, J0) from
-      // wave 0), then the panel tiles (row J1 + 1, the next pair's chain, is
-      // wave 1's first)
-      if (tid == 64) M3S_CSTAMP(2, 800 + J0, 2);
-      wait_lds(&lready);
-      const f64x4 ls = Lsub[lane];
-#pragma unroll
-      for (int u = 0; u < kRC; u++)
-        if (live(u)) mma(acc1[u], ls, d0[u]);
-      if (tid == 64) M3S_CSTAMP(2, 800 + J0, 3);
-      wait_lds(&wready[1]);
-      if (tid == 64) M3S_CSTAMP(2, 900 + J0, 0);
-#pragma unroll
-      for (int u = 0; u < kRC; u++) {
-        const int I = rowI(u);
-        if (live(u)) {
+        if (jn == 2) {
+          if (!have_l) {
+            if (tid == 64) M3S_CSTAMP(2, 800 + J0, 2);
+            wait_lds(&lready);
+            ls = Lsub[lane];
+            have_l = true;
+          }
+          mma(acc1[u], ls, d0);
+          if (!have_w1) {
+            if (tid == 64) M3S_CSTAMP(2, 800 + J0, 3);
+            wait_lds(&wready[1]);
+            have_w1 = true;
+            if (tid == 64) M3S_CSTAMP(2, 900 + J0, 0);
+          }
           const f64x4 d = panel(acc1[u], 1);
           gran_store(R, tail_tile(I, J1), lane, d, want);
           if (I == J1 + 1 && tid == 64) M3S_CSTAMP(2, J1, 0);
@@ -4691,7 +4674,7 @@ struct Knobs {
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel
   std::atomic<int> debug_drop_item{-1};  // drop one LLT dispatch item (bounded-wait test)
   std::atomic<int> gather_lds{1};      // 0: the round-2 VGPR-staged gathering kernel (bitwise reference)
-  std::atomic<int> subtree{1};         // 0: df_factor_kernel factors the sparse columns too (round-3 path)
+  std::atomic<int> subtree{0};         // 1: the subtree kernels (one LDS workgroup per subtree; measured slower)
   std::atomic<int> tail_pair{1};       // 0: tail_cyc_kernel (one tile column per workgroup)
 #endif
   Knobs() {
@@ -4738,7 +4721,7 @@ constexpr bool border_split() { return true; }
 constexpr bool force_dense_knob() { return false; }
 constexpr int drop_item_knob() { return -1; }
 bool gather_lds_path() { return true; }
-constexpr bool subtree_path() { return true; }
+constexpr bool subtree_path() { return false; }
 constexpr bool tail_pair_path() { return true; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
@@ -5106,6 +5089,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         F.tail_A = tail;
         F.tail_ld = tld;
         F.Wgr = at<double>(ws, Ly.wgran);
+#ifdef M3S_TEST_PATHS
         if (subtree_path() && meta.n_sub > 0) {
           // the sparse columns: one LDS workgroup per subtree; df_factor_kernel
           // then runs only the dense tail's border tasks (if any)
@@ -5124,6 +5108,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           F.items = D.plan + meta.off_dfb;
           F.n_items = meta.n_dfb;
         }
+#endif
         const int nw = std::max(1, std::min(F.n_items, 1024));
         if (F.n_items > 0) df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
       } else {
@@ -5164,6 +5149,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
         }
       }
+#ifdef M3S_TEST_PATHS
       if (subtree_path() && meta.n_sub > 0) {
         SubBsArgs B;
         B.sub = D.plan + meta.off_sub;
@@ -5171,7 +5157,9 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         B.fin_ctr = C.ctr + 5;
         B.C = C;
         subtree_backsub_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_bs_lds, st>>>(B);
-      } else {
+      } else
+#endif
+      {
         const int g4 = std::max(1, std::min(C.ncols, 256));
         col_backsub_kernel<<<g4, 64, 0, st>>>(C);
       }
@@ -5295,10 +5283,12 @@ void set_lds_attributes_once() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gn_prologue_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+#ifdef M3S_TEST_PATHS
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(subtree_factor_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSubLdsCap);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(subtree_backsub_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSubLdsCap);
+#endif
   });
 }
 
@@ -5332,6 +5322,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
     meta.n_dfsparse = (int)img.data.size() - meta.off_dfitems;
     for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
     meta.n_dfitems = (int)img.data.size() - meta.off_dfitems;
+#ifdef M3S_TEST_PATHS
     if (chip_path) {
       // the subtree path's df_factor_kernel list: the OFF tasks of the sparse
       // columns' border rows (rows in the dense tail) in level order, then the
@@ -5352,6 +5343,7 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
       meta.sub_bs_lds = SI.bs_lds_bytes;
       img.data.insert(img.data.end(), SI.data.begin(), SI.data.end());
     }
+#endif
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
     if (fits && !force_dense) {
       meta.sparse = true;

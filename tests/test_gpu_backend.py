@@ -518,13 +518,15 @@ def test_block_dataflow_matches_column_tasks_bitwise(test_lib, be, N, knobs):
 @pytest.mark.parametrize("N", [90, 140, 256, 400])
 def test_subtree_factor_matches_block_dataflow_bitwise(test_lib, be, N, knobs):
     """Large graphs (round 4): the sparse columns below the dense tail factored
-    as subtrees, one LDS workgroup each (subtree_factor_kernel, the default),
-    against df_factor_kernel's chip-wide dataflow over the same columns (test
-    knob subtree=0). Both run every block's update list in the global plan's
-    order with the same per-block arithmetic: poses and dx agree bitwise."""
+    as subtrees, one LDS workgroup each (subtree_factor_kernel, test knob
+    subtree=1; the A/B path, measured slower), against df_factor_kernel's
+    chip-wide dataflow over the same columns (the product path). Both run
+    every block's update list in the global plan's order with the same
+    per-block arithmetic: poses and dx agree bitwise."""
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 12, 16, seed=750 + N)
+    knobs("subtree", "1")
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     knobs("subtree", "0")
     T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)

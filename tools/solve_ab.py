@@ -27,7 +27,7 @@ def main():
     mode = os.environ.get("SOLVE_MODE", "calib")
     iters = int(os.environ.get("SOLVE_ITERS", "3"))
     rounds = int(os.environ.get("SOLVE_ROUNDS", "7"))
-    groups = [dict(kv.split("=") for kv in g.split(";") if kv) for g in os.environ.get("SOLVE_AB", "subtree=1;tail_pair=1|subtree=0;tail_pair=1|subtree=1;tail_pair=0|subtree=0;tail_pair=0").split("|")]
+    groups = [dict(kv.split("=") for kv in g.split(";") if kv) for g in os.environ.get("SOLVE_AB", "subtree=0;tail_pair=1|subtree=0;tail_pair=0|subtree=1;tail_pair=1").split("|")]
     H, W = 12, 16
     for N in [int(x) for x in os.environ.get("SOLVE_N", "128,256").split(",")]:
         g = synthetic.make_graph(N, H, W, seed=1003, device=dev)

@@ -3256,11 +3256,27 @@ struct TailArgs {
 
 // augmented tail matrix entry (i, j): padding columns are identity (and the
 // unused (n, n)), padding rows zero, row n the RHS y of the tail columns
-__device__ __forceinline__ double tail_entry(const TailArgs &A, int n, int i, int j) {
-  const bool pad = j >= n || i > n;
-  const double *src = (i == n) ? A.rhs + 7 * A.c0 + j : A.Ad + (size_t)i * A.ld + j;
-  const double v = pad ? 0.0 : *src;
-  return (j >= n && i == j) ? 1.0 : v;
+// Both loads are buffer loads, unconditional: an out-of-range offset reads 0
+// (kFar), so a workgroup's initial tiles are all in flight at once (a
+// guarded pointer load became one branch and one vmcnt(0) per entry).
+struct TailSrc {
+  __amdgpu_buffer_rsrc_t ad, rhs;
+};
+__device__ __forceinline__ TailSrc tail_src(const TailArgs &A, int n) {
+  return {__builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(A.Ad), 0, n * A.ld * 8, 0x00020000),
+          __builtin_amdgcn_make_buffer_rsrc(A.rhs + 7 * A.c0, 0, n * 8, 0x00020000)};
+}
+__device__ __forceinline__ double tail_entry(const TailArgs &A, const TailSrc &T, int n, int i, int j) {
+  constexpr int kFar = 0x7fff0000;
+  const bool pad = j >= n || i > n, rrow = i == n;
+  const int ao = (!pad && !rrow) ? (i * A.ld + j) * 8 : kFar;
+  const int ro = (!pad && rrow) ? j * 8 : kFar;
+  const unsigned long long a = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_raw_buffer_load_b64(T.ad, ao, 0, 0));
+  const unsigned long long r = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_raw_buffer_load_b64(T.rhs, ro, 0, 0));
+  // at most one of the three is non-zero (the other loads read 0): OR, not a
+  // select, so the loads stay unconditional
+  const unsigned long long p = (pad && j >= n && i == j) ? 0x3ff0000000000000ull : 0ull;
+  return __builtin_bit_cast(double, a | r | p);
 }
 
 // Diagonal tile (one wave, round 2): the tile stays in the MFMA C layout it
@@ -3358,10 +3374,29 @@ __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], doub
   for (int r = 0; r < 4; r++) Wk[lk + 4 * r][lr] = M[r];
   return bad;
 }
+// Not inlined: each tail workgroup factors its diagonal tile(s) once, so the
+// ~600 instructions run from a cold instruction cache (measured ~2.5 us per
+// tile, ~4x the MFMA / LDS latencies it is made of). One copy of the code, run
+// once on a dummy tile while the workgroup waits for its updates
+// (tail_diag_warm), is then hot when the real tile arrives.
+__device__ __noinline__ bool tail_diag_full(f64x4 a, double (*Wk)[17], double *yv_k, int lane) {
+  return tail_diag_mfma_t<true>(a, Wk, yv_k, 16, -1, lane);
+}
+__device__ __noinline__ bool tail_diag_part(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row, int lane) {
+  return tail_diag_mfma_t<false>(a, Wk, yv_k, jv, rhs_row, lane);
+}
 __device__ __forceinline__ bool tail_diag_mfma(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row,
                                                int lane) {
-  return jv == 16 ? tail_diag_mfma_t<true>(a, Wk, yv_k, jv, rhs_row, lane)
-                  : tail_diag_mfma_t<false>(a, Wk, yv_k, jv, rhs_row, lane);
+  return jv == 16 ? tail_diag_full(a, Wk, yv_k, lane) : tail_diag_part(a, Wk, yv_k, jv, rhs_row, lane);
+}
+// the warm-up: an identity tile through the same call (W lands in Wk before
+// the real factor overwrites it; y' goes to the dummy yv_k)
+__device__ __forceinline__ void tail_diag_warm(double (*Wk)[17], double *yv_dummy, int jv, int rhs_row, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+  f64x4 e;
+#pragma unroll
+  for (int r = 0; r < 4; r++) e[r] = (lk + 4 * r == lr) ? 1.0 : 0.0;
+  (void)tail_diag_mfma(e, Wk, yv_dummy, jv, rhs_row, lane);
 }
 
 __device__ __forceinline__ int tail_tile(int I, int J) { return I * (I + 1) / 2 + J; }
@@ -3378,6 +3413,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
   __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
   __shared__ int fail_s;
   const int n = 7 * A.nc;
+  const TailSrc TS = tail_src(A, n);
   const int TC = (n + 15) / 16, TR = (n + 16) / 16;  // tile columns; tile rows incl. the RHS row n
   const int In = n / 16, rn = n - 16 * In;             // RHS row: tile row, local row
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -3402,7 +3438,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_llt_kernel(TailArgs A) {
       f64x4 v = {0.0, 0.0, 0.0, 0.0};
       if (I < TR) {
 #pragma unroll
-        for (int r = 0; r < 4; r++) v[r] = tail_entry(A, n, 16 * I + lr, 16 * k + lk + 4 * r);
+        for (int r = 0; r < 4; r++) v[r] = tail_entry(A, TS, n, 16 * I + lr, 16 * k + lk + 4 * r);
       }
       acc[u] = v;
     }
@@ -3547,6 +3583,7 @@ struct TailSync {
   double *ypg;     // y' of every tile column [16 TC]
   double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout (back-substitution A operands)
   double *LgG;     // the L tiles as tagged granules, [tile][64][4] x {double, epoch tag, 0} (16 B; zeroed per call)
+  int warm;        // 1: warm the diagonal factor's code on a dummy tile first (tail_diag_warm)
 };
 constexpr size_t kTailGranBytes = (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 64 * 4 * 16;
 
@@ -3761,6 +3798,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
   __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
   __shared__ int fail_s, wready;
   const int n = 7 * A.nc;
+  const TailSrc TS = tail_src(A, n);
   const int TC = (n + 15) / 16, TR = (n + 16) / 16;
   const int In = n / 16, rn = n - 16 * In;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -3786,7 +3824,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     f64x4 v = {0.0, 0.0, 0.0, 0.0};
     if (live(u)) {
 #pragma unroll
-      for (int r = 0; r < 4; r++) v[r] = tail_entry(A, n, 16 * rowI(u) + lr, 16 * J + lk + 4 * r);
+      for (int r = 0; r < 4; r++) v[r] = tail_entry(A, TS, n, 16 * rowI(u) + lr, 16 * J + lk + 4 * r);
     }
     acc[u] = v;
   }
@@ -3804,6 +3842,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
       }
     }
   };
+  if (wave == 0 && J > 0 && S.warm) tail_diag_warm(Wk, xv + 16 * J, min(16, n - 16 * J), In == J ? rn : -1, lane);
   f64x4 rk_last = {0.0, 0.0, 0.0, 0.0};  // tile L(J, J-1): waves 1..3 apply column J - 1 row by row below
   for (int k = 0; k < J; k++) {
     GranTile gk;
@@ -3947,6 +3986,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
   __shared__ f64x4 Lsub[64];  // L(J1, J0) in operand order (waves 1..3 update their J1 tiles with it)
   __shared__ int fail_s, wready[2], lready;
   const int n = 7 * A.nc;
+  const TailSrc TS = tail_src(A, n);
   const int TC = (n + 15) / 16, TR = (n + 16) / 16;
   const int In = n / 16, rn = n - 16 * In;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -3972,10 +4012,10 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     if (live(u)) {
       const int I = rowI(u);
 #pragma unroll
-      for (int r = 0; r < 4; r++) v0[r] = tail_entry(A, n, 16 * I + lr, 16 * J0 + lk + 4 * r);
+      for (int r = 0; r < 4; r++) v0[r] = tail_entry(A, TS, n, 16 * I + lr, 16 * J0 + lk + 4 * r);
       if (jn == 2 && I >= J1) {
 #pragma unroll
-        for (int r = 0; r < 4; r++) v1[r] = tail_entry(A, n, 16 * I + lr, 16 * J1 + lk + 4 * r);
+        for (int r = 0; r < 4; r++) v1[r] = tail_entry(A, TS, n, 16 * I + lr, 16 * J1 + lk + 4 * r);
       }
     }
     acc0[u] = v0;
@@ -3997,6 +4037,8 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
 #pragma unroll
     for (int q = 0; q < 4; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-key[q], ri[q], acc, 0, 0, 0);
   };
+  if (wave == 0 && J0 > 0 && S.warm)
+    tail_diag_warm(Wk[0], xv + 16 * J0, min(16, n - 16 * J0), In == J0 ? rn : -1, lane);
   f64x4 rk0_last = {0.0, 0.0, 0.0, 0.0}, rk1_last = {0.0, 0.0, 0.0, 0.0};
   for (int k = 0; k < J0; k++) {
     // the pair's two key tiles L(J0, k), L(J1, k): both loads in flight, one poll
@@ -4131,6 +4173,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     // at once. (Per tile the same updates in the same order.)
     bool have_w0 = false, have_l = false, have_w1 = false;
     f64x4 ls = {0.0, 0.0, 0.0, 0.0};
+    if (lane == 0) M3S_CSTAMP(2, 1000 + 16 * J0 + 15, wave);
 #pragma unroll
     for (int u = 0; u < kRC; u++) {
       const int I = rowI(u);
@@ -4176,6 +4219,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
             for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J1 + lk + 4 * r, d[r]);
           }
         }
+        if (lane == 0 && u < 15) M3S_CSTAMP(2, 1000 + 16 * J0 + u, wave);
       }
     }
     // the L tiles for the back-substitution, after every hand-off
@@ -4676,6 +4720,7 @@ struct Knobs {
   std::atomic<int> gather_lds{1};      // 0: the round-2 VGPR-staged gathering kernel (bitwise reference)
   std::atomic<int> subtree{0};         // 1: the subtree kernels (one LDS workgroup per subtree; measured slower)
   std::atomic<int> tail_pair{1};       // 0: tail_cyc_kernel (one tile column per workgroup)
+  std::atomic<int> tail_warm{1};       // 0: no warm-up of the tail's diagonal factor code
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -4694,6 +4739,7 @@ struct Knobs {
     env("M3S_BORDER_SPLIT", border_split);
     env("M3S_SUBTREE", subtree);
     env("M3S_TAIL_PAIR", tail_pair);
+    env("M3S_TAIL_WARM", tail_warm);
 #endif
   }
 };
@@ -4712,6 +4758,7 @@ inline int drop_item_knob() { return knobs().debug_drop_item; }
 bool gather_lds_path() { return knobs().gather_lds != 0; }
 inline bool subtree_path() { return knobs().subtree != 0; }
 inline bool tail_pair_path() { return knobs().tail_pair != 0; }
+inline bool tail_warm_knob() { return knobs().tail_warm != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -4723,6 +4770,7 @@ constexpr int drop_item_knob() { return -1; }
 bool gather_lds_path() { return true; }
 constexpr bool subtree_path() { return false; }
 constexpr bool tail_pair_path() { return true; }
+constexpr bool tail_warm_knob() { return true; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -5140,6 +5188,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.ypg = T.Wg + (size_t)kTailMaxT * 256;
           Y.LgT = Y.ypg + 16 * kTailMaxT;
           Y.LgG = tail + tail_gran_offset_doubles();
+          Y.warm = tail_warm_knob() ? 1 : 0;
           const int TC = (7 * meta.nc + 15) / 16;
           if (tail_pair_path())
             tail_pair_kernel<<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
@@ -6448,7 +6497,7 @@ int m3s_set_knob(const char *name, int value) {
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
              {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
-             {"tail_pair", &k.tail_pair}
+             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}
 #endif
   };
   for (const auto &t : tab)

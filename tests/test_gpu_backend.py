@@ -633,3 +633,20 @@ def test_pipelined_gathering_launch_matches_round2_kernel_bitwise(test_lib, be, 
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
     assert int(out[1][2][be.INFO_SOLVE_FAIL]) == 0
+
+
+@pytest.mark.parametrize("N", [140, 256])
+def test_tail_warmup_leaves_factor_bitwise(test_lib, be, N, knobs):
+    """The warm-up run of the tail's diagonal factor on a dummy tile (round 4:
+    the code is hot when the real tile arrives) writes only scratch that the
+    real factor overwrites: poses and dx agree bitwise with it off."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 12, 16, seed=950 + N)
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    knobs("tail_warm", "0")
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
+    np.testing.assert_array_equal(dx_a, dx_b)
+    np.testing.assert_array_equal(T_a, T_b)

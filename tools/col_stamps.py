@@ -99,6 +99,12 @@ if TC:
         for J0 in range(0, TC - 1, 2):
             v = [(T[800 + J0, i] - tt0) / 100.0 for i in range(4)] + [(T[900 + J0, 0] - tt0) / 100.0]
             print(f"  J0={J0:2d} " + " ".join(f"{x:8.2f}" for x in v))
+    if T[1000 + 15, 1]:
+        print("  pair kernel, waves 1..3: k-loop done / each row done (us)")
+        for J0 in range(0, min(TC - 1, 8), 2):
+            for w in (1, 2, 3):
+                row = [T[1000 + 16 * J0 + 15, w]] + [T[1000 + 16 * J0 + u, w] for u in range(11)]
+                print(f"  J0={J0:2d} w{w} " + " ".join(f"{(x - tt0) / 100.0:7.2f}" for x in row if x))
     print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")
     if T[699, 0]:
         print(f"  back-substitution: flags seen {(T[698, 0] - tt0) / 100.0:.2f}, loop start {(T[699, 0] - tt0) / 100.0:.2f}; "

@@ -223,77 +223,82 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
 // (matching_kernels.cu:25-81.)
 constexpr int kRefTile = 16;
 constexpr int kRefLdsBytes = 144 * 1024;
+constexpr int kRefNear = 32;  // centres within this many pixels of the anchor set the box
 
 template <typename T, int FMAX>
 __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_args A, int tiles_x, int tiles_per_b,
                                                                    int tiled) {
+  constexpr int EV = 16 / (int)sizeof(T);  // elements per 16-B vector
+  static_assert(FMAX % EV == 0, "16-B vectors per pixel");
+  constexpr int NV = FMAX / EV;            // vectors per pixel
+  typedef T TV __attribute__((ext_vector_type(EV)));
   extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
-  __shared__ int red[4];
-  constexpr int VB = FMAX * (int)sizeof(T);  // bytes per pixel (a multiple of 16)
-  static_assert(VB % 16 == 0, "16-B vectors per pixel");
-  constexpr int NV = VB / 16;
+  TV *Ls = reinterpret_cast<TV *>(rsm);
+  __shared__ int red[8];
   const int tid = threadIdx.x;
-  const int64_t b = blockIdx.x / tiles_per_b;
-  const int tb = (int)(blockIdx.x - b * tiles_per_b);
-  const int64_t H = A.H, W = A.W;
-  int64_t n;
+  const int b = (int)(blockIdx.x / tiles_per_b);
+  const int tb = (int)(blockIdx.x - (unsigned)b * tiles_per_b);
+  const int H = (int)A.H, W = (int)A.W;
+  int n;
   bool valid;
   if (tiled) {
     const int x = (tb % tiles_x) * kRefTile + tid % kRefTile, y = (tb / tiles_x) * kRefTile + tid / kRefTile;
     valid = x < W && y < H;
-    n = (int64_t)y * W + x;
+    n = y * W + x;
   } else {
-    n = (int64_t)tb * kMatchThreads + tid;
+    n = tb * kMatchThreads + tid;
     valid = n < A.N;
   }
-  const int64_t gid = b * A.N + n;
-  const T *D11 = static_cast<const T *>(A.D11) + b * H * W * FMAX;
-  T q[FMAX];
-  int64_t u0 = 0, v0 = 0;
-  if (valid) {
-    const T *d21 = static_cast<const T *>(A.D21) + gid * FMAX;
+  const int64_t gid = (int64_t)b * A.N + n;
+  const TV *Dv = reinterpret_cast<const TV *>(static_cast<const T *>(A.D11) + (int64_t)b * H * W * FMAX);
+  TV q[NV];
+  int u0 = 0, v0 = 0;
+  {
+    const TV *d21 = reinterpret_cast<const TV *>(static_cast<const T *>(A.D21) + (valid ? gid : 0) * FMAX);
 #pragma unroll
-    for (int k = 0; k < FMAX; k++) q[k] = d21[k];
-    u0 = A.p1[2 * gid], v0 = A.p1[2 * gid + 1];
+    for (int c = 0; c < NV; c++) q[c] = d21[c];
+    if (valid) u0 = (int)A.p1[2 * gid], v0 = (int)A.p1[2 * gid + 1];
   }
   T max_score = min_normal<T>();
-  int64_t u_new = u0, v_new = v0;
-  const int cap_px = kRefLdsBytes / VB;
+  int u_new = u0, v_new = v0;
+  const int cap_px = kRefLdsBytes / (16 * NV);
   for (int d = A.dilation_max; d > 0; d--) {
     const int rd = A.radius * d;
-    // the box of this dilation's windows (ints: image coordinates fit)
-    if (tid == 0) red[0] = INT32_MAX, red[1] = INT32_MIN, red[2] = INT32_MAX, red[3] = INT32_MIN;
+    // the box of this dilation's windows over the centres near the tile's
+    // anchor (its middle query, or the first valid one): a few far-off
+    // matches (occluded pixels) would otherwise blow the box past LDS and
+    // leave the whole tile on global reads; they read D11 directly instead
+    if (tid == 0) red[0] = INT32_MAX, red[1] = INT32_MIN, red[2] = INT32_MAX, red[3] = INT32_MIN, red[4] = INT32_MAX;
     __syncthreads();
-    if (valid) {
-      const int ui = (int)max<int64_t>(min<int64_t>(u0, INT32_MAX / 2), INT32_MIN / 2);
-      const int vi = (int)max<int64_t>(min<int64_t>(v0, INT32_MAX / 2), INT32_MIN / 2);
-      atomicMin(&red[0], ui), atomicMax(&red[1], ui), atomicMin(&red[2], vi), atomicMax(&red[3], vi);
-    }
+    if (valid) atomicMin(&red[4], tid == kMatchThreads / 2 + kRefTile / 2 ? -1 : tid);
     __syncthreads();
-    const int64_t bx0 = max<int64_t>((int64_t)red[0] - rd, 0), bx1 = min<int64_t>((int64_t)red[1] + rd, W - 1);
-    const int64_t by0 = max<int64_t>((int64_t)red[2] - rd, 0), by1 = min<int64_t>((int64_t)red[3] + rd, H - 1);
-    const int64_t bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
-    const bool staged = bw > 0 && bh > 0 && bw * bh <= cap_px;
+    const int at = red[4] < 0 ? kMatchThreads / 2 + kRefTile / 2 : red[4];
+    if (tid == at) red[5] = u0, red[6] = v0;
+    __syncthreads();
+    if (valid && abs(u0 - red[5]) <= kRefNear && abs(v0 - red[6]) <= kRefNear)
+      atomicMin(&red[0], u0), atomicMax(&red[1], u0), atomicMin(&red[2], v0), atomicMax(&red[3], v0);
+    __syncthreads();
+    const int bx0 = max(red[0] - rd, 0), bx1 = min(red[1] + rd, W - 1);
+    const int by0 = max(red[2] - rd, 0), by1 = min(red[3] + rd, H - 1);
+    const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+    const bool staged = red[0] <= red[1] && bw > 0 && bh > 0 && bw * bh <= cap_px;
     __syncthreads();  // red read by every lane before the next dilation rewrites it
     if (staged) {
-      const int nvec = (int)(bw * bh) * NV;
-      const uint4 *src = reinterpret_cast<const uint4 *>(D11);
-      uint4 *dst = reinterpret_cast<uint4 *>(rsm);
-      for (int i0 = 0; i0 < nvec; i0 += 8 * kMatchThreads) {
-        uint4 v[8];
+      // box rows are contiguous in D11: 16-B loads, four in flight per lane
+      const int nvec = bw * bh * NV;
+      for (int i0 = 0; i0 < nvec; i0 += 4 * kMatchThreads) {
+        TV v[4];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int i = i0 + u * kMatchThreads + tid;
-          if (i < nvec) {
-            const int px = i / NV, c = i - px * NV;
-            const int64_t yy = by0 + px / bw, xx = bx0 + px % bw;
-            v[u] = src[(yy * W + xx) * NV + c];
-          }
+        for (int u = 0; u < 4; u++) {
+          const int i = min(i0 + u * kMatchThreads + tid, nvec - 1);
+          const int px = i / NV, c = i - px * NV;
+          const int yy = by0 + px / bw, xx = bx0 + px % bw;
+          v[u] = Dv[(yy * W + xx) * NV + c];
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 4; u++) {
           const int i = i0 + u * kMatchThreads + tid;
-          if (i < nvec) dst[i] = v[u];
+          if (i < nvec) Ls[i] = v[u];
         }
       }
     }
@@ -303,24 +308,25 @@ __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_ar
       // time: their FMA chains run interleaved, then they are compared in order
       const int nw = 2 * A.radius + 1;
       constexpr int G = 4;
-      constexpr int EV = 16 / (int)sizeof(T);  // elements per 16-B vector
       for (int i = 0; i < nw; i++) {
-        const int64_t u = u0 - rd + (int64_t)i * d;
+        const int u = u0 - rd + i * d;
+        const bool ucol = u >= 0 && u < W, ubox = staged && u >= bx0 && u <= bx1;
         for (int j0 = 0; j0 < nw; j0 += G) {
-          T x[G][FMAX];
+          TV x[G][NV];
           bool ok[G];
 #pragma unroll
           for (int g = 0; g < G; g++) {
-            const int64_t v = v0 - rd + (int64_t)(j0 + g) * d;
-            ok[g] = j0 + g < nw && v >= 0 && v < H && u >= 0 && u < W;
-            const bool in_box = staged && u >= bx0 && u <= bx1 && v >= by0 && v <= by1;
-            const uint4 *pv;
-            if (in_box)
-              pv = reinterpret_cast<const uint4 *>(rsm) + ((v - by0) * bw + (u - bx0)) * NV;
-            else  // (a candidate outside the image reads pixel 0 and is discarded)
-              pv = reinterpret_cast<const uint4 *>(D11 + (ok[g] ? (v * W + u) * FMAX : 0));
+            const int v = v0 - rd + (j0 + g) * d;
+            ok[g] = j0 + g < nw && ucol && v >= 0 && v < H;
+            if (ubox && v >= by0 && v <= by1) {
+              const TV *pl = Ls + ((v - by0) * bw + (u - bx0)) * NV;
 #pragma unroll
-            for (int c = 0; c < NV; c++) *reinterpret_cast<uint4 *>(&x[g][c * EV]) = pv[c];
+              for (int c = 0; c < NV; c++) x[g][c] = pl[c];
+            } else {  // (a candidate outside the image reads pixel 0 and is discarded)
+              const TV *pg = Dv + (ok[g] ? (v * W + u) * NV : 0);
+#pragma unroll
+              for (int c = 0; c < NV; c++) x[g][c] = pg[c];
+            }
           }
           T score[G];
 #pragma unroll
@@ -328,13 +334,13 @@ __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_ar
 #pragma unroll
           for (int k = 0; k < FMAX; k++)
 #pragma unroll
-            for (int g = 0; g < G; g++) score[g] = __builtin_elementwise_fma(q[k], x[g][k], score[g]);
+            for (int g = 0; g < G; g++) score[g] = __builtin_elementwise_fma(q[k / EV][k % EV], x[g][k / EV][k % EV], score[g]);
 #pragma unroll
           for (int g = 0; g < G; g++) {
             if (ok[g] && score[g] > max_score) {
               max_score = score[g];
               u_new = u;
-              v_new = v0 - rd + (int64_t)(j0 + g) * d;
+              v_new = v0 - rd + (j0 + g) * d;
             }
           }
         }
@@ -353,8 +359,10 @@ __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_ar
 template <typename T>
 int launch_refine(const m3s_refine_args &a, hipStream_t st) {
   // LDS-staged windows for 16-B multiples of descriptor bytes (f16: F = 8k)
+  // (int image arithmetic: H W F and the pixel coordinates fit 31 bits)
   const bool vec = (a.F * (int64_t)sizeof(T)) % 16 == 0 && (a.F == 16 || a.F == 24 || a.F == 32) &&
-                   reinterpret_cast<uintptr_t>(a.D11) % 16 == 0;
+                   reinterpret_cast<uintptr_t>(a.D11) % 16 == 0 && reinterpret_cast<uintptr_t>(a.D21) % 16 == 0 &&
+                   a.H * a.W * a.F < (int64_t)1 << 30 && a.N < (int64_t)1 << 30;
   if (vec && refine_staged_knob()) {
     const bool tiled = a.N == a.H * a.W;
     const int tiles_x = (int)((a.W + kRefTile - 1) / kRefTile);

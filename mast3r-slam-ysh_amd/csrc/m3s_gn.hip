@@ -1505,12 +1505,15 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// 1/sqrt(d) for d > 0: hardware estimate + two Newton steps (~full fp64
-// precision, no IEEE division/sqrt sequences on the pivot chain)
+// 1/sqrt(d) for d > 0: hardware estimate + one Newton step, no IEEE
+// division/sqrt sequences on the pivot chain. Measured on gfx950
+// (tools/ubench_icache.hip, 16M inputs over 2^-30..2^30): v_rsq_f64 alone
+// 5.2e-8 relative, one step 4.2e-15, two steps 3.0e-16; the factor's inputs
+// are fp32 sums, so the second step (4 dependent fp64 ops per pivot on the
+// DIAG chain) bought nothing measurable.
 __device__ __forceinline__ double rsqrt_nr(double d) {
   double x = __builtin_amdgcn_rsq(d);
   const double hd = 0.5 * d;
-  x = x * (1.5 - hd * x * x);
   x = x * (1.5 - hd * x * x);
   return x;
 }
@@ -4185,6 +4188,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
           mma(acc0[u], rk0_last, ri);
           if (jn == 2) mma(acc1[u], rk1_last, ri);
         }
+        if (tid == 64 && u < 8) M3S_CSTAMP(2, 1300 + 16 * J0 + u, 0);
         if (!have_w0) {
           if (tid == 64) M3S_CSTAMP(2, 800 + J0, 0);
           wait_lds(&wready[0]);
@@ -4193,6 +4197,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
         }
         const f64x4 d0 = panel(acc0[u], 0);
         gran_store(R, tail_tile(I, J0), lane, d0, want);
+        if (tid == 64 && u < 8) M3S_CSTAMP(2, 1300 + 16 * J0 + u, 1);
         if (I == In && lr == rn) {
 #pragma unroll
           for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J0 + lk + 4 * r, d0[r]);
@@ -4213,6 +4218,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
           }
           const f64x4 d = panel(acc1[u], 1);
           gran_store(R, tail_tile(I, J1), lane, d, want);
+          if (tid == 64 && u < 8) M3S_CSTAMP(2, 1300 + 16 * J0 + u, 3);
           if (I == J1 + 1 && tid == 64) M3S_CSTAMP(2, J1, 0);
           if (I == In && lr == rn) {
 #pragma unroll

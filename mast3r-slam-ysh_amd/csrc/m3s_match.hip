@@ -26,13 +26,14 @@ constexpr int kMatchThreads = 256;
 
 inline int launch_status() { return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH; }
 
-// M3S_REFINE_STAGED=0: refine_matches on the round-3 global-read kernel (A/B)
-bool refine_staged_knob() {
-  static const bool on = [] {
+// M3S_REFINE_STAGED (A/B): 0 = the round-3 global-read kernel, 1 = windows
+// staged in LDS, 2 (default) = four candidates interleaved, global reads
+int refine_staged_knob() {
+  static const int v = [] {
     const char *e = std::getenv("M3S_REFINE_STAGED");
-    return !(e && std::atoi(e) == 0);
+    return e ? std::atoi(e) : 2;
   }();
-  return on;
+  return v;
 }
 
 // ------------------------------------------------------------ iter_proj --
@@ -225,7 +226,7 @@ constexpr int kRefTile = 16;
 constexpr int kRefLdsBytes = 144 * 1024;
 constexpr int kRefNear = 32;  // centres within this many pixels of the anchor set the box
 
-template <typename T, int FMAX>
+template <typename T, int FMAX, bool STAGE>
 __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_args A, int tiles_x, int tiles_per_b,
                                                                    int tiled) {
   constexpr int EV = 16 / (int)sizeof(T);  // elements per 16-B vector
@@ -281,7 +282,7 @@ __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_ar
     const int bx0 = max(red[0] - rd, 0), bx1 = min(red[1] + rd, W - 1);
     const int by0 = max(red[2] - rd, 0), by1 = min(red[3] + rd, H - 1);
     const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
-    const bool staged = red[0] <= red[1] && bw > 0 && bh > 0 && bw * bh <= cap_px;
+    const bool staged = STAGE && red[0] <= red[1] && bw > 0 && bh > 0 && bw * bh <= cap_px;
     __syncthreads();  // red read by every lane before the next dilation rewrites it
     if (staged) {
       // box rows are contiguous in D11: 16-B loads, four in flight per lane
@@ -363,7 +364,7 @@ int launch_refine(const m3s_refine_args &a, hipStream_t st) {
   const bool vec = (a.F * (int64_t)sizeof(T)) % 16 == 0 && (a.F == 16 || a.F == 24 || a.F == 32) &&
                    reinterpret_cast<uintptr_t>(a.D11) % 16 == 0 && reinterpret_cast<uintptr_t>(a.D21) % 16 == 0 &&
                    a.H * a.W * a.F < (int64_t)1 << 30 && a.N < (int64_t)1 << 30;
-  if (vec && refine_staged_knob()) {
+  if (vec && refine_staged_knob() != 0) {
     const bool tiled = a.N == a.H * a.W;
     const int tiles_x = (int)((a.W + kRefTile - 1) / kRefTile);
     const int tiles_per_b = tiled ? tiles_x * (int)((a.H + kRefTile - 1) / kRefTile)
@@ -371,16 +372,24 @@ int launch_refine(const m3s_refine_args &a, hipStream_t st) {
     const unsigned blocks = (unsigned)(a.B * tiles_per_b);
     static bool attr = false;
     if (!attr) {
-      for (const void *f : {reinterpret_cast<const void *>(refine_lds_kernel<T, 16>),
-                            reinterpret_cast<const void *>(refine_lds_kernel<T, 24>),
-                            reinterpret_cast<const void *>(refine_lds_kernel<T, 32>)})
+      for (const void *f : {reinterpret_cast<const void *>(refine_lds_kernel<T, 16, true>),
+                            reinterpret_cast<const void *>(refine_lds_kernel<T, 24, true>),
+                            reinterpret_cast<const void *>(refine_lds_kernel<T, 32, true>)})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRefLdsBytes);
       attr = true;
     }
-    switch (a.F) {
-      case 16: refine_lds_kernel<T, 16><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
-      case 24: refine_lds_kernel<T, 24><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
-      default: refine_lds_kernel<T, 32><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+    if (refine_staged_knob() == 1) {
+      switch (a.F) {
+        case 16: refine_lds_kernel<T, 16, true><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+        case 24: refine_lds_kernel<T, 24, true><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+        default: refine_lds_kernel<T, 32, true><<<blocks, kMatchThreads, kRefLdsBytes, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+      }
+    } else {
+      switch (a.F) {
+        case 16: refine_lds_kernel<T, 16, false><<<blocks, kMatchThreads, 0, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+        case 24: refine_lds_kernel<T, 24, false><<<blocks, kMatchThreads, 0, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+        default: refine_lds_kernel<T, 32, false><<<blocks, kMatchThreads, 0, st>>>(a, tiles_x, tiles_per_b, tiled); break;
+      }
     }
     return launch_status();
   }

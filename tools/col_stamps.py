@@ -105,6 +105,15 @@ if TC:
             for w in (1, 2, 3):
                 row = [T[1000 + 16 * J0 + 15, w]] + [T[1000 + 16 * J0 + u, w] for u in range(11)]
                 print(f"  J0={J0:2d} w{w} " + " ".join(f"{(x - tt0) / 100.0:7.2f}" for x in row if x))
+    if T[1300, 1]:
+        print("  pair kernel, wave 1 rows: (row start, J0 tile stored, J1 tile stored) us")
+        for J0 in range(0, min(TC - 1, 6), 2):
+            cells = []
+            for u in range(8):
+                r = T[1300 + 16 * J0 + u]
+                if r[0]:
+                    cells.append("(" + ",".join(f"{(r[i] - tt0) / 100.0:.2f}" for i in (0, 1, 3)) + ")")
+            print(f"  J0={J0:2d} " + " ".join(cells))
     print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")
     if T[699, 0]:
         print(f"  back-substitution: flags seen {(T[698, 0] - tt0) / 100.0:.2f}, loop start {(T[699, 0] - tt0) / 100.0:.2f}; "

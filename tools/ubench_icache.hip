@@ -139,6 +139,26 @@ __global__ void k_diag(double *out, long long *t) {
   out[lane] = a[0] + a[1] + a[2] + a[3];
 }
 
+// accuracy of v_rsq_f64 and of one / two Newton steps on it, vs 1/sqrt in fp64
+__global__ void k_rsq_acc(double *err, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+  for (int i = t; i < n; i += gridDim.x * blockDim.x) {
+    const double d = ldexp(1.0 + (double)((i * 2654435761u) % 1000003u) / 1000003.0, (i % 61) - 30);
+    const double ref = 1.0 / sqrt(d);
+    double x = __builtin_amdgcn_rsq(d);
+    e0 = fmax(e0, fabs(x - ref) / ref);
+    const double hd = 0.5 * d;
+    x = x * (1.5 - hd * x * x);
+    e1 = fmax(e1, fabs(x - ref) / ref);
+    x = x * (1.5 - hd * x * x);
+    e2 = fmax(e2, fabs(x - ref) / ref);
+  }
+  atomicMax(reinterpret_cast<unsigned long long *>(err + 0), (unsigned long long)__double_as_longlong(e0));
+  atomicMax(reinterpret_cast<unsigned long long *>(err + 1), (unsigned long long)__double_as_longlong(e1));
+  atomicMax(reinterpret_cast<unsigned long long *>(err + 2), (unsigned long long)__double_as_longlong(e2));
+}
+
 #define CK(x)                                                         \
   do {                                                                \
     hipError_t e = (x);                                               \
@@ -153,6 +173,15 @@ int main() {
   long long *t, h[4];
   CK(hipMalloc(&out, 64 * 8));
   CK(hipMalloc(&t, 32));
+  {
+    double *err, he[3];
+    CK(hipMalloc(&err, 24));
+    CK(hipMemset(err, 0, 24));
+    k_rsq_acc<<<256, 256>>>(err, 1 << 24);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(he, err, 24, hipMemcpyDeviceToHost));
+    printf("v_rsq_f64 max rel error: raw %.3e, 1 Newton step %.3e, 2 steps %.3e (2^-52 = 2.2e-16)\n", he[0], he[1], he[2]);
+  }
   for (int rep = 0; rep < 2; rep++) {
     k_icache<<<1, 64>>>(out, t);
     CK(hipDeviceSynchronize());

@@ -2035,19 +2035,24 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   const bool lazy_asm = asm_in && D.nc == 0 && phase == 0;
   double *fl = reinterpret_cast<double *>(sdone + ((n_flags + 1) & ~1));  // staged fin (asm_in)
   {
+    // buffer loads: unconditional (an index past the end reads 0 with no
+    // access), so all 12 of a round are in flight together; guarded pointer
+    // loads compiled to one branch and one vmcnt(0) each (~5 us at C3)
     const int np_ = STORE == 1 ? D.plan_len : 0, nf_ = asm_in ? D.E * kFin : 0;
+    const __amdgpu_buffer_rsrc_t Rpl = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(D.plan), 0, 4 * np_, 0x00020000);
+    const __amdgpu_buffer_rsrc_t Rfn = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(D.fin), 0, 8 * nf_, 0x00020000);
     for (int r = 0; r * 4096 < np_ || r * 8192 < nf_; r++) {
       int32_t pv[4];
       double fv[8];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         const int i = r * 4096 + u * 1024 + tid;
-        if (i < np_) pv[u] = D.plan[i];
+        pv[u] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(Rpl, 4 * i, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int i = r * 8192 + u * 1024 + tid;
-        if (i < nf_) fv[u] = D.fin[i];
+        fv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(Rfn, 8 * i, 0, 0));
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {

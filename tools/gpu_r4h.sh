@@ -7,3 +7,4 @@ tail -1 $OUT/r4h_tests1.log
 for k in 2 1 0; do M3S_REFINE_STAGED=$k timeout -k 10 120 python -u tools/refine_time.py 2>&1 | grep -v amdgpu.ids; done
 N=256 M3S_SUBTREE=0 timeout -k 10 200 python -u tools/col_stamps.py variants/lib_colst.so > $OUT/r4h_stamps.txt 2>&1 || { echo "stamps failed"; tail -20 $OUT/r4h_stamps.txt; exit 1; }
 grep -A60 "pair kernel, waves" $OUT/r4h_stamps.txt
+timeout -k 5 60 ./variants/ubench_diag7

@@ -1664,7 +1664,26 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
                                                int lane49, int lane, double *stg, const int32_t *wflag = nullptr,
                                                int want = 0, bool *ok = nullptr) {
   if (!STAGE) {
+    // four products at a time: their index and block loads in flight together
+    // and four independent FMA chains; subtracted in list order (bitwise the
+    // same sums as one at a time). C3's DIAG items sum ~10 products after
+    // their pickup: ~250 cycles each one by one (round-4 LLT stamps)
     int q = q0;
+    for (; q + 3 < q1; q += 4) {
+      const double *A[4], *B[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        A[u] = Lb + (size_t)sa[q + u] * 49;
+        B[u] = SAME ? A[u] : Lb + (size_t)sb[q + u] * 49;
+      }
+      double sx[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) sx[u] += A[u][r7 + mm] * B[u][c7 + mm];
+#pragma unroll
+      for (int u = 0; u < 4; u++) v -= sx[u];
+    }
     for (; q + 1 < q1; q += 2) {
       const double *A0 = Lb + (size_t)sa[q] * 49, *A1 = Lb + (size_t)sa[q + 1] * 49;
       const double *B0 = SAME ? A0 : Lb + (size_t)sb[q] * 49, *B1 = SAME ? A1 : Lb + (size_t)sb[q + 1] * 49;
@@ -1743,7 +1762,20 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
                                              const int32_t *vidx, int q0, int q1, const double *y,
                                              int lane7, int lane49, int lane, double *stg) {
   if (!STAGE) {
-    for (int q = q0; q < q1; q++) {
+    int q = q0;
+    for (; q + 3 < q1; q += 4) {  // (as sub_products: four in flight, subtracted in list order)
+      const double *A[4], *yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) A[u] = Lb + (size_t)slot[q + u] * 49, yv[u] = y + (size_t)vidx[q + u] * 7;
+      double tx[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) tx[u] += (TRANS ? A[u][mm * 7 + lane7] : A[u][lane7 * 7 + mm]) * yv[u][mm];
+#pragma unroll
+      for (int u = 0; u < 4; u++) acc -= tx[u];
+    }
+    for (; q < q1; q++) {
       const double *A = Lb + (size_t)slot[q] * 49;
       const double *yv = y + (size_t)vidx[q] * 7;
       double t0 = 0.0;

@@ -27,11 +27,12 @@ constexpr int kMatchThreads = 256;
 inline int launch_status() { return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH; }
 
 // M3S_REFINE_STAGED (A/B): 0 = the round-3 global-read kernel, 1 = windows
-// staged in LDS, 2 (default) = four candidates interleaved, global reads
+// staged in LDS, 2 = four candidates interleaved per lane, 3 (default) = four
+// lanes per query (refine_split_kernel)
 int refine_staged_knob() {
   static const int v = [] {
     const char *e = std::getenv("M3S_REFINE_STAGED");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : 3;
   }();
   return v;
 }
@@ -357,6 +358,85 @@ __global__ void __launch_bounds__(kMatchThreads) refine_lds_kernel(m3s_refine_ar
   }
 }
 
+// Round 4 (default, M3S_REFINE_STAGED=3): S = 4 lanes per query. The round-3
+// kernel (one lane per query, ~245 candidates in a row, each a dependent
+// 24-FMA chain behind its loads) had only ~4 waves per SIMD for a 512 x 512
+// pair: latency-bound. Here lane s of a query's group scores the candidates
+// c = s, s + S, ... of each dilation (two at a time), keeps the first
+// occurrence of its best score (strict >, ascending c), and the group
+// combines (higher score; equal scores: lower c) with two lane shuffles: the
+// first candidate in scan order that attains the dilation's maximum, taken if
+// it beats the running maximum - exactly the sequential scan's result
+// (strict >, ties to the earlier candidate). Same fp16 FMA chain per score.
+constexpr int kRefS = 4;
+template <typename T, int FMAX>
+__global__ void __launch_bounds__(kMatchThreads) refine_split_kernel(m3s_refine_args A) {
+  constexpr int EV = 16 / (int)sizeof(T);
+  constexpr int NV = FMAX / EV;
+  typedef T TV __attribute__((ext_vector_type(EV)));
+  const int tid = threadIdx.x, sub = tid % kRefS;
+  const int64_t gq = (int64_t)blockIdx.x * (kMatchThreads / kRefS) + tid / kRefS;  // (batch, query)
+  const bool valid = gq < A.B * A.N;
+  const int64_t gid = valid ? gq : 0;
+  const int64_t b = gid / A.N;
+  const int H = (int)A.H, W = (int)A.W;
+  const TV *Dv = reinterpret_cast<const TV *>(static_cast<const T *>(A.D11) + b * (int64_t)H * W * FMAX);
+  TV q[NV];
+  {
+    const TV *d21 = reinterpret_cast<const TV *>(static_cast<const T *>(A.D21) + gid * FMAX);
+#pragma unroll
+    for (int c = 0; c < NV; c++) q[c] = d21[c];
+  }
+  int u0 = (int)A.p1[2 * gid], v0 = (int)A.p1[2 * gid + 1];
+  T max_score = min_normal<T>();
+  const int nw = 2 * A.radius + 1, ncand = nw * nw;
+  for (int d = A.dilation_max; d > 0; d--) {
+    const int rd = A.radius * d;
+    T best = (T)0.0f;
+    int bi = INT32_MAX;  // no candidate yet
+    for (int c0 = sub; c0 < ncand; c0 += 2 * kRefS) {
+      int cc[2];
+      bool ok[2];
+      TV x[2][NV];
+#pragma unroll
+      for (int g = 0; g < 2; g++) {
+        cc[g] = c0 + g * kRefS;
+        const int i = cc[g] / nw, j = cc[g] - (cc[g] / nw) * nw;
+        const int u = u0 - rd + i * d, v = v0 - rd + j * d;
+        ok[g] = cc[g] < ncand && u >= 0 && u < W && v >= 0 && v < H;
+        const TV *pg = Dv + (ok[g] ? (v * W + u) * NV : 0);
+#pragma unroll
+        for (int c = 0; c < NV; c++) x[g][c] = pg[c];
+      }
+      T sc[2] = {(T)0.0f, (T)0.0f};
+#pragma unroll
+      for (int k = 0; k < FMAX; k++)
+#pragma unroll
+        for (int g = 0; g < 2; g++) sc[g] = __builtin_elementwise_fma(q[k / EV][k % EV], x[g][k / EV][k % EV], sc[g]);
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+        if (ok[g] && (bi == INT32_MAX || sc[g] > best)) best = sc[g], bi = cc[g];
+    }
+    // the group's first maximum (lanes of a group are adjacent: xor 1, 2)
+#pragma unroll
+    for (int o = 1; o < kRefS; o <<= 1) {
+      const float bo = __shfl_xor((float)best, o, 64);
+      const int io = __shfl_xor(bi, o, 64);
+      const T bt = (T)bo;
+      if (io != INT32_MAX && (bi == INT32_MAX || bt > best || (bt == best && io < bi))) best = bt, bi = io;
+    }
+    if (bi != INT32_MAX && best > max_score) {
+      max_score = best;
+      u0 = u0 - rd + (bi / nw) * d;
+      v0 = v0 - rd + (bi - (bi / nw) * nw) * d;
+    }
+  }
+  if (valid && sub == 0) {
+    A.p1_new[2 * gid] = u0;
+    A.p1_new[2 * gid + 1] = v0;
+  }
+}
+
 template <typename T>
 int launch_refine(const m3s_refine_args &a, hipStream_t st) {
   // LDS-staged windows for 16-B multiples of descriptor bytes (f16: F = 8k)
@@ -364,6 +444,15 @@ int launch_refine(const m3s_refine_args &a, hipStream_t st) {
   const bool vec = (a.F * (int64_t)sizeof(T)) % 16 == 0 && (a.F == 16 || a.F == 24 || a.F == 32) &&
                    reinterpret_cast<uintptr_t>(a.D11) % 16 == 0 && reinterpret_cast<uintptr_t>(a.D21) % 16 == 0 &&
                    a.H * a.W * a.F < (int64_t)1 << 30 && a.N < (int64_t)1 << 30;
+  if (vec && refine_staged_knob() == 3) {
+    const unsigned blocks = (unsigned)((a.B * a.N + kMatchThreads / kRefS - 1) / (kMatchThreads / kRefS));
+    switch (a.F) {
+      case 16: refine_split_kernel<T, 16><<<blocks, kMatchThreads, 0, st>>>(a); break;
+      case 24: refine_split_kernel<T, 24><<<blocks, kMatchThreads, 0, st>>>(a); break;
+      default: refine_split_kernel<T, 32><<<blocks, kMatchThreads, 0, st>>>(a); break;
+    }
+    return launch_status();
+  }
   if (vec && refine_staged_knob() != 0) {
     const bool tiled = a.N == a.H * a.W;
     const int tiles_x = (int)((a.W + kRefTile - 1) / kRefTile);

@@ -167,6 +167,10 @@ std::pair<int, int64_t> etree_shape(int m, const BitRows &adj, const std::vector
 constexpr double kCostDiag0 = 3500.0, kCostOff0 = 900.0, kCostUpd = 250.0;
 constexpr double kCostPart0 = 150.0, kCostPartUpd = 60.0, kCostPartIn = 120.0;
 constexpr double kCostFwd0 = 1000.0, kCostFwdUpd = 200.0, kHop = 400.0;
+#ifndef M3S_SCHED_DIAG_EARLY
+#define M3S_SCHED_DIAG_EARLY 1
+#endif
+constexpr bool kDiagEarly = M3S_SCHED_DIAG_EARLY != 0;  // (A/B: -DM3S_SCHED_DIAG_EARLY=0)
 constexpr double kSlack = 300.0;  // start-time tolerance of the rank choice (small plans)
 
 static void schedule_items(SparsePlan &P) {
@@ -230,6 +234,13 @@ static void schedule_items(SparsePlan &P) {
   }
   std::vector<int> missing(n);
   std::vector<double> ready_at(n, 0.0);
+  // DIAG items may start before their last input lands: the kernel's DIAG
+  // sums its update products as they arrive, so a wave that takes it when all
+  // but the last input are out has only the last product left when it lands
+  // (round 4: C3's DIAG items were picked up after all their inputs and then
+  // summed ~10 products, 1-4k cycles, on the critical path). ready_2nd: the
+  // second-latest input's publish time.
+  std::vector<double> ready_2nd(n, 0.0);
   using Entry = std::pair<double, int>;  // (priority, -item) max-heap
   std::priority_queue<Entry> ready;
   for (int it = 0; it < n; it++) {
@@ -262,11 +273,12 @@ static void schedule_items(SparsePlan &P) {
     int it;
     if (est_first) {
       double best_est = 1e300;
-      for (int c : cand) best_est = std::min(best_est, std::max(free_at[w], ready_at[c]));
+      auto est = [&](int c) { return std::max(free_at[w], kDiagEarly && P.items[c] < 0 ? ready_2nd[c] : ready_at[c]); };
+      for (int c : cand) best_est = std::min(best_est, est(c));
       int bi = -1;
       for (int q = 0; q < (int)cand.size(); q++) {
         const int c = cand[q];
-        if (std::max(free_at[w], ready_at[c]) > best_est + kSlack) continue;
+        if (est(c) > best_est + kSlack) continue;
         if (bi < 0 || rank[c] > rank[cand[bi]] || (rank[c] == rank[cand[bi]] && c < cand[bi])) bi = q;
       }
       it = cand[bi];
@@ -276,13 +288,18 @@ static void schedule_items(SparsePlan &P) {
       it = -ready.top().second;
       ready.pop();
     }
-    const double start = std::max(free_at[w], ready_at[it]);
-    free_at[w] = start + cost[it];
-    const double published = start + pub[it] + kHop;
+    const bool early = est_first && kDiagEarly && P.items[it] < 0;
+    const double start = std::max(free_at[w], early ? ready_2nd[it] : ready_at[it]);
+    // an early DIAG: the products of the inputs out by `start` run first, the
+    // last input's product and the factor after it lands
+    const double fin = early ? std::max(start + pub[it], ready_at[it] + kCostUpd + kCostDiag0) : start + pub[it];
+    free_at[w] = fin + (cost[it] - pub[it]);
+    const double published = fin + kHop;
     pub_at[it] = published;
     P.witems.push_back(P.items[it]);
     for (int s2 : succ[it]) {
-      ready_at[s2] = std::max(ready_at[s2], published);
+      if (published > ready_at[s2]) ready_2nd[s2] = ready_at[s2], ready_at[s2] = published;
+      else ready_2nd[s2] = std::max(ready_2nd[s2], published);
       if (--missing[s2] == 0) {
         if (est_first) cand.push_back(s2);
         else ready.push({rank[s2], -s2});

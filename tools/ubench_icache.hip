@@ -122,6 +122,76 @@ __device__ __noinline__ bool diag16(f64x4 a, double (*Wk)[17], int lane) {
   return bad;
 }
 
+// the same with shader-clock stamps per step phase (ps[5 b + 0..4])
+__device__ __noinline__ bool diag16s(f64x4 a, double (*Wk)[17], int lane, long long *ps) {
+  __shared__ double xd[4][16], xw[4][16];
+  const int lr = lane & 15, lk = lane >> 4;
+  f64x4 M;
+#pragma unroll
+  for (int r = 0; r < 4; r++) M[r] = (lk + 4 * r == lr) ? 1.0 : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const int c0 = 4 * b;
+    if (lr >= c0 && lr < c0 + 4) xd[b][4 * lk + lr - c0] = a[b];
+    wave_lds_fence();
+    ps[5 * b + 0] = clock64();
+    double D[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) D[i][j] = xd[b][4 * i + j];
+    double L[4][4], Wd[4][4], iv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      double d = D[j][j];
+      bad |= !(d > 0.0);
+      d = d > 0.0 ? d : 1.0;
+      iv[j] = rsqrt_nr(d);
+#pragma unroll
+      for (int i = j + 1; i < 4; i++) L[i][j] = D[i][j] * iv[j];
+#pragma unroll
+      for (int i = j + 1; i < 4; i++)
+#pragma unroll
+        for (int k = j + 1; k <= i; k++) D[i][k] -= L[i][j] * L[k][j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      Wd[i][i] = iv[i];
+#pragma unroll
+      for (int j = 0; j < i; j++) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = j; k < i; k++) s += L[i][k] * Wd[k][j];
+        Wd[i][j] = -s * iv[i];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    ps[5 * b + 1] = clock64() + (long long)(Wd[3][0] != 0.0 ? 0 : 1);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) xw[b][4 * i + k] = k <= i ? Wd[i][k] : 0.0;
+    }
+    wave_lds_fence();
+    const double wpad = lr < 4 ? xw[b][4 * lr + lk] : 0.0;
+    const double a1 = (lr >= c0 && lr < c0 + 4) ? xw[b][4 * (lr - c0) + lk] - (lr - c0 == lk ? 1.0 : 0.0) : 0.0;
+    ps[5 * b + 2] = clock64() + (long long)(wpad + a1 != 0.0 ? 0 : 1);
+    double p = __builtin_amdgcn_mfma_f64_16x16x4f64(wpad, a[b], f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0)[0];
+    ps[5 * b + 3] = clock64() + (long long)(p != 0.0 ? 0 : 1);
+    p = (lr >= c0) ? p : 0.0;
+    a = __builtin_amdgcn_mfma_f64_16x16x4f64(-p, p, a, 0, 0, 0);
+    const f64x4 Y = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, M[b], M, 0, 0, 0);
+    const double a2 = (lr >= c0 + 4) ? -p : 0.0;
+    M = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, Y[b], Y, 0, 0, 0);
+    ps[5 * b + 4] = clock64() + (long long)(a[b < 3 ? b + 1 : 3] != 0.0 ? 0 : 1);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) Wk[lk + 4 * r][lr] = M[r];
+  return bad;
+}
+
 __global__ void k_diag(double *out, long long *t) {
   __shared__ double Wk[16][17];
   const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
@@ -136,6 +206,11 @@ __global__ void k_diag(double *out, long long *t) {
     if (lane == 0) t[c] = c1 - c0;
     a[0] += bad ? 1.0 : Wk[lr][lk] * 1e-12;
   }
+  long long ps[20];
+  const long long s0 = clock64();
+  (void)diag16s(a, Wk, lane, ps);
+  if (lane == 0)
+    for (int i = 0; i < 20; i++) t[4 + i] = ps[i] - s0;
   out[lane] = a[0] + a[1] + a[2] + a[3];
 }
 
@@ -172,7 +247,7 @@ int main() {
   double *out;
   long long *t, h[4];
   CK(hipMalloc(&out, 64 * 8));
-  CK(hipMalloc(&t, 32));
+  CK(hipMalloc(&t, 24 * 8));
   {
     double *err, he[3];
     CK(hipMalloc(&err, 24));
@@ -197,8 +272,12 @@ int main() {
     printf("dependent v_rsq_f64 + add: %.1f cycles\n", h[0] / 256.0);
     k_diag<<<1, 64>>>(out, t);
     CK(hipDeviceSynchronize());
-    CK(hipMemcpy(h, t, 32, hipMemcpyDeviceToHost));
-    printf("16x16 diagonal factor: calls 1..4: %lld %lld %lld %lld cycles\n", h[0], h[1], h[2], h[3]);
+    long long hh[24];
+    CK(hipMemcpy(hh, t, 24 * 8, hipMemcpyDeviceToHost));
+    printf("16x16 diagonal factor: calls 1..4: %lld %lld %lld %lld cycles\n", hh[0], hh[1], hh[2], hh[3]);
+    printf("  stamped call, per step: D in / chol+inv done / W_D in / panel MFMA done / step end (cycles from entry)\n");
+    for (int b = 0; b < 4; b++)
+      printf("    step %d: %6lld %6lld %6lld %6lld %6lld\n", b, hh[4 + 5 * b], hh[5 + 5 * b], hh[6 + 5 * b], hh[7 + 5 * b], hh[8 + 5 * b]);
   }
   return 0;
 }

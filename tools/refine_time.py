@@ -1,5 +1,6 @@
 """refine_matches / iter_proj timing on bench.py's 512x512 matching pair
-(GPU box): python tools/refine_time.py  (M3S_REFINE_STAGED=0: global kernel)."""
+(GPU box): python tools/refine_time.py (round 4 timed its kernel variants
+with it: profiles/r04/refine_variants.txt, the label is the variant)."""
 import os
 import sys
 
@@ -11,4 +12,4 @@ import bench  # noqa: E402
 import mast3r_slam_backends as be  # noqa: E402
 from mast3r_slam_amd import synthetic  # noqa: E402
 
-print(os.environ.get("M3S_REFINE_STAGED", "1"), bench.matching_leg(be, synthetic, torch.device("cuda:0"), 512, 512))
+print(bench.matching_leg(be, synthetic, torch.device("cuda:0"), 512, 512))

@@ -9,6 +9,7 @@
 #include <cstdio>
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __global__ void k_mfma_dep(double *out, long long *t, int n) {
   const int lane = threadIdx.x;
@@ -106,6 +107,24 @@ __global__ void k_load_l2(double *buf, double *out, long long *t, int n) {
   if (lane == 0) t[0] = c1 - c0, t[1] = w1 - w0;
 }
 
+// store throughput of one wave: n x 16-B stores per lane (1 KB per wave
+// instruction) to distinct lines, then a full drain; AUX = cache policy
+// (0 plain, 1 sc0, 2 sc1, 3 sc0 sc1); mode 1 times the issue only (no drain)
+template <int AUX>
+__global__ void k_store_bw(double *buf, long long *t, int n, int drain) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(buf, 0, 1 << 24, 0x00020000);
+  __syncthreads();
+  const long long c0 = clock64();
+  for (int i = 0; i < n; i++) {
+    const u32x4 w = {(unsigned)i, (unsigned)lane, (unsigned)wv, 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(w, R, ((wv * n + i) * 64 + lane) * 16, 0, AUX);
+  }
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const long long c1 = clock64();
+  if (threadIdx.x == 0) t[0] = c1 - c0;
+}
+
 #define CK(x)                                                  \
   do {                                                         \
     hipError_t e = (x);                                        \
@@ -131,6 +150,26 @@ int main() {
            h[1] * 10.0 / (n * per), (double)h[0] / (h[1] * 10.0));
     return 0;
   };
+  {
+    double *sb;
+    CK(hipMalloc(&sb, 1 << 24));
+    for (int waves = 1; waves <= 4; waves *= 4)
+      for (int drain = 0; drain < 2; drain++) {
+        k_store_bw<0><<<1, 64 * waves>>>(sb, t, 64, drain);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h, t, 8, hipMemcpyDeviceToHost));
+        const long long plain = h[0];
+        k_store_bw<2><<<1, 64 * waves>>>(sb, t, 64, drain);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h, t, 8, hipMemcpyDeviceToHost));
+        const long long wt = h[0];
+        k_store_bw<3><<<1, 64 * waves>>>(sb, t, 64, drain);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h, t, 8, hipMemcpyDeviceToHost));
+        printf("64 x 16-B stores per lane, %d wave(s) on one CU, %s: plain %.1f, sc1 %.1f, sc0 sc1 %.1f cycles per wave instruction\n",
+               waves, drain ? "drained" : "issue only", plain / 64.0, wt / 64.0, h[0] / 64.0);
+      }
+  }
   for (int pass = 0; pass < 2; pass++) {
     k_mfma_dep<<<1, 64>>>(out, t, n);
     rep("mfma f64 16x16x4, dependent (C)", 1);

@@ -367,9 +367,10 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
         first = [ms for k, ms in spans if k == 0]
         lin = [ms for k, ms in spans if k == 1]
         slv = [ms for k, ms in spans if k == 2]
-        timing = ("HIP events on the call's stream around each linearize launch inside the drop-in call "
-                  "(m3s_debug_call_timing: its own launch pattern, 5 calls x %d packed launches); "
-                  "back_to_back_ms = the same kernel launched back to back" % (args.iters - 1))
+        timing = ("each packed launch's own span inside the drop-in call (m3s_debug_call_timing: first "
+                  "block start to last block end on the device wall clock, stamped by the kernel; the call's "
+                  "own launch pattern, 5 calls x %d packed launches); back_to_back_ms = the same kernel "
+                  "launched back to back (HIP events around the run)" % (args.iters - 1))
     else:
         for rep in range(4):
             Twc.copy_(T_init)

@@ -1,0 +1,9 @@
+set -o pipefail
+OUT=gpurun_out; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_backend.py tests/test_gpu_matching.py -x -q --timeout 300 --timeout-method thread > $OUT/r4l_tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $OUT/r4l_tests.log | head; tail -20 $OUT/r4l_tests.log; exit 1; }
+tail -1 $OUT/r4l_tests.log
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/r4l_prof -o run -- python3 bench.py --no-cpu > $OUT/r4l_prof_bench.json 2> $OUT/r4l_prof_bench.err || { echo "prof failed"; tail -5 $OUT/r4l_prof_bench.err; exit 1; }
+python3 tools/prof_split.py $(find $OUT/r4l_prof -name "*kernel_trace.csv" | head -1) $OUT/r4l_prof_bench.json | tee $OUT/r4l_prof_split.txt
+timeout -k 10 400 python bench.py --no-cpu > $OUT/r4l_bench.json 2> $OUT/r4l_bench.err || { echo "bench failed"; tail -5 $OUT/r4l_bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/r4l_bench.json')); r=d['roofline']; print('ms/step', d['ms_per_step'], 'pk', r['avg_launch_ms'], r['in_call_ms_min_max'], 'b2b', r['back_to_back_ms'], 'frac', r['frac'], 'gather', r['gather_kernel']['avg_launch_ms'], 'solve', r['solve']['avg_ms'])"

@@ -27,6 +27,7 @@
 //
 // The tracker entry points reuse linearize_kernel (no gather, frame-local
 // Jacobian) plus a one-block 7x7 solve/convergence kernel.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -241,19 +242,7 @@ struct LinArgs {
   int64_t HW, edge_begin, chunks, chunk_pix;
   ResidualParams P;
   const float *Kd;  // calib backend: the caller's 3x3 K (device), read by the kernels (P.fx.. unset)
-  unsigned long long *tspan = nullptr;  // in-call timing: {first block's start, last block's end} (wall clock)
 };
-
-// In-call kernel span (m3s_debug_call_timing): the launch's first block start
-// and last block end on the 100 MHz wall clock, by thread 0 of every block:
-// the kernel's own execution span, as a kernel trace records it (timing
-// events around the launch read ~8% more, profiles/r04/prof_split_incall_b2b.txt)
-__device__ __forceinline__ void span_start(const LinArgs &A) {
-  if (A.tspan && threadIdx.x == 0) atomicMin(A.tspan, (unsigned long long)wall_clock64());
-}
-__device__ __forceinline__ void span_end(const LinArgs &A) {
-  if (A.tspan && threadIdx.x == 0) atomicMax(A.tspan + 1, (unsigned long long)wall_clock64());
-}
 
 // The residual parameters of a launch: the intrinsics of a calib backend
 // launch come from the caller's K on the device (uniform loads), so the first
@@ -703,7 +692,6 @@ __device__ __forceinline__ void lds_xj6(const float *xs, int h, float (&xf)[6]) 
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_PK_WAVES)
     linearize_packed_kernel(LinArgs A) {
-  span_start(A);
   if (*A.stop) return;
   const int64_t b = block_task(A);
   if (b < 0) return;
@@ -892,7 +880,6 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   sums[0] += sink;
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
-  span_end(A);
 }
 
 // ------------------------------------------ pipelined gathering launch --
@@ -940,7 +927,6 @@ __device__ __forceinline__ void gslot_read(uint32_t a, uint32_t av, bool i64, GS
 
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
-  span_start(A);
   if (*A.stop) return;
   const int64_t b = block_task(A);
   if (b < 0) return;
@@ -1088,7 +1074,6 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
   acc.fold(sums);
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
-  span_end(A);
 }
 
 // fp64 sum of each edge's chunk partials (fixed order)
@@ -4686,6 +4671,22 @@ bool gather_lds_path();  // (knobs, below)
 
 // pack: 0 gathering kernel, 1 gathering kernel that stores the planes,
 // 2 packed kernel (reads the planes; VEC layout only)
+// In-call timing (m3s_debug_call_timing): the drop-in call sets a start /
+// stop event pair for its next linearize launch, which then goes through
+// hipExtLaunchKernel: the events take the dispatch's own begin / end
+// timestamps (the kernel's span, as a kernel trace records it; events
+// recorded around the launch read 8-12% more, profiles/r04/prof_split_*.txt)
+hipEvent_t *g_lin_ext_ev = nullptr;  // {start, stop}; guarded by the CallTiming lock
+template <typename K>
+void launch_lin(K kernel, dim3 g, dim3 b, hipStream_t st, const LinArgs &L) {
+  if (g_lin_ext_ev) {
+    hipExtLaunchKernelGGL(kernel, g, b, 0, st, g_lin_ext_ev[0], g_lin_ext_ev[1], 0, L);
+    g_lin_ext_ev = nullptr;
+  } else {
+    kernel<<<g, b, 0, st>>>(L);
+  }
+}
+
 template <int MODE, bool TRACK>
 int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipStream_t st) {
   if (blocks <= 0) return M3S_OK;
@@ -4697,13 +4698,13 @@ int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipSt
       linearize_kernel<MODE, TRACK, false, false><<<g, b, 0, st>>>(L);
   } else if (pack == 1) {
     if (vec && M3S_GATHER_LDS && gather_lds_path())
-      linearize_gather_kernel<MODE><<<g, b, 0, st>>>(L);
+      launch_lin(linearize_gather_kernel<MODE>, g, b, st, L);
     else if (vec)
-      linearize_kernel<MODE, false, true, true><<<g, b, 0, st>>>(L);
+      launch_lin(linearize_kernel<MODE, false, true, true>, g, b, st, L);
     else
-      linearize_kernel<MODE, false, false, true><<<g, b, 0, st>>>(L);
+      launch_lin(linearize_kernel<MODE, false, false, true>, g, b, st, L);
   } else {
-    linearize_packed_kernel<MODE><<<g, b, 0, st>>>(L);
+    launch_lin(linearize_packed_kernel<MODE>, g, b, st, L);
   }
   return launch_ok();
 }
@@ -4974,14 +4975,12 @@ void build_eorder(const std::vector<int32_t> &rj, int64_t eb, int64_t E_loc, std
 int host_finish(const m3s_gn_args *a, hipStream_t st);
 
 int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb, int64_t ee,
-                      double *edge_sums, hipStream_t st, bool fuse_fin = false, int64_t *chunks_used = nullptr,
-                      unsigned long long *tspan = nullptr) {
+                      double *edge_sums, hipStream_t st, bool fuse_fin = false, int64_t *chunks_used = nullptr) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
   void *ws = a->workspace;
   const int64_t E_loc = ee - eb;
   if (E_loc <= 0) return M3S_OK;
   LinArgs L;
-  L.tspan = tspan;
   L.Twc = a->Twc;
   L.T_rel = nullptr;
   L.Xs = a->Xs;
@@ -5863,16 +5862,14 @@ int gn_prepare_async(const m3s_gn_args *a, hipStream_t st) {
 // so the packed kernel is timed in the call's own launch pattern (behind the
 // previous iteration's solve), not back to back. Kinds: 0 first-iteration
 // (gathering) linearize, 1 packed linearize, 2 solve (every launch of it).
-constexpr int kSpanSlots = 1024;
-__device__ unsigned long long g_kspan[kSpanSlots][2];  // per timed linearize launch: {min start, max end}
 struct CallTiming {
   std::mutex mu;
   bool on = false;
   std::vector<hipEvent_t> ev;  // pool, reused
   std::vector<int> kind;       // kind of the span from event q to q + 1 (-1: none)
   size_t used = 0;
-  int nspan = 0;               // linearize launches given a g_kspan slot
-  unsigned long long *spans = nullptr;  // device address of g_kspan
+  std::vector<hipEvent_t> kev;  // pool: {start, stop} of each timed linearize dispatch
+  size_t kused = 0;
 };
 CallTiming &call_timing() {
   static CallTiming t;
@@ -5917,8 +5914,18 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
   for (int it = 0; it < a->max_iter; it++) {
     int64_t chunks = 0;  // of this iteration's linearize launch (the dense path reduces its partials)
     if (timing && !call_mark(st, it == 0 ? 0 : 1)) return M3S_ELAUNCH;
-    unsigned long long *ts = timing && CT.spans && CT.nspan < kSpanSlots ? CT.spans + 2 * CT.nspan++ : nullptr;
-    if ((rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse, &chunks, ts))) return rc;
+    if (timing) {  // the linearize dispatch's own begin / end (launch_lin)
+      while (CT.kev.size() < CT.kused + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return M3S_ELAUNCH;
+        CT.kev.push_back(e);
+      }
+      g_lin_ext_ev = &CT.kev[CT.kused];
+      CT.kused += 2;
+    }
+    rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse, &chunks);
+    g_lin_ext_ev = nullptr;
+    if (rc) return rc;
     if (timing && !call_mark(st, 2)) return M3S_ELAUNCH;
     if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st, sparse))) return rc;
     if (timing && !call_mark(st, -1)) return M3S_ELAUNCH;
@@ -6592,15 +6599,7 @@ int m3s_debug_call_timing(int enable) {
   std::lock_guard<std::mutex> g(T.mu);
   T.on = enable != 0;
   T.used = 0;
-  T.nspan = 0;
-  if (T.on) {  // the span slots: {~0, 0} (min / max identities), set before the timed calls
-    if (!T.spans && hipGetSymbolAddress(reinterpret_cast<void **>(&T.spans), HIP_SYMBOL(g_kspan)) != hipSuccess)
-      return M3S_ELAUNCH;
-    std::vector<unsigned long long> init(2 * kSpanSlots);
-    for (int i = 0; i < kSpanSlots; i++) init[2 * i] = ~0ull, init[2 * i + 1] = 0ull;
-    if (hipMemcpy(T.spans, init.data(), init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice) != hipSuccess)
-      return M3S_ELAUNCH;
-  }
+  T.kused = 0;
   return M3S_OK;
 }
 
@@ -6609,29 +6608,25 @@ int m3s_debug_call_times(float *ms, int32_t *kinds, int cap) {
   std::lock_guard<std::mutex> g(T.mu);
   if (T.used == 0) return 0;
   if (hipEventSynchronize(T.ev[T.used - 1]) != hipSuccess) return M3S_ELAUNCH;
-  // linearize spans (kinds 0, 1): the kernel's own span from its block stamps
-  // (wall clock, 10 ns); solve spans (kind 2): the timing events around its
-  // launches
-  std::vector<unsigned long long> sp(2 * (size_t)T.nspan);
-  if (T.nspan && hipMemcpy(sp.data(), T.spans, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-    return M3S_ELAUNCH;
-  int n = 0, li = 0;
+  // linearize spans (kinds 0, 1): the dispatch's own begin / end events
+  // (hipExtLaunchKernel); solve spans (kind 2): the events around its launches
+  int n = 0;
+  size_t li = 0;
   for (size_t q = 0; q + 1 < T.used; q++) {
     if (T.kind[q] < 0) continue;
     if (n < cap) {
       float t = 0.0f;
-      if (T.kind[q] <= 1 && li < T.nspan && sp[2 * li + 1] >= sp[2 * li]) {
-        t = (float)((sp[2 * li + 1] - sp[2 * li]) * 1e-5);  // 100 MHz ticks -> ms
-      } else if (hipEventElapsedTime(&t, T.ev[q], T.ev[q + 1]) != hipSuccess) {
+      const bool lin = T.kind[q] <= 1 && li + 1 < T.kused;
+      if (hipEventElapsedTime(&t, lin ? T.kev[li] : T.ev[q], lin ? T.kev[li + 1] : T.ev[q + 1]) != hipSuccess)
         return M3S_ELAUNCH;
-      }
       ms[n] = t;
       kinds[n] = T.kind[q];
     }
-    if (T.kind[q] <= 1) li++;
+    if (T.kind[q] <= 1) li += 2;
     n++;
   }
   T.used = 0;
+  T.kused = 0;
   return n;
 }
 

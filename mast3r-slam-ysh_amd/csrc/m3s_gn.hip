@@ -4020,6 +4020,9 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
 // columns. Per tile the same updates in the same order as tail_cyc_kernel
 // (columns k ascending, then the pair's own first column): bitwise the same
 // factor; the back-substitution is the same code (tail_backsub_wg).
+// RC: row tiles per wave (waves 1..3 hold rows J1 + w + 3 u, u < RC): 7 up to
+// 23 tile rows (the register arrays of 11 spill), 11 up to kTailMaxT
+template <int RC>
 __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, TailSync S) {
   if (A.flags[kFlagStop]) return;
   __shared__ double Wk[2][16][17];
@@ -4036,7 +4039,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
   const int want = S.epoch + 1;
   double *Wg = A.Wg;
   const __amdgpu_buffer_rsrc_t R = gran_rsrc(S.LgG);
-  constexpr int kRC = (kTailMaxT + 2) / 3;
+  constexpr int kRC = RC;
   auto rowI = [&](int u) { return wave == 0 ? (u < jn ? J0 + u : -1) : Jl + wave + 3 * u; };
   auto live = [&](int u) {
     const int I = rowI(u);
@@ -4206,65 +4209,120 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     }
     if (jn == 2) store_lgt(J1, J0, acc0[1], 0);
   } else {
-    // row by row (the first row of waves 1 and 2 carries the next pair's
-    // chain: its two tiles go out before any other row's work): the deferred
-    // update from column J0 - 1 as the row's tile lands, the panel tile
-    // L(I, J0), the update of (I, J1) from the pair's first column
-    // (L(J1, J0) from wave 0), the panel tile L(I, J1); each tile handed off
-    // at once. (Per tile the same updates in the same order.)
-    bool have_w0 = false, have_l = false, have_w1 = false;
-    f64x4 ls = {0.0, 0.0, 0.0, 0.0};
+    // The wave's first row first, on its own (in waves 1 and 2 it carries
+    // the next pair's chain: its two tiles go out before any other work):
+    // the deferred update from column J0 - 1 as its tile lands, the panel
+    // tile L(I, J0), the update of (I, J1) from the pair's first column
+    // (L(J1, J0) from wave 0), the panel tile L(I, J1), each handed off at
+    // once. Then the other rows phase by phase, every row's MFMA chain of a
+    // phase interleaved with the others' (one row at a time left each
+    // row's ~12 dependent MFMAs and stores exposed: ~1.5 us per row,
+    // profiles/r04/tail_stamps_pair_rows_fine.txt). Per tile the same
+    // updates in the same order.
     if (lane == 0) M3S_CSTAMP(2, 1000 + 16 * J0 + 15, wave);
+    auto deferred = [&](int u) {
+      GranTile g;
+      poll_tile(tail_tile(rowI(u), J0 - 1), g);
+      const f64x4 ri = gran_val(g);
+      mma(acc0[u], rk0_last, ri);
+      if (jn == 2) mma(acc1[u], rk1_last, ri);
+    };
+    auto put_y = [&](int I, int J, const f64x4 &d) {  // y' of column J from the RHS row
+      if (I == In && lr == rn) {
 #pragma unroll
-    for (int u = 0; u < kRC; u++) {
-      const int I = rowI(u);
-      if (live(u)) {
-        if (J0 > 0) {
-          GranTile g;
-          poll_tile(tail_tile(I, J0 - 1), g);
-          const f64x4 ri = gran_val(g);
-          mma(acc0[u], rk0_last, ri);
-          if (jn == 2) mma(acc1[u], rk1_last, ri);
-        }
-        if (tid == 64 && u < 8) M3S_CSTAMP(2, 1300 + 16 * J0 + u, 0);
-        if (!have_w0) {
-          if (tid == 64) M3S_CSTAMP(2, 800 + J0, 0);
-          wait_lds(&wready[0]);
-          have_w0 = true;
-          if (tid == 64) M3S_CSTAMP(2, 800 + J0, 1);
-        }
-        const f64x4 d0 = panel(acc0[u], 0);
-        gran_store(R, tail_tile(I, J0), lane, d0, want);
-        if (tid == 64 && u < 8) M3S_CSTAMP(2, 1300 + 16 * J0 + u, 1);
-        if (I == In && lr == rn) {
-#pragma unroll
-          for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J0 + lk + 4 * r, d0[r]);
-        }
-        if (jn == 2) {
-          if (!have_l) {
-            if (tid == 64) M3S_CSTAMP(2, 800 + J0, 2);
-            wait_lds(&lready);
-            ls = Lsub[lane];
-            have_l = true;
-          }
-          mma(acc1[u], ls, d0);
-          if (!have_w1) {
-            if (tid == 64) M3S_CSTAMP(2, 800 + J0, 3);
-            wait_lds(&wready[1]);
-            have_w1 = true;
-            if (tid == 64) M3S_CSTAMP(2, 900 + J0, 0);
-          }
-          const f64x4 d = panel(acc1[u], 1);
-          gran_store(R, tail_tile(I, J1), lane, d, want);
-          if (tid == 64 && u < 8) M3S_CSTAMP(2, 1300 + 16 * J0 + u, 3);
-          if (I == J1 + 1 && tid == 64) M3S_CSTAMP(2, J1, 0);
-          if (I == In && lr == rn) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J1 + lk + 4 * r, d[r]);
-          }
-        }
-        if (lane == 0 && u < 15) M3S_CSTAMP(2, 1000 + 16 * J0 + u, wave);
+        for (int r = 0; r < 4; r++) st_sc1(S.ypg + 16 * J + lk + 4 * r, d[r]);
       }
+    };
+    f64x4 ls = {0.0, 0.0, 0.0, 0.0};
+    if (live(0)) {
+      const int I = rowI(0);
+      if (J0 > 0) deferred(0);
+      if (tid == 64) M3S_CSTAMP(2, 1300 + 16 * J0, 0);
+      wait_lds(&wready[0]);
+      const f64x4 d0 = panel(acc0[0], 0);
+      gran_store(R, tail_tile(I, J0), lane, d0, want);
+      if (tid == 64) M3S_CSTAMP(2, 1300 + 16 * J0, 1);
+      put_y(I, J0, d0);
+      if (jn == 2) {
+        wait_lds(&lready);
+        ls = Lsub[lane];
+        mma(acc1[0], ls, d0);
+        wait_lds(&wready[1]);
+        const f64x4 d = panel(acc1[0], 1);
+        gran_store(R, tail_tile(I, J1), lane, d, want);
+        if (tid == 64) M3S_CSTAMP(2, 1300 + 16 * J0, 3);
+        if (I == J1 + 1 && tid == 64) M3S_CSTAMP(2, J1, 0);
+        put_y(I, J1, d);
+      }
+      if (lane == 0) M3S_CSTAMP(2, 1000 + 16 * J0, wave);
+    }
+    if (live(1)) {  // (rows are dealt in order: live(1) implies live(0))
+      // the deferred update: every remaining row's tile in flight at once,
+      // applied as they land
+      if (J0 > 0) {
+        unsigned pend = 0;
+#pragma unroll
+        for (int u = 1; u < kRC; u++)
+          if (live(u)) pend |= 1u << u;
+        int spins = 0;
+        while (pend) {
+          GranTile g[kRC];
+#pragma unroll
+          for (int u = 1; u < kRC; u++)
+            if (pend & (1u << u)) gran_load(R, tail_tile(rowI(u), J0 - 1), lane, g[u]);
+#pragma unroll
+          for (int u = 1; u < kRC; u++) {
+            if ((pend & (1u << u)) && gran_ready(g[u], want)) {
+              const f64x4 ri = gran_val(g[u]);
+              mma(acc0[u], rk0_last, ri);
+              if (jn == 2) mma(acc1[u], rk1_last, ri);
+              pend &= ~(1u << u);
+            }
+          }
+          if (pend) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kColSpins) {
+              if (lane == 0) fail_s = 1;
+              break;
+            }
+          }
+        }
+      }
+      if (tid == 64) M3S_CSTAMP(2, 1300 + 16 * J0 + 1, 0);
+      // (a wave whose row 0 is dead has no rows at all, so the flags below
+      // were already seen by row 0)
+      f64x4 d0[kRC];
+#pragma unroll
+      for (int u = 1; u < kRC; u++) {
+        d0[u] = f64x4{0.0, 0.0, 0.0, 0.0};
+        if (live(u)) d0[u] = panel(acc0[u], 0);
+      }
+#pragma unroll
+      for (int u = 1; u < kRC; u++)
+        if (live(u)) {
+          gran_store(R, tail_tile(rowI(u), J0), lane, d0[u], want);
+          put_y(rowI(u), J0, d0[u]);
+        }
+      if (tid == 64) M3S_CSTAMP(2, 1300 + 16 * J0 + 1, 1);
+      if (jn == 2) {
+#pragma unroll
+        for (int u = 1; u < kRC; u++)
+          if (live(u)) mma(acc1[u], ls, d0[u]);
+        f64x4 d1[kRC];
+#pragma unroll
+        for (int u = 1; u < kRC; u++) {
+          d1[u] = f64x4{0.0, 0.0, 0.0, 0.0};
+          if (live(u)) d1[u] = panel(acc1[u], 1);
+        }
+#pragma unroll
+        for (int u = 1; u < kRC; u++)
+          if (live(u)) {
+            gran_store(R, tail_tile(rowI(u), J1), lane, d1[u], want);
+            put_y(rowI(u), J1, d1[u]);
+          }
+        if (tid == 64) M3S_CSTAMP(2, 1300 + 16 * J0 + 1, 3);
+      }
+      if (lane == 0) M3S_CSTAMP(2, 1000 + 16 * J0 + 1, wave);
     }
     // the L tiles for the back-substitution, after every hand-off
 #pragma unroll
@@ -5251,7 +5309,10 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.warm = tail_warm_knob() ? 1 : 0;
           const int TC = (7 * meta.nc + 15) / 16;
           if (tail_pair_path())
-            tail_pair_kernel<<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
+            if (((7 * meta.nc + 16) / 16 + 2) / 3 <= 7)  // tile rows TR: rows per wave of waves 1..3
+              tail_pair_kernel<7><<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
+            else
+              tail_pair_kernel<(kTailMaxT + 2) / 3><<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
           else
             tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
         } else {

@@ -3622,8 +3622,8 @@ struct TailSync {
   int32_t *tflag;    // [TC] epoch flags: tile column published (W_J, y'_J, the LgT tiles: back-substitution)
   int epoch;
   double *ypg;     // y' of every tile column [16 TC]
-  double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout (back-substitution A operands)
-  double *LgG;     // the L tiles as tagged granules, [tile][64][4] x {double, epoch tag, 0} (16 B; zeroed per call)
+  double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout, [tile][2][64 lanes][2] (back-substitution A operands)
+  double *LgG;     // the L tiles as tagged granules, [tile][4][64 lanes] x {double, epoch tag, 0} (16 B; zeroed per call)
   int warm;        // 1: warm the diagonal factor's code on a dummy tile first (tail_diag_warm)
 };
 constexpr size_t kTailGranBytes = (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 64 * 4 * 16;
@@ -3651,7 +3651,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(double *p) {
 }
 __device__ __forceinline__ void gran_load(__amdgpu_buffer_rsrc_t R, int tile, int lane, GranTile &g) {
 #pragma unroll
-  for (int r = 0; r < 4; r++) g.v[r] = __builtin_amdgcn_raw_buffer_load_b128(R, ((tile * 64 + lane) * 4 + r) * 16, 0, 16);
+  for (int r = 0; r < 4; r++) g.v[r] = __builtin_amdgcn_raw_buffer_load_b128(R, ((tile * 4 + r) * 64 + lane) * 16, 0, 16);
 }
 __device__ __forceinline__ bool gran_ready(const GranTile &g, int want) {  // wave-uniform
   const bool ok = g.v[0].z == (unsigned)want && g.v[1].z == (unsigned)want && g.v[2].z == (unsigned)want &&
@@ -3664,12 +3664,16 @@ __device__ __forceinline__ f64x4 gran_val(const GranTile &g) {
   for (int r = 0; r < 4; r++) d[r] = __longlong_as_double((long long)(((unsigned long long)g.v[r].y << 32) | g.v[r].x));
   return d;
 }
+// Granule r of every lane of a tile is one 1-KB run ([tile][4][64 lanes]):
+// each 16-B store / load instruction of the wave covers whole lines (round 4;
+// lane-major [tile][64][4] made every instruction a 25 %-dense 4-KB stride of
+// partial-line write-through stores)
 __device__ __forceinline__ void gran_store(__amdgpu_buffer_rsrc_t R, int tile, int lane, f64x4 d, int want) {
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(d[r]);
     const u32x4 w = {(unsigned)(b & 0xffffffffu), (unsigned)(b >> 32), (unsigned)want, 0u};
-    __builtin_amdgcn_raw_buffer_store_b128(w, R, ((tile * 64 + lane) * 4 + r) * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(w, R, ((tile * 4 + r) * 64 + lane) * 16, 0, 16);
   }
 }
 
@@ -3759,10 +3763,13 @@ __device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSyn
 #pragma unroll
     for (int t = 0; t < kTW; t++) {
       const int Jc = wave + kTailNW * t;
-      const int off = (K >= 0 && Jc < K) ? (tail_tile(K, Jc) * 256 + 4 * lane) * 8 : kFar;
+      // tile layout [tile][2 halves][64 lanes][2 doubles] (every 16-B access of
+      // the wave covers whole lines)
+      const bool in = K >= 0 && Jc < K;
+      const int off = in ? (tail_tile(K, Jc) * 256 + 2 * lane) * 8 : kFar;
       double x0, x1, x2, x3;
       ld2(off, x0, x1);
-      ld2(off + 16, x2, x3);
+      ld2(in ? off + 1024 : kFar, x2, x3);
       lt[slot][t] = f64x4{x0, x1, x2, x3};
     }
   };
@@ -3934,11 +3941,14 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // Wk (and y') before the flag
     if (lane == 0) __hip_atomic_store(&wready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (tid == 0) M3S_CSTAMP(2, J, 2);
-    if (lane < 16) {
+    // W^T ([16][16] row-major, element e = 16 l + r holds W[r][l]): four
+    // stores of 64 consecutive elements, whole lines each
 #pragma unroll
-      for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)J * 256 + lane * 16 + r, Wk[r][lane]);  // W^T
-      if (In == J) st_sc1(S.ypg + 16 * J + lane, yv[16 * J + lane]);
+    for (int i = 0; i < 4; i++) {
+      const int e = 64 * i + lane;
+      st_sc1(Wg + (size_t)J * 256 + e, Wk[e & 15][e >> 4]);
     }
+    if (In == J && lane < 16) st_sc1(S.ypg + 16 * J + lane, yv[16 * J + lane]);
   } else {
     // row by row, the sub-diagonal tile first: the update from column J - 1
     // (as its tile lands), then the panel tile L(I, J)^T = W_J A(I, J)^T,
@@ -3992,9 +4002,9 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
                                  b2 = __double_as_longlong(dt[2]), b3 = __double_as_longlong(dt[3]);
         const u32x4 w0 = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
         const u32x4 w1 = {(unsigned)b2, (unsigned)(b2 >> 32), (unsigned)b3, (unsigned)(b3 >> 32)};
-        const int off = (tail_tile(I, J) * 256 + 4 * lane) * 8;
+        const int off = (tail_tile(I, J) * 256 + 2 * lane) * 8;  // (halves of 1 KB: whole lines per store)
         __builtin_amdgcn_raw_buffer_store_b128(w0, RT, off, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(w1, RT, off + 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(w1, RT, off + 1024, 0, 16);
       }
     }
   }
@@ -4152,9 +4162,9 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
                              b2 = __double_as_longlong(dt[2]), b3 = __double_as_longlong(dt[3]);
     const u32x4 w0 = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
     const u32x4 w1 = {(unsigned)b2, (unsigned)(b2 >> 32), (unsigned)b3, (unsigned)(b3 >> 32)};
-    const int off = (tail_tile(I, J) * 256 + 4 * lane) * 8;
+    const int off = (tail_tile(I, J) * 256 + 2 * lane) * 8;  // (halves of 1 KB: whole lines per store)
     __builtin_amdgcn_raw_buffer_store_b128(w0, RT, off, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(w1, RT, off + 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(w1, RT, off + 1024, 0, 16);
   };
   auto panel = [&](const f64x4 &a, int slot) {  // L(I, J)^T = W_J A(I, J)^T, operand order
     f64x4 d = {0.0, 0.0, 0.0, 0.0};
@@ -4199,13 +4209,17 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
       if (lane == 0) __hip_atomic_store(&wready[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (tid == 0) M3S_CSTAMP(2, J1, 2);
     }
-    if (lane < 16) {
+    // W^T of each column ([16][16] row-major: element e = 16 l + r holds
+    // W[r][l]): four stores of 64 consecutive elements, whole lines each
+    // (lane l storing its row of 16 was 16 partial-line write-through stores)
 #pragma unroll
-      for (int j = 0; j < jn; j++) {
+    for (int j = 0; j < jn; j++) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) st_sc1(Wg + (size_t)(J0 + j) * 256 + lane * 16 + r, Wk[j][r][lane]);  // W^T
-        if (In == J0 + j) st_sc1(S.ypg + 16 * (J0 + j) + lane, yv[16 * (J0 + j) + lane]);
+      for (int i = 0; i < 4; i++) {
+        const int e = 64 * i + lane;
+        st_sc1(Wg + (size_t)(J0 + j) * 256 + e, Wk[j][e & 15][e >> 4]);
       }
+      if (In == J0 + j && lane < 16) st_sc1(S.ypg + 16 * (J0 + j) + lane, yv[16 * (J0 + j) + lane]);
     }
     if (jn == 2) store_lgt(J1, J0, acc0[1], 0);
   } else {

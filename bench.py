@@ -367,9 +367,10 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
         first = [ms for k, ms in spans if k == 0]
         lin = [ms for k, ms in spans if k == 1]
         slv = [ms for k, ms in spans if k == 2]
-        timing = ("each packed launch's own span inside the drop-in call (m3s_debug_call_timing: first "
-                  "block start to last block end on the device wall clock, stamped by the kernel; the call's "
-                  "own launch pattern, 5 calls x %d packed launches); back_to_back_ms = the same kernel "
+        timing = ("each packed launch's own dispatch span inside the drop-in call (m3s_debug_call_timing: "
+                  "begin / end events of the dispatch itself via hipExtLaunchKernel; the call's own launch "
+                  "pattern, 5 calls x %d packed launches; profiles/r04/prof_bench/prof_split.txt puts it "
+                  "within 1%% of the kernel trace of the same calls); back_to_back_ms = the same kernel "
                   "launched back to back (HIP events around the run)" % (args.iters - 1))
     else:
         for rep in range(4):

@@ -1938,33 +1938,6 @@ __device__ __forceinline__ bool diag_factor(double v, int k, double *Lb, double 
     }
     wave_lds_fence();
   }
-  if (SC1) {
-    // global factor (write-through): L_kk and W_k each gathered in the wave's
-    // scratch and stored by 49 lanes in one instruction (round 4: the 7-lane
-    // form was 14 store instructions of 8-B pieces, partial-line write-through
-    // stores that the publishing drain then waits for); W_k stays in scr[0..49)
-    // for the caller (df_factor_kernel's W granules)
-    if (lane < 7) {
-#pragma unroll
-      for (int qq = 0; qq < 7; qq++) scr[lane * 7 + qq] = (qq <= lane) ? a[qq] : 0.0;  // row `lane` of L_kk
-    }
-    wave_lds_fence();
-    const double lv = scr[lane < 49 ? lane : 0];
-    wave_lds_fence();
-    if (lane < 7) {
-#pragma unroll
-      for (int qq = 0; qq < 7; qq++) {
-        scr[qq * 7 + lane] = wcol[qq];  // column `lane` of W
-        if (Wl) Wl[qq * 7 + lane] = wcol[qq];
-      }
-    }
-    wave_lds_fence();
-    if (lane < 49) {
-      st_blk<SC1>(Lb + (size_t)k * 49 + lane, lv);
-      st_blk<SC1>(Di + (size_t)k * 49 + lane, scr[lane]);
-    }
-    return bad;
-  }
   if (lane < 7) {
 #pragma unroll
     for (int qq = 0; qq < 7; qq++) {
@@ -2753,23 +2726,17 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       if (lane == 0) M3S_CSTAMP(0, k, 2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (M3S_DF_WGRAN) {
+      if (M3S_DF_WGRAN && lane < 7) {
         // W_k as tagged granules (after the drain: an OFF item that sees a
-        // tag also sees y_k and L_kk): entry e = qq * 7 + c of Dinv[k], by 49
-        // lanes in one 784-B store (the 7-lane form was 7 partial-line ones)
-        if (lane < 7) {
+        // tag also sees y_k and L_kk): entry qq * 7 + lane of Dinv[k]
+        const __amdgpu_buffer_rsrc_t RG =
+            __builtin_amdgcn_make_buffer_rsrc(D.Wgr, 0, (int)(16 * 49 * (D.m + 1)), 0x00020000);
 #pragma unroll
-          for (int qq = 0; qq < 7; qq++) scr[qq * 7 + lane] = wcol[qq];
-        }
-        wave_lds_fence();
-        if (act49) {
-          const __amdgpu_buffer_rsrc_t RG =
-              __builtin_amdgcn_make_buffer_rsrc(D.Wgr, 0, (int)(16 * 49 * (D.m + 1)), 0x00020000);
-          const unsigned long long bw = (unsigned long long)__double_as_longlong(scr[lane]);
+        for (int qq = 0; qq < 7; qq++) {
+          const unsigned long long bw = (unsigned long long)__double_as_longlong(wcol[qq]);
           const u32x4 gw = {(unsigned)(bw & 0xffffffffu), (unsigned)(bw >> 32), (unsigned)want, 0u};
-          __builtin_amdgcn_raw_buffer_store_b128(gw, RG, (k * 49 + lane) * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(gw, RG, (k * 49 + qq * 7 + lane) * 16, 0, 16);
         }
-        wave_lds_fence();
       }
       if (lane == 0) M3S_CSTAMP(0, k, 3);
     } else if (code < D.n_tasks) {  // OFF(t)

@@ -894,9 +894,6 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 // flight), the pose-only math, the rest, the plane stores. Same arithmetic per
 // pixel as linearize_kernel<MODE, false, true, true> (gather_pixel +
 // make_pixin + pixel_contrib): bitwise the same planes, partials and sums.
-#ifndef M3S_TAIL_DIAG_RL  // the tail's 16x16 diagonal: each step's 4x4 block by readlanes (0: LDS broadcast)
-#define M3S_TAIL_DIAG_RL 0
-#endif
 #ifndef M3S_DIAG_RL
 #define M3S_DIAG_RL 1  // sparse_llt_kernel's 7x7 DIAG factor: column broadcast by readlanes (0: through LDS, A/B)
 #endif
@@ -3342,7 +3339,7 @@ template <bool FULL>  // FULL: jv == 16 (every tile column but possibly the last
 __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row,
                                                  int lane) {
   if (FULL) jv = 16;
-  __shared__ double xd[4][16];
+  __shared__ double xd[4][16], xw[4][16];
   const int lr = lane & 15, lk = lane >> 4;
   f64x4 M;  // W accumulator, identity
 #pragma unroll
@@ -3352,10 +3349,8 @@ __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], doub
   for (int b = 0; b < 4; b++) {
     const int c0 = 4 * b;
     // D_b[i][j] = A[c0 + i][c0 + j]: register b of the lanes with column lr in the block
-#if !M3S_TAIL_DIAG_RL
     if (lr >= c0 && lr < c0 + 4) xd[b][4 * lk + lr - c0] = a[b];
     wave_lds_fence();
-#endif
     bool real[4];
 #pragma unroll
     for (int m = 0; m < 4; m++) real[m] = FULL || c0 + m < jv;
@@ -3364,15 +3359,11 @@ __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], doub
     for (int i = 0; i < 4; i++)
 #pragma unroll
       for (int j = 0; j <= i; j++) {
-#if M3S_TAIL_DIAG_RL  // D_b[i][j] = register b of lane (c0 + j) + 16 i: constant-lane readlanes
-        const double v = readlane_d(a[b], c0 + j + 16 * i);
-#else
         const double v = xd[b][4 * i + j];
-#endif
         D[i][j] = (real[i] && real[j]) ? v : (i == j ? 1.0 : 0.0);
       }
     // 4x4 Cholesky and W_D = L_D^-1, on every lane
-    double L[4][4], iv[4];
+    double L[4][4], Wd[4][4], iv[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       double d = D[j][j];
@@ -3386,22 +3377,29 @@ __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], doub
 #pragma unroll
         for (int k = j + 1; k <= i; k++) D[i][k] -= L[i][j] * L[k][j];
     }
-    // column lk of W_D = L_D^-1 on each lane (round 4: every lane computes the
-    // column its A operands need, so no lane-0 LDS broadcast of W_D and no
-    // second round trip per step; the same products and order as the full
-    // inverse, the leading terms exact zeros): wc[i] = W_D[i][lk]
-    double wc[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      double s = 0.0;
+      Wd[i][i] = iv[i];
 #pragma unroll
-      for (int k = 0; k < i; k++) s += L[i][k] * wc[k];
-      wc[i] = (i == lk) ? iv[i] : (i < lk ? 0.0 : -s * iv[i]);
+      for (int j = 0; j < i; j++) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = j; k < i; k++) s += L[i][k] * Wd[k][j];
+        Wd[i][j] = -s * iv[i];
+      }
     }
-    // A operands: Wpad[lr][lk] = W_D[lr][lk] (lr < 4); A1[lr][lk] = (W_D - I)[lr - c0][lk] (lr in the block)
-    auto pick = [&](int i) { return i == 0 ? wc[0] : i == 1 ? wc[1] : i == 2 ? wc[2] : wc[3]; };
-    const double wpad = lr < 4 ? pick(lr) : 0.0;
-    const double a1 = (lr >= c0 && lr < c0 + 4) ? pick(lr - c0) - (lr - c0 == lk ? 1.0 : 0.0) : 0.0;
+    // A operands: Wpad[lr][lk] = W_D[lr][lk] (lr < 4); A1[lr][lk] = (W_D - I)[lr - c0][lk] (lr in the
+    // block): W_D through LDS (every lane holds it; lane 0 writes, each lane reads its entry)
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) xw[b][4 * i + k] = k <= i ? Wd[i][k] : 0.0;
+    }
+    wave_lds_fence();
+    const double wpad = lr < 4 ? xw[b][4 * lr + lk] : 0.0;
+    const double a1 =
+        (lr >= c0 && lr < c0 + 4) ? xw[b][4 * (lr - c0) + lk] - (lr - c0 == lk ? 1.0 : 0.0) : 0.0;
     // panel P[lr][lk] = L[lr][c0 + lk] (rows above the block and padding columns 0)
     double p = __builtin_amdgcn_mfma_f64_16x16x4f64(wpad, a[b], f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0)[0];
     p = (lr >= c0 && (FULL || c0 + lk < jv)) ? p : 0.0;

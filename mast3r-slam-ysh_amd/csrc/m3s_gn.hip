@@ -6164,11 +6164,14 @@ __device__ void track_solve_block(const LinArgs &A) {
 //   2. arrival: one lane per workgroup adds 1 to counter shard b % 8 (8
 //      counters on lines of their own: 32 arrivals per word instead of 256);
 //      wave 0 polls all shards (sc1 loads) until every workgroup has arrived;
-//   3. EVERY workgroup reads all G partials (sc1 loads) and sums them in fp64
-//      in a fixed order, then its thread 0 runs the same 7x7 update
-//      (track_update): identical inputs and order give identical poses and
-//      convergence decisions in every workgroup, so nothing is broadcast and
-//      all workgroups leave the loop together.
+//   3. the last arriver of a shard sums the shard's partials (fp64, fixed
+//      order) into its shard slot and arrives at the top counter; the last of
+//      those sums the 8 shard slots in shard order, runs the 7x7 update
+//      (track_update) and publishes the record (pose, status, cost) as four
+//      16-B write-through stores, each carrying the iteration as a tag in its
+//      last word; the other workgroups poll the four granules until every tag
+//      reads it + 1 (a 16-B store lands whole: no drain, no flag word and no
+//      second load of the payload; round 4).
 // Slot reuse is safe: a workgroup writes slot it % 2 for iteration it only
 // after every workgroup arrived at it - 1, i.e. finished reading slot it - 2.
 // Waits are bounded (a timeout ends the solve with info[SOLVE_FAIL] = 2).
@@ -6182,11 +6185,10 @@ constexpr int kTrkSpins = 1 << 22;
 struct TrackSync {
   uint32_t ctr[kTrkShards][32];  // arrival counters, one 128-B line each
   uint32_t top[32];              // arrivals of the shards' last workgroups
-  uint32_t gen[32];              // iterations published by the reducer
-  float rec[32];                 // the published pose (8) and status
-  double old_cost[16];           // the published cost (check_convergence)
+  uint32_t rec[32];  // the published record: 4 tagged 16-B granules (pose 0-7, status 8, cost 9-10 | tag)
   double shard_sum[kTrkShards][kNP];  // level-1 sums (fp64)
 };
+static_assert(offsetof(TrackSync, rec) % 128 == 0, "the record granules share one line");
 inline size_t track_sync_off() { return 128; }  // after TrackState (<= 128 B)
 inline size_t track_part_off() { return track_sync_off() + sizeof(TrackSync); }
 static_assert(sizeof(TrackState) <= 128, "TrackState must fit before the sync lines");
@@ -6205,8 +6207,9 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
   __shared__ float redf[NW][kNP];
   __shared__ double redd[NW][kNP];
   __shared__ double s_sum[kNP];
-  __shared__ float T_s[8];
-  __shared__ int state_s;  // kTrackContinue / kTrackConverged / kTrackFailed / 3 = barrier timeout
+  // the iteration's record: pose (0-7), status (8: kTrackContinue /
+  // kTrackConverged / kTrackFailed / 3 = barrier timeout), cost (9-10)
+  __shared__ uint32_t pub_s[12];
   __shared__ __attribute__((aligned(16))) float blk_s[kNP];
   TrackState *st = A.track;
   const int64_t HW = A.HW;
@@ -6224,6 +6227,9 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
   Sim3f T = load_sim3(st->T_rel);
   const Sim3f Tk = load_sim3(st->T_WCk);
   int it = 0, status = kTrackContinue;
+  // the record granules (lanes >= 4: offsets past the range, loads read zeros
+  // and stores are dropped)
+  const __amdgpu_buffer_rsrc_t Rrec = __builtin_amdgcn_make_buffer_rsrc(sync->rec, 0, 64, 0x00020000);
   for (; it < max_iters; it++) {
     M3S_TSTAMP(0)
     const Sim3Mat Tm = sim3_matrix(T);
@@ -6313,49 +6319,46 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
         wave_lds_fence();
         M3S_TSTAMP(4)
         if (lane == 0) {
-          // the previous reducer's cost (published with its record; inf first)
-          double oc = it == 0 ? __builtin_inf() : ld_sc1(&sync->old_cost[0]);
+          // the previous record's cost (inf first)
+          double oc = it == 0 ? __builtin_inf()
+                              : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
           Sim3f Tn = T;
           const int r = track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
           if (r == kTrackFailed) Tn = T;
-          float rec[9];
+          float rec[8];
           store_sim3(rec, Tn);
-          rec[8] = __int_as_float(r);
 #pragma unroll
-          for (int k = 0; k < 8; k++) T_s[k] = rec[k];
-          state_s = r;
-#pragma unroll
-          for (int k = 0; k < 9; k++) store_sc1(&sync->rec[k], rec[k]);
-          st_sc1(&sync->old_cost[0], oc);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(&sync->gen[0], (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int k = 0; k < 8; k++) pub_s[k] = __float_as_uint(rec[k]);
+          const unsigned long long ob = (unsigned long long)__double_as_longlong(oc);
+          pub_s[8] = (uint32_t)r, pub_s[9] = (uint32_t)(ob & 0xffffffffull), pub_s[10] = (uint32_t)(ob >> 32);
+          pub_s[11] = 0;
         }
-      } else if (lane == 0) {
+        wave_lds_fence();
+        const int q = lane < 4 ? 3 * lane : 0;
+        const u32x4 w = {pub_s[q], pub_s[q + 1], pub_s[q + 2], (unsigned)(it + 1)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, Rrec, lane * 16, 0, 16);
+      } else {
         int spins = 0;
-        while (__hip_atomic_load(&sync->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)(it + 1)) {
+        u32x4 g;
+        for (;;) {
+          g = __builtin_amdgcn_raw_buffer_load_b128(Rrec, lane * 16, 0, 16);
+          if (__ballot(lane < 4 && g.w != (unsigned)(it + 1)) == 0) break;
           __builtin_amdgcn_s_sleep(1);
           if (++spins > kTrkSpins) break;
         }
         M3S_TSTAMP(4)
         if (spins > kTrkSpins) {
-          state_s = 3;
-        } else {
-          float rec[9];
-#pragma unroll
-          for (int k = 0; k < 9; k++)
-            rec[k] = __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t *>(&sync->rec[k]), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT));
-#pragma unroll
-          for (int k = 0; k < 8; k++) T_s[k] = rec[k];
-          state_s = __float_as_int(rec[8]);
+          if (lane == 0) pub_s[8] = 3;
+        } else if (lane < 4) {
+          pub_s[3 * lane] = g.x, pub_s[3 * lane + 1] = g.y, pub_s[3 * lane + 2] = g.z;
         }
       }
     }
     M3S_TSTAMP(5)
     __syncthreads();
-    status = state_s;
+    status = (int)pub_s[8];
     if (status == 3 || status == kTrackFailed) break;
-    T = load_sim3(T_s);
+    T = load_sim3(reinterpret_cast<const float *>(pub_s));
     if (status == kTrackConverged) break;
   }
   if (b == 0 && t == 0) {  // outputs: the last successful pose, the iteration count, the status

@@ -6165,8 +6165,9 @@ __device__ void track_solve_block(const LinArgs &A) {
 //      counters on lines of their own: 32 arrivals per word instead of 256);
 //      wave 0 polls all shards (sc1 loads) until every workgroup has arrived;
 //   3. the last arriver of a shard sums the shard's partials (fp64, fixed
-//      order) into its shard slot and arrives at the top counter; the last of
-//      those sums the 8 shard slots in shard order, runs the 7x7 update
+//      order) and publishes the 36 sums as tagged 16-B granules; the last
+//      arriver of shard 0 polls the 8 shards' granules, sums them in shard
+//      order, runs the 7x7 update
 //      (track_update) and publishes the record (pose, status, cost) as four
 //      16-B write-through stores, each carrying the iteration as a tag in its
 //      last word; the other workgroups poll the four granules until every tag
@@ -6184,9 +6185,8 @@ constexpr int kTrkShards = 8;
 constexpr int kTrkSpins = 1 << 22;
 struct TrackSync {
   uint32_t ctr[kTrkShards][32];  // arrival counters, one 128-B line each
-  uint32_t top[32];              // arrivals of the shards' last workgroups
   uint32_t rec[32];  // the published record: 4 tagged 16-B granules (pose 0-7, status 8, cost 9-10 | tag)
-  double shard_sum[kTrkShards][kNP];  // level-1 sums (fp64)
+  uint32_t shard_sum[kTrkShards][kNP][4];  // level-1 sums (fp64), tagged 16-B granules {lo, hi, tag, 0}
 };
 static_assert(offsetof(TrackSync, rec) % 128 == 0, "the record granules share one line");
 inline size_t track_sync_off() { return 128; }  // after TrackState (<= 128 B)
@@ -6230,6 +6230,8 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
   // the record granules (lanes >= 4: offsets past the range, loads read zeros
   // and stores are dropped)
   const __amdgpu_buffer_rsrc_t Rrec = __builtin_amdgcn_make_buffer_rsrc(sync->rec, 0, 64, 0x00020000);
+  const __amdgpu_buffer_rsrc_t Rsh = __builtin_amdgcn_make_buffer_rsrc(sync->shard_sum, 0, (int)sizeof(sync->shard_sum), 0x00020000);
+  constexpr int kShFar = (int)sizeof(TrackSync::shard_sum);  // past the range: no access
   for (; it < max_iters; it++) {
     M3S_TSTAMP(0)
     const Sim3Mat Tm = sim3_matrix(T);
@@ -6297,25 +6299,38 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
         int idx;
         bool ok;
         const double x = xreduce36(a, lane, idx, ok);
-        if (ok) st_sc1(&sync->shard_sum[sh][idx], x);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // level 2: the last shard reducer sums the shard sums in shard order
-        uint32_t o2 = 0;
-        if (lane == 0) o2 = __hip_atomic_fetch_add(&sync->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        o2 = __builtin_amdgcn_readfirstlane(o2);
-        top_last = o2 == n_top * (uint32_t)(it + 1) - 1;
+        {
+          const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
+          const u32x4 w = {(unsigned)(xb & 0xffffffffull), (unsigned)(xb >> 32), (unsigned)(it + 1), 0u};
+          __builtin_amdgcn_raw_buffer_store_b128(w, Rsh, ok ? (sh * kNP + idx) * 16 : kShFar, 0, 16);
+        }
+        // level 2: the last arriver of shard 0 sums the shard sums in shard
+        // order as their granules land
+        top_last = sh == 0;
       }
       if (top_last) {
         M3S_TSTAMP(3)
-        if (lane < kNP) {
-          double v[kTrkShards];
+        u32x4 g[kTrkShards];
+        int spins = 0;
+        for (;;) {
 #pragma unroll
-          for (int j = 0; j < kTrkShards; j++) v[j] = j < (int)n_top ? ld_sc1(&sync->shard_sum[j][lane]) : 0.0;
+          for (int j = 0; j < kTrkShards; j++)
+            g[j] = __builtin_amdgcn_raw_buffer_load_b128(Rsh, (lane < kNP && j < (int)n_top) ? (j * kNP + lane) * 16 : kShFar, 0, 16);
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < kTrkShards; j++) ok &= lane >= kNP || j >= (int)n_top || g[j].z == (unsigned)(it + 1);
+          if (__ballot(!ok) == 0) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kTrkSpins) break;
+        }
+        if (lane < kNP) {
           double x = 0.0;
 #pragma unroll
-          for (int j = 0; j < kTrkShards; j++) x += v[j];
+          for (int j = 0; j < kTrkShards; j++)
+            x += j < (int)n_top ? __longlong_as_double((long long)(((unsigned long long)g[j].y << 32) | g[j].x)) : 0.0;
           s_sum[lane] = x;
         }
+        const bool timed_out = spins > kTrkSpins;  // bounded wait: published as status 3
         wave_lds_fence();
         M3S_TSTAMP(4)
         if (lane == 0) {
@@ -6323,8 +6338,8 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
           double oc = it == 0 ? __builtin_inf()
                               : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
           Sim3f Tn = T;
-          const int r = track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
-          if (r == kTrackFailed) Tn = T;
+          const int r = timed_out ? 3 : track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
+          if (r != kTrackContinue && r != kTrackConverged) Tn = T;
           float rec[8];
           store_sim3(rec, Tn);
 #pragma unroll

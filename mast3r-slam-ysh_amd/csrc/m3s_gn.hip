@@ -6157,34 +6157,32 @@ __device__ void track_solve_block(const LinArgs &A) {
 // 173-266). G <= 256 workgroups, one per CU, each owning PPL pixels per lane.
 // A lane loads its pixels' inputs once (target-side PixIn from Xk / Q / valid
 // and the source point Xf) and keeps them in registers across iterations, so
-// iterations 2.. read nothing from HBM. Per iteration:
+// iterations 2.. read nothing from HBM. Per iteration (round 4: every
+// hand-off is a tagged 16-B granule, {payload | it + 1}, stored write-through
+// and polled by its reader; a 16-B store lands whole, so no drain, counter or
+// second load of the payload sits on the critical path):
 //   1. each workgroup accumulates its pixels (the packed Accum of the backend
-//      kernels) and stores its 36-float partial, write-through (sc1), into the
-//      iteration's slot (double-buffered by iteration parity);
-//   2. arrival: one lane per workgroup adds 1 to counter shard b % 8 (8
-//      counters on lines of their own: 32 arrivals per word instead of 256);
-//      wave 0 polls all shards (sc1 loads) until every workgroup has arrived;
-//   3. the last arriver of a shard sums the shard's partials (fp64, fixed
-//      order) and publishes the 36 sums as tagged 16-B granules; the last
-//      arriver of shard 0 polls the 8 shards' granules, sums them in shard
-//      order, runs the 7x7 update
-//      (track_update) and publishes the record (pose, status, cost) as four
-//      16-B write-through stores, each carrying the iteration as a tag in its
-//      last word; the other workgroups poll the four granules until every tag
-//      reads it + 1 (a 16-B store lands whole: no drain, no flag word and no
-//      second load of the payload; round 4).
-// Slot reuse is safe: a workgroup writes slot it % 2 for iteration it only
-// after every workgroup arrived at it - 1, i.e. finished reading slot it - 2.
-// Waits are bounded (a timeout ends the solve with info[SOLVE_FAIL] = 2).
-// Hand-off form: MI355X_MICROARCH.md inter-workgroup table, row 1 (sc1 stores
-// drained by the storing wave, agent atomic add by one lane of it, sc1 poll,
-// sc1 loads after a workgroup barrier).
+//      kernels) and stores its 36-float partial as 12 granules;
+//   2. workgroup s < 8 polls the granules of shard s = {s, s + 8, ...} (lane j:
+//      member s + 8 j), sums them across lanes in a fixed order (fp64) and
+//      publishes the 36 shard sums as granules;
+//   3. workgroup 0 polls the 8 shards' granules, sums them in shard order,
+//      runs the 7x7 update (track_update) and publishes the record (pose,
+//      status, cost) as 4 granules; every other workgroup polls those.
+// Reuse of the granules is safe: a workgroup stores iteration it + 1's
+// partial only after it read iteration it's record, which workgroup 0
+// published after every shard reducer had read iteration it's partials.
+// The reduction order is fixed (deterministic). Waits are bounded: a timed-out
+// shard sum is NaN (the update then fails, info[SOLVE_FAIL] = 1), a timed-out
+// record poll ends the solve with info[SOLVE_FAIL] = 2. Round 2 and 3 used
+// drained sc1 stores + agent atomic counters (MI355X_MICROARCH.md
+// inter-workgroup table, row 1): 95-99k GN it/s at C2 against ~112k+ now.
 constexpr int kTrkThreads = 512;
 constexpr int kTrkMaxBlocks = 256;
 constexpr int kTrkShards = 8;
+constexpr int kTrkGran = kNP / 3;  // 16-B granules per workgroup partial (3 sums + tag)
 constexpr int kTrkSpins = 1 << 22;
 struct TrackSync {
-  uint32_t ctr[kTrkShards][32];  // arrival counters, one 128-B line each
   uint32_t rec[32];  // the published record: 4 tagged 16-B granules (pose 0-7, status 8, cost 9-10 | tag)
   uint32_t shard_sum[kTrkShards][kNP][4];  // level-1 sums (fp64), tagged 16-B granules {lo, hi, tag, 0}
 };
@@ -6192,6 +6190,7 @@ static_assert(offsetof(TrackSync, rec) % 128 == 0, "the record granules share on
 inline size_t track_sync_off() { return 128; }  // after TrackState (<= 128 B)
 inline size_t track_part_off() { return track_sync_off() + sizeof(TrackSync); }
 static_assert(sizeof(TrackState) <= 128, "TrackState must fit before the sync lines");
+static_assert((128 + sizeof(TrackSync)) % 16 == 0, "the partial granules are 16-B aligned");
 
 #ifdef M3S_TRK_STAMPS  // phase stamps of workgroups 0 and G - 1 (tools/trk_stamps.py)
 __device__ int64_t g_trk_stamp[2][16][8];
@@ -6232,6 +6231,9 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
   const __amdgpu_buffer_rsrc_t Rrec = __builtin_amdgcn_make_buffer_rsrc(sync->rec, 0, 64, 0x00020000);
   const __amdgpu_buffer_rsrc_t Rsh = __builtin_amdgcn_make_buffer_rsrc(sync->shard_sum, 0, (int)sizeof(sync->shard_sum), 0x00020000);
   constexpr int kShFar = (int)sizeof(TrackSync::shard_sum);  // past the range: no access
+  const __amdgpu_buffer_rsrc_t Rpart =
+      __builtin_amdgcn_make_buffer_rsrc(A.partials, 0, kTrkMaxBlocks * kTrkGran * 16, 0x00020000);
+  constexpr int kPartFar = kTrkMaxBlocks * kTrkGran * 16;
   for (; it < max_iters; it++) {
     M3S_TSTAMP(0)
     const Sim3Mat Tm = sim3_matrix(T);
@@ -6257,9 +6259,9 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
       if (ok) redf[wv][idx] = x;
     }
     __syncthreads();
-    float *slot = A.partials;
     if (wv == 0) {
-      // block partial -> LDS -> 9 x 16-B write-through stores
+      // block partial -> LDS -> 12 tagged 16-B granules {3 sums | it + 1}
+      // (write-through, no drain: the shard reducer polls them)
       if (lane < kNP) {
         float x = 0.0f;
 #pragma unroll
@@ -6267,35 +6269,44 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
         blk_s[lane] = x;
       }
       wave_lds_fence();
-      if (lane < kNP / 4) st_sc1_x4(slot + (size_t)b * kNP + 4 * lane, reinterpret_cast<const f32x4 *>(blk_s)[lane]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has left this wave
+      {
+        const int q = lane < kTrkGran ? 3 * lane : 0;
+        const u32x4 w = {__float_as_uint(blk_s[q]), __float_as_uint(blk_s[q + 1]), __float_as_uint(blk_s[q + 2]),
+                         (unsigned)(it + 1)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, Rpart, lane < kTrkGran ? (b * kTrkGran + lane) * 16 : kPartFar, 0, 16);
+      }
       M3S_TSTAMP(2)
-      // level 1: the last arriver of shard s = b % 8 (told by the value its
-      // add returned) sums the shard's partials (blocks s, s + 8, ..., lane j
-      // = block s + 8 j: a fixed order) into shard_sum[s] in fp64
-      const int sh = b % kTrkShards;
-      const uint32_t n_sh = (uint32_t)(G - sh + kTrkShards - 1) / kTrkShards;
+      // level 1: workgroup s < 8 reduces shard s = {s, s + 8, ...}: lane j
+      // polls member s + 8 j's granules, then the 36 sums are reduced across
+      // the lanes in a fixed order (fp64)
+      const int sh = b;
       const uint32_t n_top = (uint32_t)(G < kTrkShards ? G : kTrkShards);
-      uint32_t o = 0;
-      if (lane == 0) o = __hip_atomic_fetch_add(&sync->ctr[sh][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      o = __builtin_amdgcn_readfirstlane(o);
       bool top_last = false;
-      if (o == n_sh * (uint32_t)(it + 1) - 1) {
+      if (b < kTrkShards) {
+        const int n_sh = (G - sh + kTrkShards - 1) / kTrkShards;
+        u32x4 g[kTrkGran];
+        int spins = 0;
+        for (;;) {
+#pragma unroll
+          for (int k = 0; k < kTrkGran; k++)
+            g[k] = __builtin_amdgcn_raw_buffer_load_b128(
+                Rpart, lane < n_sh ? ((sh + kTrkShards * lane) * kTrkGran + k) * 16 : kPartFar, 0, 16);
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < kTrkGran; k++) ok &= lane >= n_sh || g[k].w == (unsigned)(it + 1);
+          if (__ballot(!ok) == 0) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kTrkSpins) break;
+        }
         double a[kNP];
 #pragma unroll
-        for (int k = 0; k < kNP; k++) a[k] = 0.0;
-        if (lane < (int)n_sh) {
-          const unsigned long long *src =
-              reinterpret_cast<const unsigned long long *>(slot + (size_t)(sh + kTrkShards * lane) * kNP);
-          unsigned long long w2[kNP / 2];
-#pragma unroll
-          for (int k = 0; k < kNP / 2; k++) w2[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-          for (int k = 0; k < kNP / 2; k++) {
-            a[2 * k] = (double)__uint_as_float((uint32_t)(w2[k] & 0xffffffffull));
-            a[2 * k + 1] = (double)__uint_as_float((uint32_t)(w2[k] >> 32));
-          }
+        for (int k = 0; k < kTrkGran; k++) {
+          a[3 * k] = (double)__uint_as_float(g[k].x);
+          a[3 * k + 1] = (double)__uint_as_float(g[k].y);
+          a[3 * k + 2] = (double)__uint_as_float(g[k].z);
         }
+        // a timed-out shard publishes a NaN sum: the update fails (status 2)
+        if (spins > kTrkSpins) a[0] = __builtin_nan("");
         int idx;
         bool ok;
         const double x = xreduce36(a, lane, idx, ok);
@@ -6304,8 +6315,8 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
           const u32x4 w = {(unsigned)(xb & 0xffffffffull), (unsigned)(xb >> 32), (unsigned)(it + 1), 0u};
           __builtin_amdgcn_raw_buffer_store_b128(w, Rsh, ok ? (sh * kNP + idx) * 16 : kShFar, 0, 16);
         }
-        // level 2: the last arriver of shard 0 sums the shard sums in shard
-        // order as their granules land
+        // level 2: workgroup 0 sums the shard sums in shard order as their
+        // granules land
         top_last = sh == 0;
       }
       if (top_last) {

@@ -37,4 +37,5 @@ for w in range(2):
         r = st[w, it]
         nxt = st[w, it + 1, 0] if it < 9 else r[5]
         ph = [(r[k + 1] - r[k]) * 0.01 for k in range(5)] + [(nxt - r[5]) * 0.01]
-        print(f"  it {it}: start {(r[0] - t0) * 0.01:7.2f} us  " + "  ".join(f"{x:5.2f}" for x in ph))
+        upd = f"   (update {(r[6] - r[4]) * 0.01:5.2f})" if w == 0 else ""
+        print(f"  it {it}: start {(r[0] - t0) * 0.01:7.2f} us  " + "  ".join(f"{x:5.2f}" for x in ph) + upd)

@@ -6350,6 +6350,7 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
                               : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
           Sim3f Tn = T;
           const int r = timed_out ? 3 : track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
+          M3S_TSTAMP(6)
           if (r != kTrackContinue && r != kTrackConverged) Tn = T;
           float rec[8];
           store_sim3(rec, Tn);

@@ -6177,7 +6177,10 @@ __device__ void track_solve_block(const LinArgs &A) {
 // record poll ends the solve with info[SOLVE_FAIL] = 2. Round 2 and 3 used
 // drained sc1 stores + agent atomic counters (MI355X_MICROARCH.md
 // inter-workgroup table, row 1): 95-99k GN it/s at C2 against ~112k+ now.
-constexpr int kTrkThreads = 512;
+// workgroup size: 256 threads (one wave per SIMD: the block reduction's waves
+// do not take turns; 116-121k -> 124-125k GN it/s at C2, round 4) while the
+// image fits 4 pixels per lane, else 512
+constexpr int kTrkThreadsLo = 256, kTrkThreadsHi = 512;
 constexpr int kTrkMaxBlocks = 256;
 constexpr int kTrkShards = 8;
 constexpr int kTrkGran = kNP / 3;  // 16-B granules per workgroup partial (3 sums + tag)
@@ -6199,10 +6202,10 @@ __device__ int64_t g_trk_stamp[2][16][8];
 #else
 #define M3S_TSTAMP(ph)
 #endif
-template <int MODE, int PPL>
-__global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A, int max_iters, TrackSync *sync) {
+template <int MODE, int PPL, int TH>
+__global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max_iters, TrackSync *sync) {
   const int G = (int)gridDim.x, b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
-  constexpr int NW = kTrkThreads / 64;
+  constexpr int NW = TH / 64;
   __shared__ float redf[NW][kNP];
   __shared__ double redd[NW][kNP];
   __shared__ double s_sum[kNP];
@@ -6217,7 +6220,7 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
   bool live[PPL];
 #pragma unroll
   for (int s = 0; s < PPL; s++) {
-    const int64_t p = ((int64_t)b * PPL + s) * kTrkThreads + t;
+    const int64_t p = ((int64_t)b * PPL + s) * TH + t;
     live[s] = p < HW;
     const int64_t pc = live[s] ? p : 0;
     in[s] = gather_pixel<MODE, true>(A, A.Xs, nullptr, pc, A.valid[pc] != 0, 0, A.Q[pc], 0.0f);
@@ -6399,9 +6402,10 @@ __global__ void __launch_bounds__(kTrkThreads) track_persistent_kernel(LinArgs A
   }
 }
 
-// pixels per lane of the persistent tracker (1, 2, 4) so that the grid fits
-// one workgroup per CU; 0: too large (one launch per iteration instead)
-int track_ppl(int64_t HW) {
+// pixels per lane of the persistent tracker (1, 2, 4) and its workgroup size
+// (threads) so that the grid fits one workgroup per CU; 0: too large (one
+// launch per iteration instead)
+int track_ppl(int64_t HW, int &threads) {
   static int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -6410,9 +6414,11 @@ int track_ppl(int64_t HW) {
     return n;
   }();
   const int64_t G = std::min<int64_t>(cus, kTrkMaxBlocks);
+  threads = kTrkThreadsLo;
   for (int ppl : {1, 2, 4})
-    if (HW <= G * kTrkThreads * ppl) return ppl;
-  return 0;
+    if (HW <= G * kTrkThreadsLo * ppl) return ppl;
+  threads = kTrkThreadsHi;
+  return HW <= G * kTrkThreadsHi * 4 ? 4 : 0;
 }
 // M3S_TRACK_PERSISTENT=0: one launch per iteration (A/B of the persistent kernel)
 bool track_persistent_enabled() { return knobs().track_persistent != 0; }
@@ -6464,18 +6470,21 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xf, 16) && vec_ok(a->Xk, 16) && vec_ok(a->Qk, 16) &&
                    vec_ok(a->valid, 4);
   // persistent: every iteration in one launch (one workgroup per CU)
-  const int ppl = track_ppl(a->HW);
+  int th = kTrkThreadsLo;
+  const int ppl = track_ppl(a->HW, th);
   if (ppl > 0 && track_persistent_enabled()) {
     if (a->max_iters < 1) return M3S_OK;
-    const int G = (int)((a->HW + (int64_t)kTrkThreads * ppl - 1) / ((int64_t)kTrkThreads * ppl));
+    const int G = (int)((a->HW + (int64_t)th * ppl - 1) / ((int64_t)th * ppl));
     if (mode == M3S_MODE_RAYS) {
-      if (ppl == 1) track_persistent_kernel<M3S_MODE_RAYS, 1><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
-      else if (ppl == 2) track_persistent_kernel<M3S_MODE_RAYS, 2><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
-      else track_persistent_kernel<M3S_MODE_RAYS, 4><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+      if (th == kTrkThreadsHi) track_persistent_kernel<M3S_MODE_RAYS, 4, kTrkThreadsHi><<<G, th, 0, st>>>(L, a->max_iters, sync);
+      else if (ppl == 1) track_persistent_kernel<M3S_MODE_RAYS, 1, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
+      else if (ppl == 2) track_persistent_kernel<M3S_MODE_RAYS, 2, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
+      else track_persistent_kernel<M3S_MODE_RAYS, 4, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
     } else {
-      if (ppl == 1) track_persistent_kernel<M3S_MODE_CALIB, 1><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
-      else if (ppl == 2) track_persistent_kernel<M3S_MODE_CALIB, 2><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
-      else track_persistent_kernel<M3S_MODE_CALIB, 4><<<G, kTrkThreads, 0, st>>>(L, a->max_iters, sync);
+      if (th == kTrkThreadsHi) track_persistent_kernel<M3S_MODE_CALIB, 4, kTrkThreadsHi><<<G, th, 0, st>>>(L, a->max_iters, sync);
+      else if (ppl == 1) track_persistent_kernel<M3S_MODE_CALIB, 1, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
+      else if (ppl == 2) track_persistent_kernel<M3S_MODE_CALIB, 2, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
+      else track_persistent_kernel<M3S_MODE_CALIB, 4, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
     }
     return launch_ok();
   }

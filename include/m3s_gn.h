@@ -230,10 +230,12 @@ int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void 
  * the recorded spans in launch order (ms[k], kinds[k]: 0 first-iteration
  * gathering linearize, 1 packed linearize, 2 solve), at most cap of them;
  * the return value is the number of spans (or a negative status). The
- * record is cleared after reading. Linearize spans are the kernel's own
- * execution span (first block start to last block end, stamped by the
- * kernel on the device wall clock; round 4: the events around the launch read
- * ~8% above the kernel trace); solve spans come from the events. */
+ * record is cleared after reading. Linearize spans are the dispatch's own
+ * begin / end timestamps: the call launches each linearize through
+ * hipExtLaunchKernel with a start / stop event pair (round 4: events recorded
+ * around the launch read 6-12% above the kernel trace). A linearize that does
+ * not go through that launch (the non-vectorised first iteration) and every
+ * solve span use the events recorded around the launches. */
 int m3s_debug_call_timing(int enable);
 int m3s_debug_call_times(float *ms, int32_t *kinds, int cap);
 

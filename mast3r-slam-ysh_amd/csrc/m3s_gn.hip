@@ -1632,6 +1632,24 @@ __device__ __forceinline__ void st_sc1(double *p, double v) {
 __device__ __forceinline__ void st_sc1_x4(float *p, f32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
+// Poll load of a tagged 16-B granule (write-through producer, sc1 load). The
+// empty asm with a memory clobber in front of every copy of the load makes it
+// a fresh read on every pass of its wait loop, whatever unrolling, peeling or
+// loop-invariant motion does to the loop. The builtin alone is a read-only
+// memory op that the compiler may hoist out of a loop that stores nothing:
+// it did once the s_sleep was gone (round 4, profiles/r04/
+// trk_ab_sleep0_INVALID.txt), and the aux "volatile" bit 31 does not stop
+// that (round 5: the load still left the loop). tests/test_isa.py checks every
+// poll loop of the library for its load.
+#ifndef M3S_POLL_BARRIER  // 0: only for tests/test_isa.py's negative check (compile-only)
+#define M3S_POLL_BARRIER 1
+#endif
+__device__ __forceinline__ u32x4 poll_b128(__amdgpu_buffer_rsrc_t R, int off) {
+#if M3S_POLL_BARRIER
+  asm volatile("" ::: "memory");
+#endif
+  return __builtin_amdgcn_raw_buffer_load_b128(R, off, 0, 16);
+}
 template <bool SC1>
 __device__ __forceinline__ double ld_blk(const double *p) {
   if (SC1) return ld_sc1(p);
@@ -2755,7 +2773,7 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
             __builtin_amdgcn_make_buffer_rsrc(D.Wgr, 0, (int)(16 * 49 * (D.m + 1)), 0x00020000);
         int spins = 0;
         for (;;) {
-          const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(RG, (k * 49 + lane49) * 16, 0, 16);
+          const u32x4 g = poll_b128(RG, (k * 49 + lane49) * 16);
           if (__ballot(act49 && g.z != (unsigned)want) == 0) {
             if (act49) W[lane] = __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
             break;
@@ -3651,7 +3669,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(double *p) {
 }
 __device__ __forceinline__ void gran_load(__amdgpu_buffer_rsrc_t R, int tile, int lane, GranTile &g) {
 #pragma unroll
-  for (int r = 0; r < 4; r++) g.v[r] = __builtin_amdgcn_raw_buffer_load_b128(R, ((tile * 4 + r) * 64 + lane) * 16, 0, 16);
+  for (int r = 0; r < 4; r++) g.v[r] = poll_b128(R, ((tile * 4 + r) * 64 + lane) * 16);
 }
 __device__ __forceinline__ bool gran_ready(const GranTile &g, int want) {  // wave-uniform
   const bool ok = g.v[0].z == (unsigned)want && g.v[1].z == (unsigned)want && g.v[2].z == (unsigned)want &&
@@ -4748,7 +4766,12 @@ bool gather_lds_path();  // (knobs, below)
 // hipExtLaunchKernel: the events take the dispatch's own begin / end
 // timestamps (the kernel's span, as a kernel trace records it; events
 // recorded around the launch read 8-12% more, profiles/r04/prof_split_*.txt)
-hipEvent_t *g_lin_ext_ev = nullptr;  // {start, stop}; guarded by the CallTiming lock
+// {start, stop}; thread_local: set and consumed by one gn_full call on its own
+// thread (a call on another thread without timing never sees it). launch_lin
+// clears it when it used the pair, so the caller can tell a span whose
+// linearize went through another launch (the pack == 0 path) and fall back to
+// the events recorded around it.
+thread_local hipEvent_t *g_lin_ext_ev = nullptr;
 template <typename K>
 void launch_lin(K kernel, dim3 g, dim3 b, hipStream_t st, const LinArgs &L) {
   if (g_lin_ext_ev) {
@@ -5944,6 +5967,7 @@ struct CallTiming {
   std::vector<int> kind;       // kind of the span from event q to q + 1 (-1: none)
   size_t used = 0;
   std::vector<hipEvent_t> kev;  // pool: {start, stop} of each timed linearize dispatch
+  std::vector<char> kev_ok;     // per pair: the dispatch took it (else the span uses ev[q], ev[q + 1])
   size_t kused = 0;
 };
 CallTiming &call_timing() {
@@ -5995,10 +6019,14 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
         if (hipEventCreate(&e) != hipSuccess) return M3S_ELAUNCH;
         CT.kev.push_back(e);
       }
+      if (CT.kev_ok.size() < CT.kev.size() / 2) CT.kev_ok.resize(CT.kev.size() / 2);
       g_lin_ext_ev = &CT.kev[CT.kused];
-      CT.kused += 2;
     }
     rc = gn_linearize_impl(a, P, 0, a->E, nullptr, st, sparse, &chunks);
+    if (timing) {
+      CT.kev_ok[CT.kused / 2] = g_lin_ext_ev == nullptr;  // launch_lin took the pair
+      CT.kused += 2;
+    }
     g_lin_ext_ev = nullptr;
     if (rc) return rc;
     if (timing && !call_mark(st, 2)) return M3S_ELAUNCH;
@@ -6013,9 +6041,16 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
 constexpr size_t kTrackStateOff = 0;
 
 struct TrackSync;
-__global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackState *st, int32_t *info,
-                                  float *T_WCf_out, float *T_CkCf_out, uint32_t *sync_words, int n_sync) {
+// Zeroes the sync words and the persistent kernel's partial granules (n_part
+// 16-B granules, 0 on the launch-per-iteration path) of THIS call: a granule
+// is accepted once its tag equals it + 1, so a granule left with tag 1 by a
+// call that stopped after its first iteration (or a reused allocation holding
+// such a word) must never be read as iteration 0's partial.
+__global__ void __launch_bounds__(256) track_init_kernel(const float *T_WCf, const float *T_WCk, TrackState *st,
+                                                         int32_t *info, float *T_WCf_out, float *T_CkCf_out,
+                                                         uint32_t *sync_words, int n_sync, u32x4 *part, int n_part) {
   for (int k = threadIdx.x; k < n_sync; k += blockDim.x) sync_words[k] = 0u;
+  for (int k = threadIdx.x; k < n_part; k += blockDim.x) part[k] = u32x4{0u, 0u, 0u, 0u};
   if (threadIdx.x != 0) return;
   const Sim3f Tk = load_sim3(T_WCk), Tf = load_sim3(T_WCf);
   const Sim3f R = compose(inverse(Tk), Tf);
@@ -6030,8 +6065,10 @@ __global__ void track_init_kernel(const float *T_WCf, const float *T_WCk, TrackS
 }
 
 // One tracker GN update from the reduced sums s (kL / kG / kCost layout):
-// 7x7 fp64 Cholesky of H (one thread, fully unrolled; 1/L_kk by rsqrt + 2
-// Newton steps, no IEEE sqrt / division sequences on the serial chain),
+// 7x7 fp64 Cholesky of H (one thread, fully unrolled; 1/L_kk by rsqrt_nr:
+// v_rsq_f64 + one Newton step, 4.2e-15 relative, round 4 -- the tracker's
+// fixture parity, 1e-5 + 1e-4 sum|tau| per pose, holds with it; no IEEE sqrt /
+// division sequences on the serial chain),
 // tau = -H^-1 g (tracker.py:156-171: g = sum w e J with e = pred - meas), the
 // retraction T <- Exp(tau) T, and check_convergence (nonlinear_optimizer.py:
 // 5-25; rel is NaN on the first step, old_cost = inf). T and old_cost are
@@ -6202,6 +6239,16 @@ __device__ int64_t g_trk_stamp[2][16][8];
 #else
 #define M3S_TSTAMP(ph)
 #endif
+// M3S_TRK_SLEEP: s_sleep(1) per failed poll pass (0: spin; correct either
+// way, the poll loads are poll_b128)
+#ifndef M3S_TRK_SLEEP
+#define M3S_TRK_SLEEP 1
+#endif
+__device__ __forceinline__ void trk_pause() {
+#if M3S_TRK_SLEEP
+  __builtin_amdgcn_s_sleep(1);
+#endif
+}
 template <int MODE, int PPL, int TH>
 __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max_iters, TrackSync *sync) {
   const int G = (int)gridDim.x, b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -6292,13 +6339,12 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         for (;;) {
 #pragma unroll
           for (int k = 0; k < kTrkGran; k++)
-            g[k] = __builtin_amdgcn_raw_buffer_load_b128(
-                Rpart, lane < n_sh ? ((sh + kTrkShards * lane) * kTrkGran + k) * 16 : kPartFar, 0, 16);
+            g[k] = poll_b128(Rpart, lane < n_sh ? ((sh + kTrkShards * lane) * kTrkGran + k) * 16 : kPartFar);
           bool ok = true;
 #pragma unroll
           for (int k = 0; k < kTrkGran; k++) ok &= lane >= n_sh || g[k].w == (unsigned)(it + 1);
           if (__ballot(!ok) == 0) break;
-          __builtin_amdgcn_s_sleep(1);
+          trk_pause();
           if (++spins > kTrkSpins) break;
         }
         double a[kNP];
@@ -6329,12 +6375,12 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         for (;;) {
 #pragma unroll
           for (int j = 0; j < kTrkShards; j++)
-            g[j] = __builtin_amdgcn_raw_buffer_load_b128(Rsh, (lane < kNP && j < (int)n_top) ? (j * kNP + lane) * 16 : kShFar, 0, 16);
+            g[j] = poll_b128(Rsh, (lane < kNP && j < (int)n_top) ? (j * kNP + lane) * 16 : kShFar);
           bool ok = true;
 #pragma unroll
           for (int j = 0; j < kTrkShards; j++) ok &= lane >= kNP || j >= (int)n_top || g[j].z == (unsigned)(it + 1);
           if (__ballot(!ok) == 0) break;
-          __builtin_amdgcn_s_sleep(1);
+          trk_pause();
           if (++spins > kTrkSpins) break;
         }
         if (lane < kNP) {
@@ -6371,9 +6417,9 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         int spins = 0;
         u32x4 g;
         for (;;) {
-          g = __builtin_amdgcn_raw_buffer_load_b128(Rrec, lane * 16, 0, 16);
+          g = poll_b128(Rrec, lane * 16);
           if (__ballot(lane < 4 && g.w != (unsigned)(it + 1)) == 0) break;
-          __builtin_amdgcn_s_sleep(1);
+          trk_pause();
           if (++spins > kTrkSpins) break;
         }
         M3S_TSTAMP(4)
@@ -6445,8 +6491,13 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   TrackState *ts = at<TrackState>(a->workspace, kTrackStateOff);
   TrackSync *sync = at<TrackSync>(a->workspace, track_sync_off());
   float *partials = at<float>(a->workspace, track_part_off());
-  track_init_kernel<<<1, 64, 0, st>>>(a->T_WCf, a->T_WCk, ts, a->info, a->T_WCf_out, a->T_CkCf_out,
-                                      reinterpret_cast<uint32_t *>(sync), (int)(sizeof(TrackSync) / 4));
+  int th = kTrkThreadsLo;
+  const int ppl = track_ppl(a->HW, th);
+  const bool persistent = ppl > 0 && track_persistent_enabled();
+  const int G = persistent ? (int)((a->HW + (int64_t)th * ppl - 1) / ((int64_t)th * ppl)) : 0;
+  track_init_kernel<<<1, 256, 0, st>>>(a->T_WCf, a->T_WCk, ts, a->info, a->T_WCf_out, a->T_CkCf_out,
+                                       reinterpret_cast<uint32_t *>(sync), (int)(sizeof(TrackSync) / 4),
+                                       reinterpret_cast<u32x4 *>(partials), G * kTrkGran);
   if ((rc = launch_ok())) return rc;
   LinArgs L;
   memset(&L, 0, sizeof L);
@@ -6470,11 +6521,8 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
   const bool vec = (a->HW % 4 == 0) && vec_ok(a->Xf, 16) && vec_ok(a->Xk, 16) && vec_ok(a->Qk, 16) &&
                    vec_ok(a->valid, 4);
   // persistent: every iteration in one launch (one workgroup per CU)
-  int th = kTrkThreadsLo;
-  const int ppl = track_ppl(a->HW, th);
-  if (ppl > 0 && track_persistent_enabled()) {
+  if (persistent) {
     if (a->max_iters < 1) return M3S_OK;
-    const int G = (int)((a->HW + (int64_t)th * ppl - 1) / ((int64_t)th * ppl));
     if (mode == M3S_MODE_RAYS) {
       if (th == kTrkThreadsHi) track_persistent_kernel<M3S_MODE_RAYS, 4, kTrkThreadsHi><<<G, th, 0, st>>>(L, a->max_iters, sync);
       else if (ppl == 1) track_persistent_kernel<M3S_MODE_RAYS, 1, kTrkThreadsLo><<<G, th, 0, st>>>(L, a->max_iters, sync);
@@ -6730,7 +6778,7 @@ int m3s_debug_call_times(float *ms, int32_t *kinds, int cap) {
     if (T.kind[q] < 0) continue;
     if (n < cap) {
       float t = 0.0f;
-      const bool lin = T.kind[q] <= 1 && li + 1 < T.kused;
+      const bool lin = T.kind[q] <= 1 && li + 1 < T.kused && T.kev_ok[li / 2];
       if (hipEventElapsedTime(&t, lin ? T.kev[li] : T.ev[q], lin ? T.kev[li + 1] : T.ev[q + 1]) != hipSuccess)
         return M3S_ELAUNCH;
       ms[n] = t;

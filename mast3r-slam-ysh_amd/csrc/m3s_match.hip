@@ -209,9 +209,164 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
   A.p1_new[2 * gid + 1] = v_new;
 }
 
+// ---- round 5: refine_f16_kernel (fp16 descriptors, F in {16, 24, 32}) ----
+// The same scan, the same sequential fp16 FMA chain per candidate and the
+// same first-maximum rule as refine_kernel (bitwise equal outputs), re-cut
+// for the memory path:
+// * XCD bands: hardware block b runs on XCD b % 8; logical block
+//   (b % 8) * per + b / 8 gives each XCD one contiguous band of queries
+//   (image rows), so the D11 rows its windows read (+-radius*dilation_max
+//   rows) stay in that XCD's 4 MB L2 instead of every XCD streaming the
+//   whole descriptor image;
+// * buffer loads whose offset is past the descriptor image when the
+//   candidate lies outside it (the hardware returns zeros without an access):
+//   no branch per candidate, and a zero score never beats max_score (>= the
+//   smallest positive normal), as a skipped candidate never does;
+// * the next candidate's 16-B loads are issued before the current one's FMA
+//   chain (one candidate in flight per lane besides the one computing);
+// * the odd features are read from the high halves by op_sel (no shifts).
+#ifndef M3S_REF_XCD
+#define M3S_REF_XCD 1
+#endif
+#ifndef M3S_REF_PF
+#define M3S_REF_PF 1
+#endif
+typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
+constexpr int kRefFar = 0x7ffffff0;  // past any descriptor image (< 2^31 B): loads return zeros
+
+// Two candidates' scores, each the sequential fp16 FMA chain of the
+// reference in feature order (the low halves of v_pk_fma_f16: one rounding
+// per step, as v_fma_f16; the high halves compute a throw-away chain). The
+// odd feature is read from the high halves by op_sel (the .yy swizzle), so
+// no shifts; the two chains interleave, which also fills the one wait state
+// gfx950 needs between a VALU write and a dependent op_sel read.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+template <int NL>
+__device__ __forceinline__ void score2_f16(const h2v (&q)[4 * NL], const u32x4m (&xa)[NL], const u32x4m (&xb)[NL],
+                                           _Float16 &sa, _Float16 &sb) {
+  h2v a = {0, 0}, b = {0, 0};
+#pragma unroll
+  for (int w = 0; w < 4 * NL; w++) {
+    const h2v pa = __builtin_bit_cast(h2v, (unsigned)xa[w >> 2][w & 3]);
+    const h2v pb = __builtin_bit_cast(h2v, (unsigned)xb[w >> 2][w & 3]);
+    a = __builtin_elementwise_fma(q[w], pa, a);
+    b = __builtin_elementwise_fma(q[w], pb, b);
+    a = __builtin_elementwise_fma(q[w].yy, pa.yy, a);
+    b = __builtin_elementwise_fma(q[w].yy, pb.yy, b);
+  }
+  sa = a.x, sb = b.x;
+}
+
+template <int FMAX, int NR>
+__global__ void __launch_bounds__(kMatchThreads) refine_f16_kernel(m3s_refine_args A, int per_xcd) {
+  constexpr int NL = FMAX / 8;  // 16-B loads per descriptor
+  constexpr int N1 = 2 * NR + 1, NN = N1 * N1;
+  constexpr int F2 = FMAX * 2;  // bytes per descriptor
+  const int bh = (int)blockIdx.x;
+  const int64_t lb = M3S_REF_XCD ? (int64_t)(bh & 7) * per_xcd + (bh >> 3) : bh;
+  const int64_t gid = lb * kMatchThreads + threadIdx.x;
+  if (gid >= A.B * A.N) return;
+  const int64_t b = gid / A.N;
+  const int H = (int)A.H, W = (int)A.W;
+  // one wave-uniform resource over every batch's image (a per-batch base
+  // would not be uniform: a wave may straddle two batches)
+  const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(A.D11), 0, (int)(A.B * A.H * A.W * F2), 0x00020000);
+  const int base = (int)(b * A.H * A.W * F2);
+  h2v q[4 * NL];
+  {
+    const u32x4m *d21 = reinterpret_cast<const u32x4m *>(static_cast<const _Float16 *>(A.D21) + gid * FMAX);
+#pragma unroll
+    for (int l = 0; l < NL; l++) {
+      const u32x4m v = d21[l];
+#pragma unroll
+      for (int k = 0; k < 4; k++) q[4 * l + k] = __builtin_bit_cast(h2v, (unsigned)v[k]);
+    }
+  }
+  const int64_t pu = A.p1[2 * gid], pv = A.p1[2 * gid + 1];
+  // a centre this far out has no candidate inside the image at any dilation
+  // (radius * dilation_max < 2^20): the reference returns it unchanged
+  const bool far = pu < -(1 << 30) || pu > (1 << 30) || pv < -(1 << 30) || pv > (1 << 30);
+  int u0 = far ? -(1 << 30) : (int)pu, v0 = far ? -(1 << 30) : (int)pv;
+  _Float16 max_score = min_normal<_Float16>();
+  bool moved = false;
+  for (int d = A.dilation_max; d > 0; d--) {
+    const int rd = NR * d;
+    const int ub = u0 - rd, vb = v0 - rd;
+    // candidate c = i * N1 + j: u = ub + i d (outer), v = vb + j d (inner)
+    // (bitwise & / selects only: a short-circuit && becomes a branch per candidate)
+    unsigned uok = 0, vok = 0;
+#pragma unroll
+    for (int k = 0; k < N1; k++) {
+      uok |= ((unsigned)(ub + k * d) < (unsigned)W ? 1u : 0u) << k;
+      vok |= ((unsigned)(vb + k * d) < (unsigned)H ? 1u : 0u) << k;
+    }
+    // offsets stepped by wave-uniform increments (no per-candidate products)
+    // unsigned: a centre far outside wraps (every candidate is then masked)
+    const unsigned o0 = (unsigned)base + ((unsigned)vb * (unsigned)W + (unsigned)ub) * (unsigned)F2;
+    const unsigned du = (unsigned)(d * F2), dv = (unsigned)d * (unsigned)W * (unsigned)F2;
+    unsigned oi = o0, oij = o0;  // offset of (i, 0) and of the last candidate formed
+    auto load = [&](int c, u32x4m (&x)[NL]) {  // c in order; c >= NN: the pair's dummy (zeros)
+      const int i = c / N1, j = c % N1;
+      if (c > 0 && c < NN) {
+        if (j == 0) oi += du, oij = oi;
+        else oij += dv;
+      }
+      const unsigned ok = c < NN ? (uok >> i) & (vok >> j) & 1u : 0u;
+      const int o = ok ? (int)oij : kRefFar;
+#pragma unroll
+      for (int l = 0; l < NL; l++) x[l] = __builtin_amdgcn_raw_buffer_load_b128(R, o + 16 * l, 0, 0);
+    };
+    // pairs of candidates; the next pair's loads go out before this pair is scored
+    u32x4m x[2][2][NL];
+    load(0, x[0][0]);
+    load(1, x[0][1]);
+    int best = -1;
+#pragma unroll
+    for (int c = 0; c < NN; c += 2) {
+      const int s = (c >> 1) & 1;
+      if (c + 2 < NN) {
+        load(c + 2, x[s ^ 1][0]);
+        load(c + 3, x[s ^ 1][1]);
+      }
+      _Float16 sa, sb;
+      score2_f16<NL>(q, x[s][0], x[s][1], sa, sb);
+      const bool wa = sa > max_score;  // scan order: c before c + 1
+      max_score = wa ? sa : max_score;
+      best = wa ? c : best;
+      const bool wb = sb > max_score;
+      max_score = wb ? sb : max_score;
+      best = wb ? c + 1 : best;
+      __builtin_amdgcn_sched_barrier(0);  // one pair in flight: no loads hoisted further up
+    }
+    if (best >= 0) {
+      moved = true;
+      u0 = ub + (best / N1) * d;
+      v0 = vb + (best % N1) * d;
+    }
+  }
+  A.p1_new[2 * gid] = moved ? (int64_t)u0 : pu;
+  A.p1_new[2 * gid + 1] = moved ? (int64_t)v0 : pv;
+}
+
+#ifndef M3S_REF_V2
+#define M3S_REF_V2 1
+#endif
 template <typename T>
 int launch_refine(const m3s_refine_args &a, hipStream_t st) {
   const unsigned blocks = (unsigned)((a.B * a.N + kMatchThreads - 1) / kMatchThreads);
+  if (M3S_REF_V2 && sizeof(T) == 2 && (a.F == 16 || a.F == 24 || a.F == 32) && a.radius == 3 &&
+      a.B * a.H * a.W * a.F * 2 < (1ll << 30) && a.dilation_max < (1 << 16) && a.H < (1 << 20) &&
+      a.W < (1 << 20)) {
+    const int per = (int)((blocks + 7) / 8);
+    const unsigned grid = M3S_REF_XCD ? 8u * (unsigned)per : blocks;
+    switch (a.F) {
+      case 16: refine_f16_kernel<16, 3><<<grid, kMatchThreads, 0, st>>>(a, per); break;
+      case 24: refine_f16_kernel<24, 3><<<grid, kMatchThreads, 0, st>>>(a, per); break;
+      default: refine_f16_kernel<32, 3><<<grid, kMatchThreads, 0, st>>>(a, per); break;
+    }
+    return launch_status();
+  }
   switch (a.F) {  // descriptor width in registers for the common sizes
     case 16: refine_kernel<T, 16><<<blocks, kMatchThreads, 0, st>>>(a); break;
     case 24: refine_kernel<T, 24><<<blocks, kMatchThreads, 0, st>>>(a); break;

@@ -593,7 +593,7 @@ def prep_rays(X11, X21):
 
 # ------------------------------------------------------------ tracker ---
 def _track(fn, Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size, sigma_a, sigma_b, huber_k,
-           max_iters, rel_error, delta_norm, pixel_border=0, z_eps=0.0, sync_every=5):
+           max_iters, rel_error, delta_norm, pixel_border=0, z_eps=0.0, sync_every=5, workspace=None):
     _check(Xf, "Xf", torch.float32)
     _check(Xk, "Xk", torch.float32)
     _check(Qk, "Qk", torch.float32)
@@ -611,7 +611,14 @@ def _track(fn, Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size, sigma_a, sigma_b, h
     out_f = torch.empty(1, 8, dtype=torch.float32, device=dev)
     out_r = torch.empty(1, 8, dtype=torch.float32, device=dev)
     info = torch.zeros(8, dtype=torch.int32, device=dev)
-    ws = _workspace(_lib.m3s_track_workspace_size(HW), dev)
+    need = _lib.m3s_track_workspace_size(HW)
+    if workspace is None:
+        ws = _workspace(need, dev)
+    else:  # caller-owned (tests: reused / poisoned workspaces)
+        _check(workspace, "workspace", torch.uint8)
+        if workspace.device != dev or workspace.numel() < need:
+            raise RuntimeError(f"tracker workspace must be a uint8 tensor of >= {need} bytes on {dev}")
+        ws = workspace
     a = TrackArgs()
     a.Xf, a.Xk, a.Qk, a.valid = _p(Xf), _p(Xk), _p(Qk), _p(valid)
     a.T_WCf, a.T_WCk, a.K = _p(T_WCf), _p(T_WCk), _p(K)
@@ -629,22 +636,29 @@ def _track(fn, Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size, sigma_a, sigma_b, h
     return out_f, out_r, info
 
 
+def track_workspace_size(HW):
+    """Bytes of the tracker workspace for an image of HW pixels."""
+    return int(_lib.m3s_track_workspace_size(int(HW)))
+
+
 def track_rays_sim3(Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma_ray, sigma_dist, huber_k, max_iters,
-                    rel_error, delta_norm, sync_every=5):
+                    rel_error, delta_norm, sync_every=5, workspace=None):
     """Device form of FrameTracker.opt_pose_ray_dist_sim3 (tracker.py:173-214).
     Returns (T_WCf [1,8], T_CkCf [1,8], info int32[8]); info[1] != 0 means the
     Cholesky failed (the reference raises; tracker.py:91-93)."""
     return _track("m3s_track_rays_sim3", Xf, Xk, T_WCf, T_WCk, Qk, valid, None, None, sigma_ray,
-                  sigma_dist, huber_k, max_iters, rel_error, delta_norm, sync_every=sync_every)
+                  sigma_dist, huber_k, max_iters, rel_error, delta_norm, sync_every=sync_every,
+                  workspace=workspace)
 
 
 def track_calib_sim3(Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size, sigma_pixel, sigma_depth,
-                     huber_k, max_iters, rel_error, delta_norm, pixel_border, z_eps, sync_every=5):
+                     huber_k, max_iters, rel_error, delta_norm, pixel_border, z_eps, sync_every=5,
+                     workspace=None):
     """Device form of FrameTracker.opt_pose_calib_sim3 (tracker.py:216-266);
     Xf/Xk already constrained to rays, meas_k formed on device."""
     return _track("m3s_track_calib_sim3", Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size,
                   sigma_pixel, sigma_depth, huber_k, max_iters, rel_error, delta_norm,
-                  pixel_border=pixel_border, z_eps=z_eps, sync_every=sync_every)
+                  pixel_border=pixel_border, z_eps=z_eps, sync_every=sync_every, workspace=workspace)
 
 
 # -------------------------------------------------- stepwise (sharded) ---

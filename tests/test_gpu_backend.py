@@ -53,12 +53,13 @@ def run_gpu(be, mode, g, max_iter, delta, Twc0=None, Xs=None, valid=None):
     return Twc.cpu().numpy(), dx.cpu().numpy(), info.cpu().numpy()
 
 
-def run_oracle(mode, g, max_iter, delta, Twc0=None, Xs=None, valid=None):
+def run_oracle(mode, g, max_iter, delta, Twc0=None, Xs=None, valid=None, f64=False):
     p = params_for(mode, g)
     T0 = g.T_init.data.numpy() if Twc0 is None else np.asarray(Twc0)
     return orc.gn(p, T0, (g.Xs if Xs is None else Xs).numpy(), g.Cs.numpy(), g.ii.numpy(),
                   g.jj.numpy(), g.idx_ii2jj.numpy(),
-                  (g.valid_match if valid is None else valid).numpy(), g.Q.numpy(), max_iter, delta)
+                  (g.valid_match if valid is None else valid).numpy(), g.Q.numpy(), max_iter, delta,
+                  f64=f64)
 
 
 def constrained(g):
@@ -398,12 +399,21 @@ def test_gn_over_capacity_plan_takes_dense_fallback(be):
     keyframes fills all m (m + 1) / 2 = 20100 blocks of its factor, more than
     the workspace's sparse-slot capacity (64 m + 4096 + 1), so the call solves
     by the tiled fp64 Cholesky (n = 1400) instead of the block-sparse LLT;
-    against the oracle's dense fp64 solve (gn_kernels.cu:57-159 builds the same
-    system as triplets). One step tight; after 2 iterations the poses get
-    2e-3 of the step: the complete graph of a loop trajectory has many
-    near-empty edges (poorly conditioned H), so the fp32 H/g summation order
-    moves the second linearisation point further than on the loop graphs
-    (measured 2.1e-4 max|pose| difference at max|dx| 0.2)."""
+    against the oracle (gn_kernels.cu:57-159 builds the same system as
+    triplets). The yardstick is the oracle with fp64 sums (exact-arithmetic
+    stand-in, as tests/test_gpu_large.py).
+
+    Every GN step must be as accurate as the reference's fp32 step from the
+    SAME linearisation point: step 1 from the initial poses, and step 2 (the
+    packed linearize + the tiled solve of a 2-iteration call) from HIP's own
+    poses after step 1, each within the fp32 reference's distance to the
+    exact step + 1e-6. The trajectories themselves are not compared beyond
+    that: the complete graph of a loop trajectory has near-empty edges
+    (poorly conditioned H), and step 2 amplifies the ~1e-6 step-1 rounding
+    ~250x. The same fp32 oracle binary sits 5.8e-4 from the exact poses after
+    two iterations on the build container's CPU and 2.5e-4 on the GPU box's
+    (libm variants differ in the last ulp), so that distance measures the
+    problem, not the solver (round 5)."""
     from mast3r_slam_amd import synthetic
 
     N = 201
@@ -412,14 +422,31 @@ def test_gn_over_capacity_plan_takes_dense_fallback(be):
     g = synthetic.make_graph(N, 8, 12, seed=45, edges=(ii_u, jj_u))
     m = N - 1
     assert m * (m + 1) // 2 > 64 * m + 4096 + 1
-    _, dx1_gpu, info1 = run_gpu(be, "rays", g, 1, 0.0)
+    # step 1 from the initial poses
+    T1_gpu, dx1_gpu, info1 = run_gpu(be, "rays", g, 1, 0.0)
     _, dx1_ref, _, failed = run_oracle("rays", g, 1, 0.0)
-    assert failed == 0 and info1[be.INFO_SOLVE_FAIL] == 0
-    np.testing.assert_allclose(dx1_gpu, dx1_ref, atol=1e-6 + 1e-4 * np.abs(dx1_ref).max())
-    T_gpu, _, info = run_gpu(be, "rays", g, 2, 0.0)
-    T_ref, _, it, _ = run_oracle("rays", g, 2, 0.0)
-    assert info[be.INFO_ITERS] == it == 2
-    np.testing.assert_allclose(T_gpu, T_ref, atol=1e-5 + 2e-3 * np.abs(dx1_ref).max())
+    _, dx1_x, _, failed_x = run_oracle("rays", g, 1, 0.0, f64=True)
+    assert failed == 0 == failed_x and info1[be.INFO_SOLVE_FAIL] == 0
+    e1_hip, e1_ref = float(np.abs(dx1_gpu - dx1_x).max()), float(np.abs(dx1_ref - dx1_x).max())
+    # step 2: a 2-iteration call (its first iteration is bitwise the call above)
+    # against the exact and the fp32 reference step from HIP's poses after step 1
+    T2_gpu, dx2_gpu, info = run_gpu(be, "rays", g, 2, 0.0)
+    assert info[be.INFO_ITERS] == 2 and info[be.INFO_SOLVE_FAIL] == 0
+    T2_ref_h, dx2_ref, _, f2 = run_oracle("rays", g, 1, 0.0, Twc0=T1_gpu)
+    T2_x_h, dx2_x, _, f2x = run_oracle("rays", g, 1, 0.0, Twc0=T1_gpu, f64=True)
+    assert f2 == 0 == f2x
+    e2_hip, e2_ref = float(np.abs(dx2_gpu - dx2_x).max()), float(np.abs(dx2_ref - dx2_x).max())
+    p2_hip, p2_ref = float(np.abs(T2_gpu - T2_x_h).max()), float(np.abs(T2_ref_h - T2_x_h).max())
+    # the trajectories (reported, see the docstring)
+    T_ref, _, _, _ = run_oracle("rays", g, 2, 0.0)
+    T_x, _, _, _ = run_oracle("rays", g, 2, 0.0, f64=True)
+    print(f"dense fallback N={N}: max|dx - dx_exact| step 1 hip {e1_hip:.3e} ref {e1_ref:.3e}; "
+          f"step 2 (from HIP's T1) hip {e2_hip:.3e} ref {e2_ref:.3e}, poses hip {p2_hip:.3e} ref {p2_ref:.3e}; "
+          f"trajectories after 2 iterations max|T - T_exact| hip {np.abs(T2_gpu - T_x).max():.3e} "
+          f"ref {np.abs(T_ref - T_x).max():.3e} (max|dx1| {np.abs(dx1_x).max():.3f})")
+    assert e1_hip <= e1_ref + 1e-6
+    assert e2_hip <= e2_ref + 1e-6
+    assert p2_hip <= p2_ref + 1e-6
 
 
 def test_gn_singular_global_factor_zero_dx(be):

@@ -96,3 +96,28 @@ def test_matching_rejects_bad_inputs():
         be.iter_proj(img.to(DEV).transpose(1, 2), pts.to(DEV), p0.to(DEV), 10, 1e-8, 1e-6)
     with pytest.raises(RuntimeError):
         be.refine_matches(m.D11.to(DEV), m.D21.to(DEV).float(), m.p_true.to(DEV), 3, 5)
+
+
+@pytest.mark.parametrize("F", [16, 24, 32])
+def test_refine_matches_f16_kernel_batches_and_far_centres(F):
+    """refine_f16_kernel (round 5: XCD bands, zero-returning out-of-image
+    loads, pk-FMA chains): batched (a wave straddles the two batches: 37 x 53
+    pixels is not a multiple of 64), centres near and past the borders and far
+    outside (|p| up to 2^40: no candidate is inside, p is returned as is),
+    F = 16 / 24 / 32; integer output equal to the oracle."""
+    H, W = 37, 53
+    ms = [synthetic.make_match_inputs(H, W, seed=1100 + k, F=F) for k in range(2)]
+    D11 = torch.cat([m.D11 for m in ms]).contiguous()
+    D21 = torch.cat([m.D21 for m in ms]).contiguous()
+    rng = np.random.default_rng(F)
+    p = np.concatenate([m.p_true.numpy() for m in ms]).astype(np.int64)
+    p = p + rng.integers(-6, 7, p.shape)
+    sel = rng.random(p.shape[:2]) < 0.05
+    p[sel] = rng.integers(-25, 80, (int(sel.sum()), 2))  # near and past the borders
+    far = rng.random(p.shape[:2]) < 0.01
+    p[far] = rng.choice(np.array([-(1 << 40), (1 << 40), -(1 << 31) - 3, (1 << 31) + 5]), (int(far.sum()), 2))
+    ref = mo.refine_matches(D11.numpy(), D21.numpy(), p, 3, 5)
+    (out,) = be.refine_matches(D11.to(DEV), D21.to(DEV), torch.from_numpy(p).to(DEV), 3, 5)
+    out = out.cpu().numpy()
+    assert np.array_equal(out, ref), (out != ref).any(-1).sum()
+    assert np.array_equal(out[far], p[far])

@@ -30,7 +30,7 @@ def pose_tol(taus):
     return 1e-5 + 1e-4 * float(np.linalg.norm(np.asarray(taus, np.float64), axis=-1).sum())
 
 
-def run_gpu(be, d, max_iters=None, sync_every=5, cfg=None):
+def run_gpu(be, d, max_iters=None, sync_every=5, cfg=None, workspace=None):
     CFG = tro.TRACKING_CFG if cfg is None else cfg
     t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k])).to(DEV)  # noqa: E731
     mi = int(d["max_iters"]) if max_iters is None else max_iters
@@ -39,11 +39,12 @@ def run_gpu(be, d, max_iters=None, sync_every=5, cfg=None):
                                   t("K"), (int(d["H"]), int(d["W"])), CFG["sigma_pixel"],
                                   CFG["sigma_depth"], CFG["huber"], mi, CFG["rel_error"],
                                   CFG["delta_norm"], CFG["pixel_border"], CFG["depth_eps"],
-                                  sync_every=sync_every)
+                                  sync_every=sync_every, workspace=workspace)
     else:
         out = be.track_rays_sim3(t("Xf"), t("Xk"), t("T_WCf_init"), t("T_WCk"), t("Qk"), t("valid"),
                                  CFG["sigma_ray"], CFG["sigma_dist"], CFG["huber"], mi,
-                                 CFG["rel_error"], CFG["delta_norm"], sync_every=sync_every)
+                                 CFG["rel_error"], CFG["delta_norm"], sync_every=sync_every,
+                                 workspace=workspace)
     torch.cuda.synchronize()
     return [o.cpu().numpy() for o in out]
 
@@ -167,3 +168,41 @@ def test_persistent_tracker_matches_launch_per_iteration(be, knobs, calib, H, W)
     knobs("track_persistent", "1")
     T_p2, _, _ = run_gpu(be, d, cfg=CFG, sync_every=0)
     assert np.array_equal(T_p, T_p2)
+
+
+@pytest.mark.parametrize("calib", [False, True])
+def test_persistent_tracker_ignores_stale_partial_granules(be, calib):
+    """a workgroup partial is accepted once its tag is it + 1.
+    A workspace whose partial granules already carry tag 1 -- left by a call
+    that stopped after its first iteration, or poisoned here on purpose --
+    must not be read as iteration 0's partials: the call on it equals a call
+    on a fresh (zeroed) workspace bitwise."""
+    from mast3r_slam_amd import synthetic
+
+    H, W = 512, 512
+    p = synthetic.make_pair(H, W, seed=1004)
+    CFG = dict(tro.TRACKING_CFG, max_iters=10, rel_error=0.0, delta_norm=0.0)
+    Xf, Xk = p.Xf.numpy(), p.Xk.numpy()
+    if calib:
+        Xf = tro.constrain_points_to_ray((H, W), Xf, p.K.numpy())
+        Xk = tro.constrain_points_to_ray((H, W), Xk, p.K.numpy())
+    d = dict(calib=int(calib), Xf=Xf, Xk=Xk, T_WCf_init=p.T_WCf_init.data.numpy(),
+             T_WCk=p.T_WCk.data.numpy(), Qk=p.Qk.numpy(), valid=p.valid.numpy(), K=p.K.numpy(),
+             H=H, W=W, max_iters=10)
+    n = be.track_workspace_size(H * W)
+    fresh = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    T0, R0, i0 = run_gpu(be, d, cfg=CFG, sync_every=0, workspace=fresh)
+    assert i0[0] == 10 and i0[1] == 0
+    # 1) a one-iteration call leaves every used partial granule tagged 1
+    ws = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    _, _, i1 = run_gpu(be, d, cfg=CFG, max_iters=1, sync_every=0, workspace=ws)
+    assert i1[0] == 1
+    T1, R1, i1 = run_gpu(be, d, cfg=CFG, sync_every=0, workspace=ws)
+    assert np.array_equal(i1, i0) and np.array_equal(T1, T0) and np.array_equal(R1, R0)
+    # 2) a reused allocation holding tag-1 words (and huge payloads) everywhere
+    w32 = torch.full((n // 4,), 1e30, dtype=torch.float32, device=DEV).view(torch.int32)
+    w32[3::4] = 1
+    ws2 = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    ws2[: (n // 4) * 4] = w32.view(torch.uint8)
+    T2, R2, i2 = run_gpu(be, d, cfg=CFG, sync_every=0, workspace=ws2)
+    assert np.array_equal(i2, i0) and np.array_equal(T2, T0) and np.array_equal(R2, R0)

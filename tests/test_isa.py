@@ -135,3 +135,154 @@ def kernel_base(text, mode):
         if l.endswith(name):
             return int(l.split()[0], 16)
     raise AssertionError(name)
+
+
+# ------------------------------------------------------------ poll loops --
+# Every cross-workgroup wait in the library is a loop that re-reads a flag or
+# a tagged granule until it changes. If the compiler hoists the read out of
+# the loop (a plain read-only load in a loop that stores nothing may be), the
+# wait can only time out: round 4 saw exactly that in the tracker once its
+# s_sleep was removed (profiles/r04/trk_ab_sleep0_INVALID.txt). The loads are
+# now poll_b128 (m3s_gn.hip: a compiler memory barrier in front of each) or
+# agent-scope atomics. These tests find the loops in the machine code (natural
+# loops of the control-flow graph) and check that each one reads memory.
+
+POLL_READ = re.compile(r"^(buffer|global|flat)_(load|atomic)|^ds_(read|load|add_rtn|cmpst)")
+SC1_LOAD = re.compile(r"^buffer_load_dword\w*\s.*\bsc1\b")
+POLL_KERNELS = ("df_factor_kernel", "col_backsub_kernel", "tail_cyc_kernel", "tail_pair_kernel",
+                "sparse_llt_kernel", "track_persistent_kernel")
+TRK_SPINS = "0x400000"  # kTrkSpins = 1 << 22: the tracker's bounded-wait compare
+
+
+def functions(text):
+    """{symbol: [(address, instruction, branch-target offset or None)]}."""
+    out, cur = {}, None
+    for l in text.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(.*)>:$", l)
+        if m:
+            cur = m.group(2)
+            out[cur] = []
+            continue
+        if cur is None or not l.strip():
+            continue
+        m = re.search(r"//\s*([0-9A-Fa-f]+):?", l)
+        if m:
+            t = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", l)
+            out[cur].append((int(m.group(1), 16), l.split("//")[0].strip(), int(t.group(1), 16) if t else None))
+    return out
+
+
+def natural_loops(ins):
+    """(blocks [(first, end)], loops [(header, {blocks})]) of one function."""
+    base = ins[0][0]
+    at = {a: i for i, (a, _, _) in enumerate(ins)}
+    starts = {0}
+    for i, (_, t, off) in enumerate(ins):
+        if re.match(r"^s_(c?branch|endpgm|setpc)", t):
+            if i + 1 < len(ins):
+                starts.add(i + 1)
+            if off is not None and base + off in at:
+                starts.add(at[base + off])
+    starts = sorted(starts)
+    blocks = [(s, starts[k + 1] if k + 1 < len(starts) else len(ins)) for k, s in enumerate(starts)]
+    bid = {s: k for k, (s, _) in enumerate(blocks)}
+    succ = [set() for _ in blocks]
+    for k, (s, e) in enumerate(blocks):
+        _, t, off = ins[e - 1]
+        if off is not None and re.match(r"^s_c?branch", t) and base + off in at:
+            succ[k].add(bid[at[base + off]])
+        if not re.match(r"^s_(branch|endpgm|setpc)", t) and e < len(ins):
+            succ[k].add(k + 1)
+    pred = [set() for _ in blocks]
+    for u, vs in enumerate(succ):
+        for v in vs:
+            pred[v].add(u)
+    reach, st = set(), [0]
+    while st:
+        u = st.pop()
+        if u not in reach:
+            reach.add(u)
+            st += list(succ[u])
+    dom = {u: set(reach) for u in reach}
+    dom[0] = {0}
+    changed = True
+    while changed:
+        changed = False
+        for u in sorted(reach - {0}):
+            ps = [dom[p] for p in pred[u] if p in reach]
+            nd = (set.intersection(*ps) if ps else set()) | {u}
+            if nd != dom[u]:
+                dom[u], changed = nd, True
+    loops = []
+    for u in reach:
+        for h in succ[u]:
+            if h in dom[u]:  # back edge u -> h
+                body, st = {h}, [u]
+                while st:
+                    x = st.pop()
+                    if x not in body:
+                        body.add(x)
+                        st += [p for p in pred[x] if p in reach]
+                loops.append((h, body))
+    return blocks, loops
+
+
+def loops_marked(ins, marker):
+    """For every block holding an instruction that satisfies `marker`: the
+    instructions of the innermost natural loop around it."""
+    blocks, loops = natural_loops(ins)
+    out = []
+    for k, (s, e) in enumerate(blocks):
+        if any(marker(ins[i][1]) for i in range(s, e)):
+            around = [b for _, b in loops if k in b]
+            body = min(around, key=len) if around else {k}
+            out.append((ins[s][0], [ins[i][1] for q in sorted(body) for i in range(*blocks[q])]))
+    return out
+
+
+def test_every_poll_loop_reads_memory(disasm):
+    """Every loop of the solver and tracker kernels that waits (s_sleep) also
+    reads: the flag / granule it waits on is loaded on every pass."""
+    fns = functions(disasm)
+    seen = {k: 0 for k in POLL_KERNELS}
+    for name, ins in fns.items():
+        kern = next((k for k in POLL_KERNELS if k in name), None)
+        if kern is None or not ins:
+            continue
+        for addr, body in loops_marked(ins, lambda t: t.startswith("s_sleep")):
+            assert any(POLL_READ.match(t) for t in body), f"{name}: wait loop at {addr:#x} reads nothing"
+            seen[kern] += 1
+        if kern == "track_persistent_kernel":  # its three granule polls: 16-B sc1 buffer loads
+            polls = loops_marked(ins, lambda t: t.startswith("s_cmp") and TRK_SPINS in t)
+            assert len(polls) >= 3, (name, len(polls))
+            for addr, body in polls:
+                assert any(SC1_LOAD.match(t) for t in body), f"{name}: poll at {addr:#x} has no sc1 load"
+    assert all(seen.values()), seen
+
+
+def test_tracker_polls_keep_their_loads_without_sleep(tmp_path):
+    """The round-4 failure mode itself: the tracker built without the s_sleep
+    in its polls (-DM3S_TRK_SLEEP=0). Each bounded-wait loop must still hold
+    its granule load (with poll_b128's barrier removed, -DM3S_POLL_BARRIER=0,
+    the compiler hoists the partial and shard-sum loads out of the loop:
+    checked when this test was written, round 5)."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not (os.path.exists(hipcc) and os.path.exists(OBJDUMP)):
+        pytest.skip("hipcc or llvm-objdump missing")
+    src = os.path.join(ROOT, "mast3r-slam-ysh_amd", "csrc", "m3s_gn.hip")
+    obj = tmp_path / "nosleep.o"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-fno-slp-vectorize", "-std=c++17", "--cuda-device-only",
+                    "--no-gpu-bundle-output", "-c", "-DM3S_TRK_SLEEP=0", "-I", os.path.join(ROOT, "include"), src,
+                    "-o", str(obj)], check=True, capture_output=True)
+    text = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", str(obj)], check=True, capture_output=True,
+                          text=True).stdout
+    n = 0
+    for name, ins in functions(text).items():
+        if "track_persistent_kernel" not in name or not ins:
+            continue
+        polls = loops_marked(ins, lambda t: t.startswith("s_cmp") and TRK_SPINS in t)
+        assert len(polls) >= 3, (name, len(polls))
+        for addr, body in polls:
+            assert any(SC1_LOAD.match(t) for t in body), f"{name}: poll at {addr:#x} lost its load"
+        n += 1
+    assert n >= 8, n

@@ -87,7 +87,10 @@ constexpr int kTargetBlocks = M3S_TARGET_BLOCKS;  // linearize grid target (edge
 // random Xi reads then stay closer together in time per XCD (C3: 249 -> 232
 // us, 128 KFs rays: 1092 -> 1004 us; profiles/r03/tb_sweep_r3f.txt)
 constexpr int kGatherBlocks = M3S_GATHER_BLOCKS;
-constexpr int kMaxBlocks = 8192;  // workspace capacity for partials (>= both targets)
+#ifndef M3S_MAX_BLOCKS
+#define M3S_MAX_BLOCKS 8192
+#endif
+constexpr int kMaxBlocks = M3S_MAX_BLOCKS;  // workspace capacity for partials (>= both targets)
 static_assert(kTargetBlocks <= kMaxBlocks && kGatherBlocks <= kMaxBlocks, "linearize grid target above capacity");
 constexpr int kMaxSmallNp = 224;     // register Cholesky limit (n + 1 <= 7 * 32)
 constexpr int kCholThreads = 512;    // 16 x 32 thread grid
@@ -6222,9 +6225,25 @@ constexpr int kTrkMaxBlocks = 256;
 constexpr int kTrkShards = 8;
 constexpr int kTrkGran = kNP / 3;  // 16-B granules per workgroup partial (3 sums + tag)
 constexpr int kTrkSpins = 1 << 22;
+// M3S_TRK_TOPALL (round 5, default): no record hand-off. Every workgroup
+// polls the 8 shard sums itself, sums them in shard order and runs the same
+// 7x7 update (the same fp64 sums in the same order: every workgroup gets the
+// bitwise same pose, the one workgroup 0 published before). The shard sums
+// are double-buffered by iteration parity: shard s writes iteration it + 1
+// into the buffer of it - 1 only after its members' it + 1 partials, and
+// every workgroup of every shard has read iteration it - 1's sums by then
+// (its iteration-it partial, which the other shard reducers waited for,
+// follows its read of them). Measured no faster than the record protocol
+// (profiles/r05/trk_ab_topall.txt: 120-122k GN it/s at C2 for both, the 8 x
+// 36-granule load on every workgroup costs what the record hop saved), so
+// the default stays the round-4 record protocol (0).
+#ifndef M3S_TRK_TOPALL
+#define M3S_TRK_TOPALL 0
+#endif
+constexpr int kTrkShBufs = M3S_TRK_TOPALL ? 2 : 1;
 struct TrackSync {
   uint32_t rec[32];  // the published record: 4 tagged 16-B granules (pose 0-7, status 8, cost 9-10 | tag)
-  uint32_t shard_sum[kTrkShards][kNP][4];  // level-1 sums (fp64), tagged 16-B granules {lo, hi, tag, 0}
+  uint32_t shard_sum[kTrkShBufs][kTrkShards][kNP][4];  // level-1 sums (fp64), tagged 16-B granules {lo, hi, tag, 0}
 };
 static_assert(offsetof(TrackSync, rec) % 128 == 0, "the record granules share one line");
 inline size_t track_sync_off() { return 128; }  // after TrackState (<= 128 B)
@@ -6326,6 +6345,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         __builtin_amdgcn_raw_buffer_store_b128(w, Rpart, lane < kTrkGran ? (b * kTrkGran + lane) * 16 : kPartFar, 0, 16);
       }
       M3S_TSTAMP(2)
+      const int shb = M3S_TRK_TOPALL ? (it & 1) : 0;  // the shard-sum buffer of this iteration
       // level 1: workgroup s < 8 reduces shard s = {s, s + 8, ...}: lane j
       // polls member s + 8 j's granules, then the 36 sums are reduced across
       // the lanes in a fixed order (fp64)
@@ -6362,12 +6382,65 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         {
           const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
           const u32x4 w = {(unsigned)(xb & 0xffffffffull), (unsigned)(xb >> 32), (unsigned)(it + 1), 0u};
-          __builtin_amdgcn_raw_buffer_store_b128(w, Rsh, ok ? (sh * kNP + idx) * 16 : kShFar, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(w, Rsh, ok ? ((shb * kTrkShards + sh) * kNP + idx) * 16 : kShFar, 0, 16);
         }
         // level 2: workgroup 0 sums the shard sums in shard order as their
         // granules land
         top_last = sh == 0;
       }
+#if M3S_TRK_TOPALL
+      (void)top_last;
+      {
+        M3S_TSTAMP(3)
+        // level 2 on every workgroup: lanes j < n_top poll the last granule of
+        // shard j (cheap passes while the shards are still summing), then all
+        // 36 x n_top granules are loaded together and their tags checked
+        u32x4 g[kTrkShards];
+        int spins = 0;
+        for (;;) {
+          const u32x4 t35 = poll_b128(Rsh, lane < (int)n_top ? ((shb * kTrkShards + lane) * kNP + kNP - 1) * 16 : kShFar);
+          if (__ballot(lane < (int)n_top && t35.z != (unsigned)(it + 1)) == 0) break;
+          trk_pause();
+          if (++spins > kTrkSpins) break;
+        }
+        for (;;) {
+#pragma unroll
+          for (int j = 0; j < kTrkShards; j++)
+            g[j] = poll_b128(Rsh, (lane < kNP && j < (int)n_top) ? ((shb * kTrkShards + j) * kNP + lane) * 16 : kShFar);
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < kTrkShards; j++) ok &= lane >= kNP || j >= (int)n_top || g[j].z == (unsigned)(it + 1);
+          if (__ballot(!ok) == 0) break;
+          trk_pause();
+          if (++spins > kTrkSpins) break;
+        }
+        if (lane < kNP) {
+          double x = 0.0;
+#pragma unroll
+          for (int j = 0; j < kTrkShards; j++)
+            x += j < (int)n_top ? __longlong_as_double((long long)(((unsigned long long)g[j].y << 32) | g[j].x)) : 0.0;
+          s_sum[lane] = x;
+        }
+        const bool timed_out = spins > kTrkSpins;  // bounded wait: status 3
+        wave_lds_fence();
+        M3S_TSTAMP(4)
+        if (lane == 0) {
+          double oc = it == 0 ? __builtin_inf()
+                              : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
+          Sim3f Tn = T;
+          const int r = timed_out ? 3 : track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
+          M3S_TSTAMP(6)
+          if (r != kTrackContinue && r != kTrackConverged) Tn = T;
+          float rec[8];
+          store_sim3(rec, Tn);
+#pragma unroll
+          for (int k = 0; k < 8; k++) pub_s[k] = __float_as_uint(rec[k]);
+          const unsigned long long ob = (unsigned long long)__double_as_longlong(oc);
+          pub_s[8] = (uint32_t)r, pub_s[9] = (uint32_t)(ob & 0xffffffffull), pub_s[10] = (uint32_t)(ob >> 32);
+          pub_s[11] = 0;
+        }
+      }
+#else
       if (top_last) {
         M3S_TSTAMP(3)
         u32x4 g[kTrkShards];
@@ -6429,6 +6502,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
           pub_s[3 * lane] = g.x, pub_s[3 * lane + 1] = g.y, pub_s[3 * lane + 2] = g.z;
         }
       }
+#endif
     }
     M3S_TSTAMP(5)
     __syncthreads();

@@ -122,14 +122,16 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 // rows (n + 1 <= 16 kTailMaxT) and its scratch (dense bordered tail, L tiles,
 // W_k); see the kernel
 constexpr int kTailMaxT = 32;
-inline size_t tail_gran_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y', LgT, then the granules
+inline size_t tail_z_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y', LgT, Z, then the granules
   const size_t nmax = 16 * kTailMaxT;
   return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2 + (size_t)kTailMaxT * 256 + nmax;
 }
+inline size_t tail_gran_offset_doubles() {  // + the tiles of Z = L^-1 (tail_zinv_col, round 5)
+  return tail_z_offset_doubles() + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256;
+}
 inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cyc_kernel)
-  const size_t nmax = 16 * kTailMaxT;
   // + the tagged-granule copy of the L tiles (tail_cyc_kernel hand-offs, 16 B per entry)
-  return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 4 + (size_t)kTailMaxT * 256 + nmax;
+  return tail_gran_offset_doubles() + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2;
 }
 
 struct Layout {
@@ -3646,6 +3648,8 @@ struct TailSync {
   double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout, [tile][2][64 lanes][2] (back-substitution A operands)
   double *LgG;     // the L tiles as tagged granules, [tile][4][64 lanes] x {double, epoch tag, 0} (16 B; zeroed per call)
   int warm;        // 1: warm the diagonal factor's code on a dummy tile first (tail_diag_warm)
+  int zinv;        // 1: back-substitution through Z = L^-1, a column per workgroup (tail_zinv_col, round 5)
+  double *Zg;      // the tiles of Z, [tile (I, J)][64 lanes][4] (MFMA C layout)
 };
 constexpr size_t kTailGranBytes = (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 64 * 4 * 16;
 
@@ -3857,6 +3861,90 @@ __device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSyn
   if (tid == 0) M3S_CSTAMP(2, 511, 0);
 }
 
+// Round 5: the back-substitution without its chain. x = L^-T y' is Z^T y'
+// with Z = L^-1, and column J of Z needs only the factor:
+//   Z(J, J) = W_J,   Z(I, J) = -W_I sum_{K = J..I-1} L(I, K) Z(K, J)  (I > J),
+// a recursion down the rows that trails the factorisation by one tile
+// column (row I waits for column I's flag: W_I and the L(I, K) granules).
+// Every column runs on its own wave as soon as its workgroup's factor work
+// is done, so x_J = sum_I Z(I, J)^T y'_I follows the last column's flag after
+// a few MFMAs, where tail_backsub_wg ran a 1-2 us step per tile column after
+// it (~26 us at 256 KFs). The fp64 sums differ from the substitution's (the
+// explicit inverse of the triangular factor): dx agrees to fp64 round-off.
+// MEASURED SLOWER, test build only (knob tail_zinv): 256-KF calib 0.764 ->
+// 0.842 ms per 3-iteration call, 128 KFs 0.508 -> 0.514
+// (profiles/r05/solve_ab_zinv_REJECTED.txt). Column J's chain loads the
+// granule tiles L(I, J..I-1) of every row below it, one wave per column:
+// O(TC^3 / 6) tile reads (~1140 at 19 tiles against 171 distinct tiles), so
+// the early columns' chains fall behind the factor and the launch ends on
+// them instead of on the substitution it replaced.
+// L(I, K) as the A operand is its granule tile (the C layout of L^T); Z(K, J)
+// as the B operand is its C layout (register q = rows 4q..); -W_I as the A
+// operand is Wg's W^T read by (column, row); Z tiles live in global scratch
+// (each lane re-reads its own stores: per-thread order, no hand-off).
+__device__ __forceinline__ void tail_zinv_col(const TailArgs &A, const TailSync &S, int J, const double (*Wk)[17],
+                                              int lane) {
+  const int n = 7 * A.nc, TC = (n + 15) / 16;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int want = S.epoch + 1;
+  const __amdgpu_buffer_rsrc_t R = gran_rsrc(S.LgG);
+  f64x4 *Z = reinterpret_cast<f64x4 *>(S.Zg);
+  f64x4 z;
+#pragma unroll
+  for (int r = 0; r < 4; r++) z[r] = Wk[lk + 4 * r][lr];  // Z(J, J) = W_J
+  Z[tail_tile(J, J) * 64 + lane] = z;
+  bool ok = true;
+  for (int I = J + 1; I < TC && ok; I++) {
+    {  // column I's flag: W_I, y'_I and the L(I', I) granules are out
+      int spins = 0;
+      while (__hip_atomic_load(S.tflag + I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kColSpins) {
+          ok = false;
+          break;
+        }
+      }
+    }
+    // the W_I operands first (their latency behind the sum)
+    double wa[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) wa[q] = -ld_sc1(A.Wg + (size_t)I * 256 + 16 * (4 * q + lk) + lr);
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int K = J; K < I; K++) {
+      GranTile g;
+      gran_load(R, tail_tile(I, K), lane, g);  // final: tag want (column K's flag was seen)
+      const f64x4 a = gran_val(g);
+      const f64x4 zk = K == I - 1 ? z : Z[tail_tile(K, J) * 64 + lane];
+      f64x4 &acc = (K - J) & 1 ? acc1 : acc0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], zk[q], acc, 0, 0, 0);
+    }
+    const f64x4 sm = acc0 + acc1;
+    f64x4 zn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) zn = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], sm[q], zn, 0, 0, 0);
+    z = zn;
+    Z[tail_tile(I, J) * 64 + lane] = z;
+  }
+  if (!ok) {
+    if (lane == 0) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // x_J = sum_I Z(I, J)^T y'_I over the real rows (every column flag was seen)
+  double part = 0.0;
+  for (int I = J; I < TC; I++) {
+    const f64x4 zi = I == TC - 1 ? z : Z[tail_tile(I, J) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = 16 * I + lk + 4 * r;
+      part += row < n ? zi[r] * ld_sc1(S.ypg + row) : 0.0;
+    }
+  }
+  part += __shfl_xor(part, 16);
+  part += __shfl_xor(part, 32);
+  if (lane < 16 && 16 * J + lane < n) A.rhs[7 * A.c0 + 16 * J + lane] = part;
+}
+
 // Round 2: the L tiles go from workgroup to workgroup as tagged granules
 // (one hop = one store + one polled load), the panel follows the updates
 // without a workgroup barrier (waves 1..3 wait for W_J on an LDS flag), and
@@ -4035,6 +4123,10 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     if (fail_s) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.tflag + J, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     M3S_CSTAMP(2, J, 3);
+  }
+  if (S.zinv) {
+    if (wave == 0) tail_zinv_col(A, S, J, Wk, lane);
+    return;
   }
   if (J != TC - 1) return;
   tail_backsub_wg(A, S, yv, xv);
@@ -4229,6 +4321,9 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&wready[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (tid == 0) M3S_CSTAMP(2, J1, 2);
+      // the pair's own sub-diagonal tile as granules too: no other workgroup's
+      // factor reads it, but the Z recursion of column J0 does (tail_zinv_col)
+      if (S.zinv) gran_store(R, tail_tile(J1, J0), lane, d, want);
     }
     // W^T of each column ([16][16] row-major: element e = 16 l + r holds
     // W[r][l]): four stores of 64 consecutive elements, whole lines each
@@ -4375,6 +4470,10 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     if (fail_s) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int j = 0; j < jn; j++) __hip_atomic_store(S.tflag + J0 + j, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int j = 0; j < jn; j++) M3S_CSTAMP(2, J0 + j, 3);
+  }
+  if (S.zinv) {  // the pair's columns on waves 0 and 1
+    if (wave < jn) tail_zinv_col(A, S, J0 + wave, Wk[wave], lane);
+    return;
   }
   if ((int)blockIdx.x != (int)gridDim.x - 1) return;
   tail_backsub_wg(A, S, yv, xv);
@@ -4879,6 +4978,7 @@ struct Knobs {
   std::atomic<int> subtree{0};         // 1: the subtree kernels (one LDS workgroup per subtree; measured slower)
   std::atomic<int> tail_pair{1};       // 0: tail_cyc_kernel (one tile column per workgroup)
   std::atomic<int> tail_warm{1};       // 0: no warm-up of the tail's diagonal factor code
+  std::atomic<int> tail_zinv{0};       // 1: the tail's back-substitution through Z = L^-1 (round 5; measured slower)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -4898,6 +4998,7 @@ struct Knobs {
     env("M3S_SUBTREE", subtree);
     env("M3S_TAIL_PAIR", tail_pair);
     env("M3S_TAIL_WARM", tail_warm);
+    env("M3S_TAIL_ZINV", tail_zinv);
 #endif
   }
 };
@@ -4917,6 +5018,7 @@ bool gather_lds_path() { return knobs().gather_lds != 0; }
 inline bool subtree_path() { return knobs().subtree != 0; }
 inline bool tail_pair_path() { return knobs().tail_pair != 0; }
 inline bool tail_warm_knob() { return knobs().tail_warm != 0; }
+inline bool tail_zinv_knob() { return knobs().tail_zinv != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -4929,6 +5031,7 @@ bool gather_lds_path() { return true; }
 constexpr bool subtree_path() { return false; }
 constexpr bool tail_pair_path() { return true; }
 constexpr bool tail_warm_knob() { return true; }
+constexpr bool tail_zinv_knob() { return false; }  // (measured slower, tail_zinv_col)
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -5347,6 +5450,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.LgT = Y.ypg + 16 * kTailMaxT;
           Y.LgG = tail + tail_gran_offset_doubles();
           Y.warm = tail_warm_knob() ? 1 : 0;
+          Y.zinv = tail_zinv_knob() ? 1 : 0;
+          Y.Zg = tail + tail_z_offset_doubles();
           const int TC = (7 * meta.nc + 15) / 16;
           if (tail_pair_path())
             if (((7 * meta.nc + 16) / 16 + 2) / 3 <= 7)  // tile rows TR: rows per wave of waves 1..3
@@ -6806,7 +6911,7 @@ int m3s_set_knob(const char *name, int value) {
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
              {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
-             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}
+             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}
 #endif
   };
   for (const auto &t : tab)

@@ -228,8 +228,10 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
 #ifndef M3S_REF_XCD
 #define M3S_REF_XCD 1
 #endif
-#ifndef M3S_REF_PF
-#define M3S_REF_PF 1
+// M3S_REF_ROWS: candidates in image-row order (measured 153 -> 136 us per
+// 512 x 512 pair, profiles/r05/refine_ab_rows.txt)
+#ifndef M3S_REF_ROWS
+#define M3S_REF_ROWS 1
 #endif
 typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
 constexpr int kRefFar = 0x7ffffff0;  // past any descriptor image (< 2^31 B): loads return zeros
@@ -305,14 +307,19 @@ __global__ void __launch_bounds__(kMatchThreads) refine_f16_kernel(m3s_refine_ar
     // unsigned: a centre far outside wraps (every candidate is then masked)
     const unsigned o0 = (unsigned)base + ((unsigned)vb * (unsigned)W + (unsigned)ub) * (unsigned)F2;
     const unsigned du = (unsigned)(d * F2), dv = (unsigned)d * (unsigned)W * (unsigned)F2;
-    unsigned oi = o0, oij = o0;  // offset of (i, 0) and of the last candidate formed
-    auto load = [&](int c, u32x4m (&x)[NL]) {  // c in order; c >= NN: the pair's dummy (zeros)
-      const int i = c / N1, j = c % N1;
-      if (c > 0 && c < NN) {
-        if (j == 0) oi += du, oij = oi;
-        else oij += dv;
+    unsigned oi = o0, oij = o0;  // offset of the line start and of the last candidate formed
+    // processing position p -> candidate (i, j): scan order (i outer) or, with
+    // M3S_REF_ROWS, image rows (j outer: consecutive candidates of a wave are
+    // the same row shifted by d pixels, so their lines are still in L1)
+    auto cand_i = [](int p) { return M3S_REF_ROWS ? p % N1 : p / N1; };
+    auto cand_j = [](int p) { return M3S_REF_ROWS ? p / N1 : p % N1; };
+    auto load = [&](int p, u32x4m (&x)[NL]) {  // p in order; p >= NN: the pair's dummy (zeros)
+      const int i = cand_i(p), j = cand_j(p);
+      if (p > 0 && p < NN) {
+        if (p % N1 == 0) oi += M3S_REF_ROWS ? dv : du, oij = oi;
+        else oij += M3S_REF_ROWS ? du : dv;
       }
-      const unsigned ok = c < NN ? (uok >> i) & (vok >> j) & 1u : 0u;
+      const unsigned ok = p < NN ? (uok >> i) & (vok >> j) & 1u : 0u;
       const int o = ok ? (int)oij : kRefFar;
 #pragma unroll
       for (int l = 0; l < NL; l++) x[l] = __builtin_amdgcn_raw_buffer_load_b128(R, o + 16 * l, 0, 0);
@@ -331,12 +338,16 @@ __global__ void __launch_bounds__(kMatchThreads) refine_f16_kernel(m3s_refine_ar
       }
       _Float16 sa, sb;
       score2_f16<NL>(q, x[s][0], x[s][1], sa, sb);
-      const bool wa = sa > max_score;  // scan order: c before c + 1
+      // scan index of the two (the reference's order: u offset outer); in row
+      // order a tie keeps the smaller scan index, as the reference's first
+      // maximum (a score equal to the initial minimum never wins)
+      const int ca = cand_i(c) * N1 + cand_j(c), cb = cand_i(c + 1) * N1 + cand_j(c + 1);
+      const bool wa = sa > max_score || (M3S_REF_ROWS && sa == max_score && best >= 0 && ca < best);
       max_score = wa ? sa : max_score;
-      best = wa ? c : best;
-      const bool wb = sb > max_score;
+      best = wa ? ca : best;
+      const bool wb = sb > max_score || (M3S_REF_ROWS && sb == max_score && best >= 0 && cb < best);
       max_score = wb ? sb : max_score;
-      best = wb ? c + 1 : best;
+      best = wb ? cb : best;
       __builtin_amdgcn_sched_barrier(0);  // one pair in flight: no loads hoisted further up
     }
     if (best >= 0) {

@@ -677,3 +677,30 @@ def test_tail_warmup_leaves_factor_bitwise(test_lib, be, N, knobs):
     assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
     np.testing.assert_array_equal(dx_a, dx_b)
     np.testing.assert_array_equal(T_a, T_b)
+
+
+@pytest.mark.parametrize("N", [128, 140, 256, 400])
+def test_tail_zinv_matches_substitution(test_lib, be, N, knobs):
+    """Round 5: the dense tail's back-substitution through Z = L^-1, one
+    column per wave as the factor's column flags land (tail_zinv_col, test
+    knob tail_zinv=1; measured slower, kept as a checked A/B path), against
+    the substitution over the tile columns after the last one
+    (tail_backsub_wg, the default): the same factor, a different fp64
+    summation order, so dx agrees to fp64 round-off seen through the fp32
+    output (as the one-workgroup tail above); bitwise run to run; odd and
+    even tile counts."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 12, 16, seed=870 + N)
+    knobs("tail_zinv", "1")
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    knobs("tail_zinv", "0")
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
+    np.testing.assert_allclose(dx_a, dx_b, rtol=0, atol=1e-6 * np.abs(dx_b).max() + 1e-9)
+    np.testing.assert_allclose(T_a, T_b, rtol=0, atol=1e-6)
+    knobs("tail_zinv", "1")
+    T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
+    np.testing.assert_array_equal(dx_a, dx_a2)
+    np.testing.assert_array_equal(T_a, T_a2)

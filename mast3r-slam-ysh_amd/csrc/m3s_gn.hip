@@ -129,6 +129,7 @@ inline size_t tail_z_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y'
 inline size_t tail_gran_offset_doubles() {  // + the tiles of Z = L^-1 (tail_zinv_col, round 5)
   return tail_z_offset_doubles() + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256;
 }
+constexpr int kGNx = 16 * kTailMaxT + 8;  // columns of X_k: a_k and one per tail dof (gcol_worker), padded
 inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cyc_kernel)
   // + the tagged-granule copy of the L tiles (tail_cyc_kernel hand-offs, 16 B per entry)
   return tail_gran_offset_doubles() + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2;
@@ -136,7 +137,7 @@ inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cy
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      colsync, wgran, tail, eorder, planes, total;
+      colsync, wgran, tail, gx, eorder, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -189,12 +190,15 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 7 * (size_t)(m + 1), 256);
   L.parts = off;  // split update partials, at most slot_cap of them
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
-  L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap] (epoch-tagged, zeroed per call)
-  off = align_up(off + sizeof(int32_t) * (size_t)(2 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
+  L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap], tail flags,
+                    // X_k chunk counters [m+1] (epoch-tagged, zeroed per call)
+  off = align_up(off + sizeof(int32_t) * (size_t)(3 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
   L.wgran = off;  // df_factor_kernel: W_k of every column as 16-B tagged granules (zeroed with colsync per call)
   off = align_up(off + (size_t)16 * 49 * (size_t)(m + 1), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
   off = align_up(off + sizeof(double) * tail_scratch_doubles(), 256);
+  L.gx = off;  // the sparse columns' X_k = [a_k | B_k] (gcol_worker), [m][7][kGNx]
+  off = align_up(off + sizeof(double) * 7 * kGNx * (size_t)(m + 1), 256);
   // target-side planes of every edge (4 planes = rays / points, the widest modes)
   L.planes = off;
   off = align_up(off + sizeof(float) * 4 * (size_t)E * (size_t)HW, 256);
@@ -1619,6 +1623,9 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_LOOKAHEAD  // DIAG(k+1) inside step k's trailing update (dense tail)
 #define M3S_TAIL_LOOKAHEAD 1
 #endif
+#ifndef M3S_BS_SYNC  // sparse_llt_kernel: level-synchronous back-substitution (round 5; 0 = dataflow)
+#define M3S_BS_SYNC 1
+#endif
 
 // Cross-workgroup hand-off of doubles (column-task kernels): write-through
 // (sc1) stores drained before the flag, sc1 loads (L2 / fabric served, never a
@@ -1995,10 +2002,15 @@ __device__ __forceinline__ void fwd_solve_store(double bb, const double (&wcol)[
 // lower triangle): the updates from the sparse columns p < c0, and for a
 // diagonal block also the tail RHS. Tasks are independent (used in
 // sparse_llt_kernel and, spread over the chip, by border_kernel).
+// wflag (df_factor_kernel, round 5): the update blocks are waited for batch by
+// batch as sub_products loads them (slot flags == want), so the products of
+// the early sparse columns run while the late ones are still being factored;
+// y_p of a block L_kp is final once that block is (DIAG(p) precedes OFF(k, p))
 template <bool STAGE, bool SC1 = false>
 __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t *pl, const int *off, double *Lb,
                                             double *y, int r7, int c7, int lane49, int lane, int lane7, bool act49,
-                                            double *stg, double *Ad = nullptr, int ld = 0) {
+                                            double *stg, double *Ad = nullptr, int ld = 0,
+                                            const int32_t *wflag = nullptr, int want = 0, bool *ok = nullptr) {
   const int32_t *dtr_ptr = pl + off[6], *dtr_slot = pl + off[7], *dtr_p = pl + off[8], *task_dst = pl + off[10],
                 *task_tr_ptr = pl + off[12], *tr_a = pl + off[13], *tr_b = pl + off[14];
   const int32_t *clq = pl + off[28];
@@ -2009,7 +2021,7 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
   if (ri == ci) {
     const int q0 = dtr_ptr[k], q1 = bend[ci * nc + ci];
     double v = Lb[(size_t)k * 49 + lane49];
-    v = sub_products<STAGE, true, SC1>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg);
+    v = sub_products<STAGE, true, SC1>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg, wflag, want, ok);
     double bb = y[k * 7 + lane7];
     bb = sub_matvec<STAGE, false, SC1>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
     if (act49) Lb[(size_t)k * 49 + lane] = v;
@@ -2019,7 +2031,7 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
     const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
     const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
     double v = Lb[(size_t)dst * 49 + lane49];
-    v = sub_products<STAGE, false, SC1>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg);
+    v = sub_products<STAGE, false, SC1>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg, wflag, want, ok);
     if (act49) Lb[(size_t)dst * 49 + lane] = v;
     if (Ad && act49) {  // the block and its transpose (tail_llt_kernel reads whole 16x16 tiles)
       Ad[(size_t)(7 * ri + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
@@ -2461,11 +2473,37 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   Sim3f T_pre;
   if (tid < m) T_pre = load_sim3(D.Twc + 8 * (size_t)(tid + 1));
 
-  // 2. back-substitution L^T x = y in reverse level order (x overwrites y),
+  // 2. back-substitution L^T x = y in reverse level order (x overwrites y).
+#if M3S_BS_SYNC
+  // Level-synchronous (round 5): the columns of one elimination-tree level
+  // run side by side on the waves, a workgroup barrier between levels (every
+  // row of struct(k) is an ancestor, at a higher level). The per-column sums
+  // are the dataflow's (sub_matvec in list order): bitwise the same x. The
+  // dataflow form paid a flag poll (s_sleep granularity), a release fence and
+  // an LDS ticket per column on the chain: ~2k cycles per level at C3.
+  {
+    const int32_t *lev_ptr = pl + D.off[4];
+    for (int L = D.levels - 1; L >= 0; L--) {
+      for (int c = lev_ptr[L] + wave; c < lev_ptr[L + 1]; c += NW) {
+        const int k = lev_col[c];
+        if (k >= m - D.nc) continue;  // dense tail: done above
+        double rr = y[k * 7 + lane7];
+        rr = sub_matvec<STAGE, true>(rr, Lb, col_slot, col_row, col_ptr[k], col_ptr[k + 1], y, lane7, lane49, lane, stg);
+        double xk = 0.0;
+#pragma unroll
+        for (int mm = 0; mm < 7; mm++) xk += Di[(size_t)k * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
+        if (lane < 7) y[k * 7 + lane] = xk;
+      }
+      __syncthreads();
+    }
+  }
+  for (; false;) {
+#else
   // dataflow: column k waits for x_i of every i in struct(k)
   // columns are taken dynamically in reverse level order; the x_i terms are
   // applied as they arrive (lane-parallel flag polling, list order)
   for (;;) {
+#endif
     const int t = wave_ticket(&next_col);
     if (t >= m) break;
     const int k = lev_col[m - 1 - t];
@@ -2568,9 +2606,17 @@ __device__ __forceinline__ void set_fail(int32_t *flags) {
   __hip_atomic_store(flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// whole-wave global ticket: every lane adds 1 (folded into one add of 64)
+// wave-uniform global ticket: the first active lane adds 64 and its old value
+// / 64 is the ticket. Explicit rather than "every lane adds 1": that form is
+// one add of 64 only when the atomic optimizer folds it, which needs the
+// counter's address provably uniform; a pointer loaded through a reference in
+// a non-inlined function (gcol_worker, round 5) got 64 per-lane adds
+// interleaved with other waves' and duplicate tickets.
 __device__ __forceinline__ int wave_gticket(int32_t *ctr) {
-  const int o = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  int o = 0;
+  if (lane == __builtin_ctzll(ex)) o = __hip_atomic_fetch_add(ctr, 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return __builtin_amdgcn_readfirstlane(o) >> 6;
 }
 
@@ -2808,23 +2854,16 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + dst, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (lane == 0) M3S_CSTAMP(3, dst, 3);
-    } else {  // BORDER(b): waits for its update prefix, then border_task (sc1 reads)
+    } else {  // BORDER(b): border_task over its update prefix (sc1 reads)
       const int bt = code - D.n_tasks, nc = D.nc;
-      const int32_t *ct0 = clq + 2, *bend = clq + 2 + nc;
-      int ci = 0, rem = bt;
-      while (rem >= nc - ci) rem -= nc - ci, ci++;
-      const int ri = ci + rem, k = D.c0 + ci;
-      bool ok;
-      if (ri == ci) {
-        ok = wait_flags(D.sdone, dtr_slot, dtr_ptr[k], bend[ci * nc + ci], BIG, want, lane);
-      } else {
-        const int task = ct0[ci] + ri - ci - 1;
-        const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
-        ok = wait_flags(D.sdone, tr_a, q0, q1, BIG, want, lane) && wait_flags(D.sdone, tr_b, q0, q1, BIG, want, lane);
-      }
-      if (!ok && lane == 0) set_fail(D.flags);
+      // the blocks of the update list waited for batch by batch, as they are
+      // loaded (round 5: waiting for the whole list first put every product
+      // of the tail border behind the last sparse level: ~20 us of the launch
+      // at 256 KFs after the last column was published)
+      bool ok = true;
       border_task<true, true>(bt, nc, D.c0, pl, D.off, L, D.y, r7, c7, lane49, lane, lane7, act49, stg, D.tail_A,
-                              D.tail_ld);
+                              D.tail_ld, D.sdone, want, &ok);
+      if (!ok && lane == 0) set_fail(D.flags);
     }
   }
 }
@@ -3070,14 +3109,31 @@ __device__ void col_finish(const ColArgs &C, int lane) {
     }
     return;
   }
+  // every x_k was published before this workgroup's ticket and the caller's
+  // agent-scope acquire: plain loads, all in flight at once (one relaxed
+  // atomic load per entry was one dependent fabric round trip each: ~28 per
+  // lane at 256 KFs, ~10 us of the kernel, round 5)
   float part = 0.0f;
-  for (int idx = lane; idx < 7 * m; idx += 64) {
-    const int vn = idx / 7, q = idx - 7 * vn;
-    const int vo = perm[vn];
-    const float v = -(float)ld_sc1(C.y + idx);
-    C.dx_out[vo * 7 + q] = v;
-    dxs[vo * 7 + q] = v;
-    part += v * v;
+  constexpr int kFinB = 8;
+  for (int i0 = 0; i0 < 7 * m; i0 += 64 * kFinB) {
+    double xv[kFinB];
+#pragma unroll
+    for (int u = 0; u < kFinB; u++) {
+      const int idx = i0 + 64 * u + lane;
+      xv[u] = idx < 7 * m ? C.y[idx] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kFinB; u++) {
+      const int idx = i0 + 64 * u + lane;
+      if (idx < 7 * m) {
+        const int vn = idx / 7, q = idx - 7 * vn;
+        const int vo = perm[vn];
+        const float v = -(float)xv[u];
+        C.dx_out[vo * 7 + q] = v;
+        dxs[vo * 7 + q] = v;
+        part += v * v;
+      }
+    }
   }
   part = wave_sum(part);
   wave_lds_fence();
@@ -4145,9 +4201,214 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
 // factor; the back-substitution is the same code (tail_backsub_wg).
 // RC: row tiles per wave (waves 1..3 hold rows J1 + w + 3 u, u < RC): 7 up to
 // 23 tile rows (the register arrays of 11 spill), 11 up to kTailMaxT
+// ------------------------------------------------------------------------
+// Round 5: the sparse back-substitution off the critical path. The sparse
+// columns' x is affine in the tail's: x_s = L_ss^-T (y_s - L_ts^T x_t), so
+// for every sparse column k
+//   X_k = [a_k | B_k] = W_k^T (R_k - sum_{i sparse in struct(k)} L_ik^T X_i),
+//   R_k = [y_k | 0] - sum_{i tail in struct(k)} L_ik^T [0 | E_i]
+// (E_i picks x_i out of x_t), and x_k = a_k + B_k x_t. The X_k recursion
+// needs only the factor, so extra workgroups of the dense tail's launch run
+// it (column tasks in reverse level order, the X_i of the sparse ancestors
+// by epoch flags) while the tail factors on its own workgroups; once the
+// tail's x_t is out, x_k = a_k + B_k x_t is one short dot product per entry
+// and col_backsub_kernel's chain of dependent hand-offs (9 levels, ~27 us,
+// plus its launch at 256 KFs) leaves the critical path. x_k differs from the
+// substitution by fp64 round-off (a different summation order).
+struct GArgs {
+  double *X;     // [m][7][nx] row-major per column (nx = 1 + 7 nc, padded)
+  int nx, n_pairs;
+  int32_t *task, *comb, *fin, *xt_ready;  // ticket / ticket / counter / flag words (colsync; zeroed per call)
+  int32_t *cnt;                           // [m] chunks of X_k done (colsync; zeroed per call)
+};
+constexpr int kGBat = 8;    // sparse ancestors' X_i loads in flight per lane
+constexpr int kGCapS = 24;  // sparse ancestors' L_ik staged in LDS per wave (the rest read from global)
+constexpr int kGMaxS = 512; // sparse ancestors of one column: < m <= 512 on the chip-wide path
+constexpr int kGTmap = kTailMaxT * 16 / 7 + 8;
+#ifndef M3S_GSLEEP
+#define M3S_GSLEEP 8
+#endif
+__device__ __forceinline__ bool g_poll(const int32_t *flag, int want) {  // bounded wait for one epoch flag
+  for (int spins = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want; spins++) {
+    if (spins > kColSpins) return false;
+    __builtin_amdgcn_s_sleep(M3S_GSLEEP);
+  }
+  return true;
+}
+// wait_flags with the workers' poll interval (they wait beside the tail's hand-offs)
+__device__ __forceinline__ bool g_wait_flags(const int32_t *flag, const int32_t *idx, int q0, int q1, int lim, int want,
+                                             int lane) {
+  int spins = 0;
+  for (int qb = q0; qb < q1; qb += 64) {
+    const int q = qb + lane;
+    const int i = q < q1 ? idx[q] : -1;
+    for (;;) {
+      const bool ok = i < 0 || i >= lim ||
+                      __hip_atomic_load(flag + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want;
+      if (__ballot(!ok) == 0) break;
+      __builtin_amdgcn_s_sleep(M3S_GSLEEP);
+      if (++spins > kColSpins) return false;
+    }
+  }
+  return true;
+}
+// Per wave, task (k, ch): the 64 columns c = 64 ch + lane of X_k (a column of
+// ~300 c at 256 KFs is ~170 KB of X_i reads: one CU's fabric bandwidth made a
+// whole-column task ~10 us, so a column is spread over S = nx / 64 waves on
+// as many CUs); the last of its S chunks to finish (per-column counter
+// G.cnt, epoch-based) publishes done2[k].
+__device__ void gcol_worker(const ColArgs &C, const GArgs &G) {
+  __shared__ double Lw[kTailNW][kGCapS * 49], Ww[kTailNW][49];
+  __shared__ int tmapw[kTailNW][kGTmap];  // tail block (i - c0) -> its position q in struct(k), or -1
+  __shared__ int sqw[kTailNW][kGMaxS];    // the sparse ancestors' positions q in struct(k), list order
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t *pl = C.plan;
+  const int32_t *col_ptr = pl + C.off[1], *col_row = pl + C.off[2], *col_slot = pl + C.off[3],
+                *corder = pl + C.off[29];
+  const int want = C.epoch + 1, c0 = C.c0, nct = C.m - c0, nx = G.nx, nt = 7 * nct;
+  const int nG = (int)gridDim.x - G.n_pairs;
+  const int S = (nx + 63) / 64;
+  double *Lk = Lw[wave], *Wk = Ww[wave];
+  int *tmap = tmapw[wave], *sq = sqw[wave];
+  // 1. the X_k recursion, column chunks in reverse level order
+  const int base = C.epoch * (C.ncols * S + kTailNW * nG);
+  for (;;) {
+    const int t = wave_gticket(G.task) - base;
+    if (t >= C.ncols * S) break;
+    const int ci = t / S, ch = t - S * ci;
+    const int k = corder[C.ncols - 1 - ci];
+    const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
+    if (lane == 0 && ch == 0) M3S_CSTAMP(1, k, 0);
+    for (int q = lane; q < nct; q += 64) tmap[q] = -1;
+    wave_lds_fence();
+    int ns = 0;
+    for (int qb = q0; qb < q1; qb += 64) {  // tail positions; sparse ancestors compacted in list order
+      const int q = qb + lane;
+      const int i = q < q1 ? col_row[q] : c0;
+      if (q < q1 && i >= c0) tmap[i - c0] = q - q0;
+      const uint64_t sm = __ballot(q < q1 && i < c0);
+      const int pos = ns + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+      if (q < q1 && i < c0 && pos < kGMaxS) sq[pos] = q - q0;
+      ns += __popcll(sm);
+    }
+    ns = min(ns, kGMaxS);
+    wave_lds_fence();
+    // the factor is final (earlier launches): the ancestors' L_ik and W_k by plain loads
+    for (int e = lane; e < 49 * min(ns, kGCapS); e += 64) Lk[e] = C.L[(size_t)col_slot[q0 + sq[e / 49]] * 49 + e % 49];
+    if (lane < 49) Wk[lane] = C.Dinv[(size_t)k * 49 + lane];
+    const int c = 64 * ch + lane;
+    const bool cv = c < nx;
+    double r[7];
+    {  // R_k: [y_k | 0] minus, for the tail block i holding dof j = c - 1, row j of L_ik^T
+      const int j = c - 1;
+      const int q = c > 0 && j < nt ? tmap[j / 7] : -1;
+      const double *Lq = C.L + (size_t)col_slot[q0 + (q >= 0 ? q : 0)] * 49 + (j % 7) * 7;
+#pragma unroll
+      for (int a = 0; a < 7; a++) r[a] = (c == 0 ? C.y[(size_t)k * 7 + a] : 0.0) - (q >= 0 ? Lq[a] : 0.0);
+    }
+    if (!g_wait_flags(C.done2, col_row, q0, q1, c0, want, lane) && lane == 0) set_fail(C.flags);  // sparse ancestors' X_i
+    wave_lds_fence();
+    if (lane == 0 && ch == 0) M3S_CSTAMP(1, k, 1);
+    const int cl = cv ? c : 0;
+    for (int u0 = 0; u0 < ns; u0 += kGBat) {  // - L_ik^T X_i, ancestors in list order
+      double xi[kGBat][7];
+#pragma unroll
+      for (int v = 0; v < kGBat; v++) {
+        const double *Xi = G.X + (size_t)col_row[q0 + sq[min(u0 + v, ns - 1)]] * 7 * nx + cl;
+#pragma unroll
+        for (int b = 0; b < 7; b++) xi[v][b] = ld_sc1(Xi + (size_t)b * nx);
+      }
+#pragma unroll
+      for (int v = 0; v < kGBat; v++) {
+        const int u = u0 + v;
+        if (u >= ns) break;
+        const double *Lq = u < kGCapS ? Lk + 49 * u : C.L + (size_t)col_slot[q0 + sq[u]] * 49;
+#pragma unroll
+        for (int a = 0; a < 7; a++) {
+          double sm = 0.0;
+#pragma unroll
+          for (int b = 0; b < 7; b++) sm += Lq[b * 7 + a] * xi[v][b];
+          r[a] -= sm;
+        }
+      }
+    }
+    double *Xk = G.X + (size_t)k * 7 * nx;
+    if (cv) {
+#pragma unroll
+      for (int a = 0; a < 7; a++) {  // X_k = W_k^T r
+        double x = 0.0;
+#pragma unroll
+        for (int b = 0; b < 7; b++) x += Wk[b * 7 + a] * r[b];
+        st_sc1(Xk + (size_t)a * nx + c, x);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's X_k stores have left
+    if (lane == 0) {
+      const int o = __hip_atomic_fetch_add(G.cnt + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (o == want * S - 1) {  // the column's last chunk
+        __hip_atomic_store(C.done2 + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        M3S_CSTAMP(1, k, 2);
+      }
+    }
+    wave_lds_fence();  // before the next task rewrites this wave's LDS
+  }
+  // 2. x_k = a_k + B_k x_t: one column per wave over every worker wave; B_k
+  // is in registers (ready once X_k is) before the tail's x_t is out, so
+  // after its flag only x_t is read (one round trip) and summed
+  const int cbase = C.epoch * (C.ncols + kTailNW * nG);
+  constexpr int kCU = 16 * kTailMaxT / 64;  // tail dofs per lane (nt < 16 kTailMaxT)
+  for (;;) {
+    const int t = wave_gticket(G.comb) - cbase;
+    if (t >= C.ncols) break;
+    const int k = corder[C.ncols - 1 - t];  // root side first: those X_k are out first
+    const double *Xk = G.X + (size_t)k * 7 * nx;
+    if (lane == 0 && !g_poll(C.done2 + k, want)) set_fail(C.flags);  // X_k of another workgroup
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double bx[kCU][7];
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const int j = lane + 64 * u;
+#pragma unroll
+      for (int a = 0; a < 7; a++) bx[u][a] = j < nt ? ld_sc1(Xk + (size_t)a * nx + 1 + j) : 0.0;
+    }
+    const double a0 = ld_sc1(Xk + (size_t)(lane < 7 ? lane : 0) * nx);
+    if (lane == 0 && !g_poll(G.xt_ready, want)) set_fail(C.flags);  // the tail's x_t
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double acc[7];
+#pragma unroll
+    for (int a = 0; a < 7; a++) acc[a] = 0.0;
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const int j = lane + 64 * u;
+      const double xt = j < nt ? ld_sc1(C.y + (size_t)7 * c0 + j) : 0.0;
+#pragma unroll
+      for (int a = 0; a < 7; a++) acc[a] += bx[u][a] * xt;
+    }
+#pragma unroll
+    for (int a = 0; a < 7; a++) acc[a] = wave_sum(acc[a]);
+    if (lane < 7) {
+      double v = 0.0;
+#pragma unroll
+      for (int a = 0; a < 7; a++) v = lane == a ? acc[a] : v;
+      st_sc1(C.y + (size_t)k * 7 + lane, a0 + v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x_k (and any failure flag) out before the ticket
+    if (lane == 0) M3S_CSTAMP(1, k, 3);
+    const int f = wave_gticket(G.fin);  // the wave that combines the last column finishes the step
+    if (f - C.epoch * C.ncols == C.ncols - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      col_finish(C, lane);
+    }
+  }
+}
+
 template <int RC>
-__global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, TailSync S) {
+__global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, TailSync S, ColArgs C, GArgs G) {
   if (A.flags[kFlagStop]) return;
+  if (G.X && (int)blockIdx.x >= G.n_pairs) {  // the sparse back-substitution's workers
+    gcol_worker(C, G);
+    return;
+  }
   __shared__ double Wk[2][16][17];
   __shared__ double yv[16 * kTailMaxT], xv[16 * kTailMaxT];
   __shared__ f64x4 Lsub[64];  // L(J1, J0) in operand order (waves 1..3 update their J1 tiles with it)
@@ -4467,7 +4728,10 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave has left
   __syncthreads();
   if (tid == 0) {
-    if (fail_s) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fail_s) {  // out before the column flags (the back-substitution workers may finish the step early)
+      __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     for (int j = 0; j < jn; j++) __hip_atomic_store(S.tflag + J0 + j, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int j = 0; j < jn; j++) M3S_CSTAMP(2, J0 + j, 3);
   }
@@ -4475,8 +4739,17 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     if (wave < jn) tail_zinv_col(A, S, J0 + wave, Wk[wave], lane);
     return;
   }
-  if ((int)blockIdx.x != (int)gridDim.x - 1) return;
+  if ((int)blockIdx.x != (G.X ? G.n_pairs : (int)gridDim.x) - 1) return;
   tail_backsub_wg(A, S, yv, xv);
+  if (G.X) {  // x_t is out (plain stores): release, then the workers combine
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(G.xt_ready, S.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 #ifdef M3S_TEST_PATHS  // reached only through the dense knob: every graph it fits (m <= 31) has a sparse plan
@@ -4979,6 +5252,8 @@ struct Knobs {
   std::atomic<int> tail_pair{1};       // 0: tail_cyc_kernel (one tile column per workgroup)
   std::atomic<int> tail_warm{1};       // 0: no warm-up of the tail's diagonal factor code
   std::atomic<int> tail_zinv{0};       // 1: the tail's back-substitution through Z = L^-1 (round 5; measured slower)
+  std::atomic<int> gcomb{1};           // 0: col_backsub_kernel after the tail instead of gcol_worker
+  std::atomic<int> gcomb_wg{64};       // gcol_worker workgroups (at most; 64 measured best at 128 / 256 KFs)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -4999,6 +5274,8 @@ struct Knobs {
     env("M3S_TAIL_PAIR", tail_pair);
     env("M3S_TAIL_WARM", tail_warm);
     env("M3S_TAIL_ZINV", tail_zinv);
+    env("M3S_GCOMB", gcomb);
+    env("M3S_GCOMB_WG", gcomb_wg);
 #endif
   }
 };
@@ -5019,6 +5296,8 @@ inline bool subtree_path() { return knobs().subtree != 0; }
 inline bool tail_pair_path() { return knobs().tail_pair != 0; }
 inline bool tail_warm_knob() { return knobs().tail_warm != 0; }
 inline bool tail_zinv_knob() { return knobs().tail_zinv != 0; }
+inline bool gcomb_knob() { return knobs().gcomb != 0; }
+inline int gcomb_wg_knob() { return std::max(1, knobs().gcomb_wg.load()); }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -5032,6 +5311,8 @@ constexpr bool subtree_path() { return false; }
 constexpr bool tail_pair_path() { return true; }
 constexpr bool tail_warm_knob() { return true; }
 constexpr bool tail_zinv_knob() { return false; }  // (measured slower, tail_zinv_col)
+constexpr bool gcomb_knob() { return true; }
+constexpr int gcomb_wg_knob() { return 64; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -5377,6 +5658,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       C.delta_thresh = a->delta_thresh;
       double *tail = at<double>(ws, Ly.tail);
       const int tld = 16 * kTailMaxT;
+      bool gcomb_used = false;  // the tail launch also ran the sparse back-substitution
       if (df_path()) {
         // every block of the sparse columns and the tail border: one wave-level dataflow
         DfArgs F;
@@ -5453,11 +5735,26 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.zinv = tail_zinv_knob() ? 1 : 0;
           Y.Zg = tail + tail_z_offset_doubles();
           const int TC = (7 * meta.nc + 15) / 16;
+          // the sparse back-substitution on extra workgroups of the tail's
+          // launch (gcol_worker) when there are sparse columns
+          GArgs G;
+          G.X = nullptr;
+          G.n_pairs = (TC + 1) / 2;
+          G.nx = ((1 + 7 * meta.nc) + 7) / 8 * 8;
+          G.task = C.ctr + 8, G.comb = C.ctr + 9, G.fin = C.ctr + 10, G.xt_ready = C.ctr + 11;
+          G.cnt = Y.tflag + 2 * kTailMaxT;
+          int nG = 0;
+          if (gcomb_knob() && tail_pair_path() && !Y.zinv && C.ncols > 0 && !(subtree_path() && meta.n_sub > 0)) {
+            G.X = at<double>(ws, Ly.gx);
+            nG = std::max(1, std::min(C.ncols, std::min(gcomb_wg_knob(), 240 - G.n_pairs)));
+            gcomb_used = true;
+          }
+          const unsigned gt = (unsigned)(G.n_pairs + nG);
           if (tail_pair_path())
             if (((7 * meta.nc + 16) / 16 + 2) / 3 <= 7)  // tile rows TR: rows per wave of waves 1..3
-              tail_pair_kernel<7><<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
+              tail_pair_kernel<7><<<gt, 64 * kTailNW, 0, st>>>(T, Y, C, G);
             else
-              tail_pair_kernel<(kTailMaxT + 2) / 3><<<(TC + 1) / 2, 64 * kTailNW, 0, st>>>(T, Y);
+              tail_pair_kernel<(kTailMaxT + 2) / 3><<<gt, 64 * kTailNW, 0, st>>>(T, Y, C, G);
           else
             tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
         } else {
@@ -5474,7 +5771,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         subtree_backsub_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_bs_lds, st>>>(B);
       } else
 #endif
-      {
+      if (!gcomb_used) {
         const int g4 = std::max(1, std::min(C.ncols, 256));
         col_backsub_kernel<<<g4, 64, 0, st>>>(C);
       }
@@ -6911,7 +7208,7 @@ int m3s_set_knob(const char *name, int value) {
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
              {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
-             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}
+             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}, {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}
 #endif
   };
   for (const auto &t : tab)

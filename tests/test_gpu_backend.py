@@ -553,6 +553,7 @@ def test_subtree_factor_matches_block_dataflow_bitwise(test_lib, be, N, knobs):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 12, 16, seed=750 + N)
+    knobs("gcomb", "0")  # the same back-substitution on both sides (col_backsub_kernel's sums)
     knobs("subtree", "1")
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     knobs("subtree", "0")
@@ -572,6 +573,7 @@ def test_tail_pairs_match_tail_columns_bitwise(test_lib, be, N, knobs):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 12, 16, seed=850 + N)
+    knobs("gcomb", "0")  # both with col_backsub_kernel (tail_cyc_kernel has no workers)
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     knobs("tail_pair", "0")
     T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
@@ -692,6 +694,7 @@ def test_tail_zinv_matches_substitution(test_lib, be, N, knobs):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 12, 16, seed=870 + N)
+    knobs("gcomb", "0")  # col_backsub_kernel on both sides (the workers need tail_backsub_wg's x_t flag)
     knobs("tail_zinv", "1")
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     knobs("tail_zinv", "0")
@@ -701,6 +704,30 @@ def test_tail_zinv_matches_substitution(test_lib, be, N, knobs):
     np.testing.assert_allclose(dx_a, dx_b, rtol=0, atol=1e-6 * np.abs(dx_b).max() + 1e-9)
     np.testing.assert_allclose(T_a, T_b, rtol=0, atol=1e-6)
     knobs("tail_zinv", "1")
+    T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
+    np.testing.assert_array_equal(dx_a, dx_a2)
+    np.testing.assert_array_equal(T_a, T_a2)
+
+
+@pytest.mark.parametrize("N", [90, 128, 140, 256, 400])
+def test_sparse_backsub_workers_match_column_tasks(test_lib, be, N, knobs):
+    """Round 5: the sparse columns' back-substitution as x_k = a_k + B_k x_t
+    (X_k = [a_k | B_k] by the extra workgroups of the dense tail's launch
+    while the tail factors, gcol_worker, the default) against the column
+    tasks after the tail (col_backsub_kernel, knob gcomb=0): the same factor,
+    a different fp64 summation order, so dx agrees to fp64 round-off seen
+    through the fp32 output; bitwise run to run; no failures."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 12, 16, seed=880 + N)
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    knobs("gcomb", "0")
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
+    np.testing.assert_allclose(dx_a, dx_b, rtol=0, atol=1e-6 * np.abs(dx_b).max() + 1e-9)
+    np.testing.assert_allclose(T_a, T_b, rtol=0, atol=1e-6)
+    knobs("gcomb", "1")
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)

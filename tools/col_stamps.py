@@ -115,6 +115,17 @@ if TC:
                     cells.append("(" + ",".join(f"{(r[i] - tt0) / 100.0:.2f}" for i in (0, 1, 3)) + ")")
             print(f"  J0={J0:2d} " + " ".join(cells))
     print(f"  back-substitution done {(T[511, 0] - tt0) / 100.0:.2f} us")
+    if B[:, 3].max() > 0:  # gcol_worker (knob gcomb): X_k recursion during the tail, then x_k = a_k + B_k x_t
+        print(f"  sparse workers (us from the tail's t0): first ticket {(B[:, 0].min() - tt0) / 100.0:.2f}, "
+              f"last X_k {(B[:, 2].max() - tt0) / 100.0:.2f}, last x_k {(B[:, 3].max() - tt0) / 100.0:.2f}; "
+              f"per column ready->X_k mean {((B[:, 2] - B[:, 1]) / 100.0).mean():.2f} us")
+        for L in range(lev[:c0].max() + 1):
+            ks = cols[lev[:c0] == L]
+            if len(ks):
+                b = B[ks]
+                print(f"    level {L:2d} cols {len(ks):4d}: ticket min {(b[:, 0].min() - tt0) / 100.0:8.2f}  ready max "
+                      f"{(b[:, 1].max() - tt0) / 100.0:8.2f}  X_k max {(b[:, 2].max() - tt0) / 100.0:8.2f}  "
+                      f"ready->X_k mean {((b[:, 2] - b[:, 1]) / 100.0).mean():6.2f}")
     if T[699, 0]:
         print(f"  back-substitution: flags seen {(T[698, 0] - tt0) / 100.0:.2f}, loop start {(T[699, 0] - tt0) / 100.0:.2f}; "
               "x_K published at " + " ".join(f"{(T[700 + K, 0] - tt0) / 100.0:.2f}" for K in range(TC - 1, -1, -1)))

@@ -6,7 +6,8 @@ time per setting and whether poses agree bitwise with the first setting.
 Under rocprofv3 --kernel-trace --stats the per-kernel times come out too.
 
 usage: python tools/solve_ab.py   (env: SOLVE_N="128,256" SOLVE_AB="subtree=1|subtree=0"
-                                    SOLVE_MODE=calib SOLVE_ITERS=3 SOLVE_ROUNDS=7)
+                                    SOLVE_MODE=calib SOLVE_ITERS=3 SOLVE_ROUNDS=7
+                                    LIB=variants/lib_X_test.so: another test build)
 """
 import os
 import statistics
@@ -22,7 +23,7 @@ from mast3r_slam_amd import synthetic  # noqa: E402
 
 
 def main():
-    be._lib = be.load_test_library()
+    be._lib = be._load(os.path.abspath(os.environ["LIB"])) if os.environ.get("LIB") else be.load_test_library()
     dev = torch.device("cuda:0")
     mode = os.environ.get("SOLVE_MODE", "calib")
     iters = int(os.environ.get("SOLVE_ITERS", "3"))

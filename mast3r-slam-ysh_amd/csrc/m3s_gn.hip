@@ -287,6 +287,9 @@ __device__ __forceinline__ PixIn<MODE> gather_pixel(const LinArgs &A, const floa
   return make_pixin<MODE>(A.P, Xi, ok, q, u_t, v_t);
 }
 
+#ifndef M3S_EORDER  // linearize task order: edges grouped by KF j (0) or by KF i (1, A/B)
+#define M3S_EORDER 0
+#endif
 // block -> task (e_loc * chunks + c). The E_loc x chunks tasks sorted by
 // (chunk, KF j) are cut into 8 contiguous runs and run x is dealt to blocks
 // x, x + 8, x + 16, ...: the edges that stream the same Xj chunk run back to
@@ -1029,7 +1032,11 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
 #pragma unroll
     for (int s4 = 0; s4 < 4; s4++) {
       vm[s4] = ((g.vb >> (8 * s4)) & 0xffu) != 0;
+#if M3S_GATHER_IDENT  // A/B bound only (wrong sums): every gather at the pixel's own index
+      id[s4] = vm[s4] ? p0 + s4 : 0;
+#else
       id[s4] = vm[s4] ? (int)ids[s4] : 0;
+#endif
       if (MODE == M3S_MODE_CALIB) {
         gx[s4][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, 12 * id[s4] + 8, 0, 0));
       } else {
@@ -5032,7 +5039,7 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
       if (e < E) {
         const int ri = rank(ei[u]), rj = rank(ej[u]);
         A.rank_i[e] = ri, A.rank_j[e] = rj;
-        erj[e] = rj;
+        erj[e] = M3S_EORDER ? ri : rj;
       }
     }
   } else {
@@ -5063,7 +5070,7 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
       if (e < E) {
         const int ri = lower_bound_i64(uniq, nu, ei[u]), rj = lower_bound_i64(uniq, nu, ej[u]);
         A.rank_i[e] = ri, A.rank_j[e] = rj;
-        erj[e] = rj;
+        erj[e] = M3S_EORDER ? ri : rj;
       }
     }
   }
@@ -5509,7 +5516,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
       M.range_b = eb, M.range_e = ee, M.planes_ok = false, M.order_ok = false;
       if ((int64_t)M.rj.size() >= ee) {
         std::vector<int32_t> order;
-        build_eorder(M.rj, eb, E_loc, order);
+        build_eorder(M3S_EORDER ? M.h_ri : M.rj, eb, E_loc, order);
         // uploaded from pinned staging guarded by an event, so the registry
         // entry owns no host memory a queued copy still reads (m3s_gn_release
         // need not synchronise)
@@ -6115,14 +6122,14 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       }
     }
   }
-  if (hit && E > 0 && meta.eorder.empty()) build_eorder(meta.rj, 0, E, meta.eorder);  // cached by the prologue path
+  if (hit && E > 0 && meta.eorder.empty()) build_eorder(M3S_EORDER ? meta.h_ri : meta.rj, 0, E, meta.eorder);  // cached by the prologue path
   if (!hit) {
     // ranks and the full-range task table now (the first linearize needs
     // them); the symbolic plan is built by the first solve of this call,
     // while the first linearize kernel runs (finish_plan)
     meta.h_ri = ri;
     meta.rj = rj;
-    if (E > 0) build_eorder(meta.rj, 0, E, meta.eorder);
+    if (E > 0) build_eorder(M3S_EORDER ? meta.h_ri : meta.rj, 0, E, meta.eorder);
     meta.sparse = !bad && !force_dense && a->N > 1;  // the expected outcome (the dense path reads partials either way)
     meta.plan_pending = !bad && a->N > 1;
     meta.force_dense = force_dense;

@@ -432,6 +432,101 @@ __device__ __forceinline__ T xreduce36(const T (&v)[kNP], int lane, int &idx, bo
   return f[0];
 }
 
+// The same transposed reduction on the VALU's cross-lane paths instead of
+// ds_bpermute (an LDS round trip per shuffle, ~6 dependent ones per call on
+// the tracker's per-iteration critical path): xor 32 and xor 16 by the gfx950
+// v_permlane32_swap / v_permlane16_swap (one swap exchanges the halves of a
+// value pair: each side then adds what it keeps to what it received), xor 8
+// by DPP row_ror:8, then DPP row_half_mirror (lane i of a half-row pairs with
+// 7 - i: the pairs still split on lane bit 2, so the keep rule and the final
+// index are xreduce36's), quad_perm [2,3,0,1] and [1,0,3,2]. Every sum is
+// keep + partner as before; only the xor-4 step's partner (and so the fp
+// rounding of the result) differs from xreduce36's.
+template <typename T>
+__device__ __forceinline__ void xr_swap(bool s32, T &x, T &y) {  // {x, y} -> {x_lo|y_lo, x_hi|y_hi}
+  if constexpr (sizeof(T) == 4) {
+    const auto r = s32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false)
+                       : __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]), y = __uint_as_float(r[1]);
+  } else {
+    const unsigned long long xb = (unsigned long long)__double_as_longlong(x), yb = (unsigned long long)__double_as_longlong(y);
+    const unsigned xl = (unsigned)xb, xh = (unsigned)(xb >> 32), yl = (unsigned)yb, yh = (unsigned)(yb >> 32);
+    const auto rl = s32 ? __builtin_amdgcn_permlane32_swap(xl, yl, false, false) : __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+    const auto rh = s32 ? __builtin_amdgcn_permlane32_swap(xh, yh, false, false) : __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+    x = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
+    y = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
+  }
+}
+template <int CTRL, typename T>
+__device__ __forceinline__ T xr_dpp(T v) {  // the DPP partner's value
+  if constexpr (sizeof(T) == 4) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  } else {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+template <int N, bool S32, typename T>
+__device__ __forceinline__ void xr_swap_step(const T (&v)[N], T (&o)[(N + 1) / 2]) {
+  constexpr int H = (N + 1) / 2;
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    T x = v[i], y = (i + H < N) ? v[i + H] : T(0);
+    xr_swap(S32, x, y);
+    o[i] = x + y;
+  }
+}
+template <int N, int CTRL, typename T>
+__device__ __forceinline__ void xr_dpp_step(const T (&v)[N], T (&o)[(N + 1) / 2], bool hi) {
+  constexpr int H = (N + 1) / 2;
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    const T lo_v = v[i];
+    const T hi_v = (i + H < N) ? v[i + H] : T(0);
+    const T keep = hi ? hi_v : lo_v, send = hi ? lo_v : hi_v;
+    o[i] = keep + xr_dpp<CTRL>(send);
+  }
+}
+template <typename T>
+__device__ __forceinline__ T xreduce36_dpp(const T (&v)[kNP], int lane, int &idx, bool &valid) {
+  T a[18], b[9], c[5], d[3], e[2], f[1];
+  xr_swap_step<36, true>(v, a);
+  xr_swap_step<18, false>(a, b);
+  xr_dpp_step<9, 0x128>(b, c, lane & 8);  // row_ror:8
+  xr_dpp_step<5, 0x141>(c, d, lane & 4);  // row_half_mirror
+  xr_dpp_step<3, 0x4E>(d, e, lane & 2);   // quad_perm [2,3,0,1]
+  xr_dpp_step<2, 0xB1>(e, f, lane & 1);   // quad_perm [1,0,3,2]
+  int base = 0, r = kNP, sz = kNP;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const int h = (sz + 1) / 2;
+    if (lane & m)
+      base += h, r = r > h ? r - h : 0;
+    else
+      r = r < h ? r : h;
+    sz = h;
+  }
+  idx = base;
+  valid = r == 1;
+  return f[0];
+}
+#ifndef M3S_XRED_DPP_LIN  // the linearize kernels' block partials on xreduce36_dpp (0: xreduce36)
+#define M3S_XRED_DPP_LIN 1
+#endif
+#ifndef M3S_XRED_DPP  // the tracker's per-iteration reductions on xreduce36_dpp (0: xreduce36)
+#define M3S_XRED_DPP 1
+#endif
+template <typename T>
+__device__ __forceinline__ T xreduce36_trk(const T (&v)[kNP], int lane, int &idx, bool &valid) {
+#if M3S_XRED_DPP
+  return xreduce36_dpp(v, lane, idx, valid);
+#else
+  return xreduce36(v, lane, idx, valid);
+#endif
+}
+
 __device__ __forceinline__ void store_partial(const float *acc, float *out) {
   __shared__ float red[kThreads / 64][kNP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -440,7 +535,11 @@ __device__ __forceinline__ void store_partial(const float *acc, float *out) {
   for (int k = 0; k < kNP; k++) v[k] = acc[k];
   int idx;
   bool valid;
+#if M3S_XRED_DPP_LIN
+  const float s = xreduce36_dpp(v, lane, idx, valid);
+#else
   const float s = xreduce36(v, lane, idx, valid);
+#endif
   if (valid) red[wave][idx] = s;
   __syncthreads();
   if (threadIdx.x < kNP) {
@@ -6733,7 +6832,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
     {
       int idx;
       bool ok;
-      const float x = xreduce36(v, lane, idx, ok);
+      const float x = xreduce36_trk(v, lane, idx, ok);
       if (ok) redf[wv][idx] = x;
     }
     __syncthreads();
@@ -6787,7 +6886,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         if (spins > kTrkSpins) a[0] = __builtin_nan("");
         int idx;
         bool ok;
-        const double x = xreduce36(a, lane, idx, ok);
+        const double x = xreduce36_trk(a, lane, idx, ok);
         {
           const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
           const u32x4 w = {(unsigned)(xb & 0xffffffffull), (unsigned)(xb >> 32), (unsigned)(it + 1), 0u};

@@ -6748,6 +6748,14 @@ constexpr int kTrkSpins = 1 << 22;
 #ifndef M3S_TRK_TOPALL
 #define M3S_TRK_TOPALL 0
 #endif
+// M3S_TRK_FLAT (round 5): no shard level. Workgroup 0 polls every
+// workgroup's partial granules on all its waves (wave w: members 64 w ..
+// 64 w + 63, one per lane), reduces them per wave and then across the waves
+// (fixed order), updates and publishes the record: two fabric hops per
+// iteration instead of three.
+#ifndef M3S_TRK_FLAT
+#define M3S_TRK_FLAT 0
+#endif
 constexpr int kTrkShBufs = M3S_TRK_TOPALL ? 2 : 1;
 struct TrackSync {
   uint32_t rec[32];  // the published record: 4 tagged 16-B granules (pose 0-7, status 8, cost 9-10 | tag)
@@ -6853,6 +6861,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         __builtin_amdgcn_raw_buffer_store_b128(w, Rpart, lane < kTrkGran ? (b * kTrkGran + lane) * 16 : kPartFar, 0, 16);
       }
       M3S_TSTAMP(2)
+#if !M3S_TRK_FLAT
       const int shb = M3S_TRK_TOPALL ? (it & 1) : 0;  // the shard-sum buffer of this iteration
       // level 1: workgroup s < 8 reduces shard s = {s, s + 8, ...}: lane j
       // polls member s + 8 j's granules, then the 36 sums are reduced across
@@ -7011,7 +7020,87 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         }
       }
 #endif
+#endif  // !M3S_TRK_FLAT
     }
+#if M3S_TRK_FLAT
+    if (b == 0) {
+      // one level: wave w polls the partial granules of members 64 w + lane,
+      // reduces its 64 members in fp64 (lane order), and wave 0 sums the
+      // waves in order, updates and publishes the record
+      u32x4 g[kTrkGran];
+      int spins = 0;
+      for (;;) {
+#pragma unroll
+        for (int k = 0; k < kTrkGran; k++) g[k] = poll_b128(Rpart, t < G ? (t * kTrkGran + k) * 16 : kPartFar);
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < kTrkGran; k++) ok &= t >= G || g[k].w == (unsigned)(it + 1);
+        if (__ballot(!ok) == 0) break;
+        trk_pause();
+        if (++spins > kTrkSpins) break;
+      }
+      double a[kNP];
+#pragma unroll
+      for (int k = 0; k < kTrkGran; k++) {
+        a[3 * k] = (double)__uint_as_float(g[k].x);
+        a[3 * k + 1] = (double)__uint_as_float(g[k].y);
+        a[3 * k + 2] = (double)__uint_as_float(g[k].z);
+      }
+      if (spins > kTrkSpins) a[0] = __builtin_nan("");  // the update then fails (status 2)
+      {
+        int idx;
+        bool ok;
+        const double x = xreduce36_trk(a, lane, idx, ok);
+        if (ok) redd[wv][idx] = x;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        M3S_TSTAMP(3)
+        if (lane < kNP) {
+          double x = 0.0;
+#pragma unroll
+          for (int w = 0; w < NW; w++) x += redd[w][lane];
+          s_sum[lane] = x;
+        }
+        wave_lds_fence();
+        M3S_TSTAMP(4)
+        if (lane == 0) {
+          double oc = it == 0 ? __builtin_inf()
+                              : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
+          Sim3f Tn = T;
+          const int r = track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
+          M3S_TSTAMP(6)
+          if (r != kTrackContinue && r != kTrackConverged) Tn = T;
+          float rec[8];
+          store_sim3(rec, Tn);
+#pragma unroll
+          for (int k = 0; k < 8; k++) pub_s[k] = __float_as_uint(rec[k]);
+          const unsigned long long ob = (unsigned long long)__double_as_longlong(oc);
+          pub_s[8] = (uint32_t)r, pub_s[9] = (uint32_t)(ob & 0xffffffffull), pub_s[10] = (uint32_t)(ob >> 32);
+          pub_s[11] = 0;
+        }
+        wave_lds_fence();
+        const int q = lane < 4 ? 3 * lane : 0;
+        const u32x4 w = {pub_s[q], pub_s[q + 1], pub_s[q + 2], (unsigned)(it + 1)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, Rrec, lane * 16, 0, 16);
+      }
+    } else if (wv == 0) {
+      int spins = 0;
+      u32x4 g;
+      for (;;) {
+        g = poll_b128(Rrec, lane * 16);
+        if (__ballot(lane < 4 && g.w != (unsigned)(it + 1)) == 0) break;
+        trk_pause();
+        if (++spins > kTrkSpins) break;
+      }
+      M3S_TSTAMP(4)
+      if (spins > kTrkSpins) {
+        if (lane == 0) pub_s[8] = 3;
+      } else if (lane < 4) {
+        pub_s[3 * lane] = g.x, pub_s[3 * lane + 1] = g.y, pub_s[3 * lane + 2] = g.z;
+      }
+    }
+#endif
     M3S_TSTAMP(5)
     __syncthreads();
     status = (int)pub_s[8];

@@ -6752,7 +6752,9 @@ constexpr int kTrkSpins = 1 << 22;
 // workgroup's partial granules on all its waves (wave w: members 64 w ..
 // 64 w + 63, one per lane), reduces them per wave and then across the waves
 // (fixed order), updates and publishes the record: two fabric hops per
-// iteration instead of three.
+// iteration instead of three. Measured slower (profiles/r05/
+// trk_ab_flat_REJECTED.txt: 133k -> 117k GN it/s at C2): one CU polling and
+// converting 256 x 12 granules costs more than the shard hop it removes.
 #ifndef M3S_TRK_FLAT
 #define M3S_TRK_FLAT 0
 #endif

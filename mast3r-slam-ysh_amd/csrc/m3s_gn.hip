@@ -468,6 +468,19 @@ __device__ __forceinline__ T xr_dpp(T v) {  // the DPP partner's value
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
   }
 }
+// u + (u of lane ^ 16), then + (that of lane ^ 32): the two butterfly steps of
+// `u += __shfl_xor(u, 16); u += __shfl_xor(u, 32)` by v_permlane16/32_swap of
+// u with itself (each side gets its partner's value; the sums are the same
+// additions, so bitwise the same result) instead of two ds_bpermute LDS round
+// trips (the dense tail's back-substitution chain, round 5)
+__device__ __forceinline__ double sum_xor16_32(double u) {
+  double a = u, b = u;
+  xr_swap(false, a, b);
+  u = a + b;
+  a = u, b = u;
+  xr_swap(true, a, b);
+  return a + b;
+}
 template <int N, bool S32, typename T>
 __device__ __forceinline__ void xr_swap_step(const T (&v)[N], T (&o)[(N + 1) / 2]) {
   constexpr int H = (N + 1) / 2;
@@ -510,6 +523,35 @@ __device__ __forceinline__ T xreduce36_dpp(const T (&v)[kNP], int lane, int &idx
   }
   idx = base;
   valid = r == 1;
+  return f[0];
+}
+// The same transposed reduction for N <= 64 values (xreduce36_dpp's steps);
+// xred_index gives the value index a lane ends with and whether it is real.
+template <int N>
+__device__ __forceinline__ void xred_index(int lane, int &idx, bool &valid) {
+  int base = 0, r = N, sz = N;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const int h = (sz + 1) / 2;
+    if (lane & m)
+      base += h, r = r > h ? r - h : 0;
+    else
+      r = r < h ? r : h;
+    sz = h;
+  }
+  idx = base;
+  valid = r == 1;
+}
+template <int N, typename T>
+__device__ __forceinline__ T xreduceN_dpp(const T (&v)[N], int lane) {
+  constexpr int S1 = (N + 1) / 2, S2 = (S1 + 1) / 2, S3 = (S2 + 1) / 2, S4 = (S3 + 1) / 2, S5 = (S4 + 1) / 2;
+  T a[S1], b[S2], c[S3], d[S4], e[S5], f[(S5 + 1) / 2];
+  xr_swap_step<N, true>(v, a);
+  xr_swap_step<S1, false>(a, b);
+  xr_dpp_step<S2, 0x128>(b, c, lane & 8);
+  xr_dpp_step<S3, 0x141>(c, d, lane & 4);
+  xr_dpp_step<S4, 0x4E>(d, e, lane & 2);
+  xr_dpp_step<S5, 0xB1>(e, f, lane & 1);
   return f[0];
 }
 #ifndef M3S_XRED_DPP_LIN  // the linearize kernels' block partials on xreduce36_dpp (0: xreduce36)
@@ -4003,8 +4045,7 @@ __device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSyn
               double u = 0.0;
 #pragma unroll
               for (int q = 0; q < 4; q++) u += lt[d][t][q] * xb[q];
-              u += __shfl_xor(u, 16);
-              u += __shfl_xor(u, 32);
+              u = sum_xor16_32(u);
               if (lane < 16) yv[16 * Jc + lane] -= u;
               if (pass == 0) {
                 wave_lds_fence();  // row K - 1's y' before this wave reads it
@@ -4102,8 +4143,7 @@ __device__ __forceinline__ void tail_zinv_col(const TailArgs &A, const TailSync 
       part += row < n ? zi[r] * ld_sc1(S.ypg + row) : 0.0;
     }
   }
-  part += __shfl_xor(part, 16);
-  part += __shfl_xor(part, 32);
+  part = sum_xor16_32(part);
   if (lane < 16 && 16 * J + lane < n) A.rhs[7 * A.c0 + 16 * J + lane] = part;
 }
 
@@ -4463,6 +4503,9 @@ __device__ void gcol_worker(const ColArgs &C, const GArgs &G) {
   // after its flag only x_t is read (one round trip) and summed
   const int cbase = C.epoch * (C.ncols + kTailNW * nG);
   constexpr int kCU = 16 * kTailMaxT / 64;  // tail dofs per lane (nt < 16 kTailMaxT)
+  int ri;
+  bool rv;
+  xred_index<7>(lane, ri, rv);
   for (;;) {
     const int t = wave_gticket(G.comb) - cbase;
     if (t >= C.ncols) break;
@@ -4477,7 +4520,7 @@ __device__ void gcol_worker(const ColArgs &C, const GArgs &G) {
 #pragma unroll
       for (int a = 0; a < 7; a++) bx[u][a] = j < nt ? ld_sc1(Xk + (size_t)a * nx + 1 + j) : 0.0;
     }
-    const double a0 = ld_sc1(Xk + (size_t)(lane < 7 ? lane : 0) * nx);
+    const double a0 = ld_sc1(Xk + (size_t)(rv ? ri : 0) * nx);  // a_k[ri]: this lane's row of the result
     if (lane == 0 && !g_poll(G.xt_ready, want)) set_fail(C.flags);  // the tail's x_t
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     double acc[7];
@@ -4490,14 +4533,10 @@ __device__ void gcol_worker(const ColArgs &C, const GArgs &G) {
 #pragma unroll
       for (int a = 0; a < 7; a++) acc[a] += bx[u][a] * xt;
     }
-#pragma unroll
-    for (int a = 0; a < 7; a++) acc[a] = wave_sum(acc[a]);
-    if (lane < 7) {
-      double v = 0.0;
-#pragma unroll
-      for (int a = 0; a < 7; a++) v = lane == a ? acc[a] : v;
-      st_sc1(C.y + (size_t)k * 7 + lane, a0 + v);
-    }
+    // the 7 wave sums by the transposed reduction (permlane swaps + DPP):
+    // lane ri-holder ends with row ri's sum
+    const double v = xreduceN_dpp<7>(acc, lane);
+    if (rv) st_sc1(C.y + (size_t)k * 7 + ri, a0 + v);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x_k (and any failure flag) out before the ticket
     if (lane == 0) M3S_CSTAMP(1, k, 3);
     const int f = wave_gticket(G.fin);  // the wave that combines the last column finishes the step
@@ -6585,29 +6624,47 @@ __global__ void __launch_bounds__(256) track_init_kernel(const float *T_WCf, con
 // 5-25; rel is NaN on the first step, old_cost = inf). T and old_cost are
 // updated in place unless the Cholesky fails.
 constexpr int kTrackContinue = 0, kTrackConverged = 1, kTrackFailed = 2;
+// A/B: the tracker's 7x7 Cholesky solve in fp32 (the reference's precision,
+// tracker.py:168) instead of fp64: +1% GN it/s at C2
+// (profiles/r05/trk_ab_f32_solve_REJECTED.txt), not worth the precision
+#ifndef M3S_TRK_F32
+#define M3S_TRK_F32 0
+#endif
 __device__ __forceinline__ int track_update(const double *s, Sim3f &T, double &old_cost, float rel_error,
                                             float delta_norm) {
-  double H[7][7], L[7][7], g[7], y[7], x[7];
+#if M3S_TRK_F32
+  typedef float real;
+#else
+  typedef double real;
+#endif
+  real H[7][7], L[7][7], g[7], y[7], x[7];
   for (int a = 0; a < 7; a++)
-    for (int c = 0; c < 7; c++) H[a][c] = s[kL + tri(a < c ? a : c, a < c ? c : a)];
-  for (int a = 0; a < 7; a++) g[a] = s[kG + a];
+    for (int c = 0; c < 7; c++) H[a][c] = (real)s[kL + tri(a < c ? a : c, a < c ? c : a)];
+  for (int a = 0; a < 7; a++) g[a] = (real)s[kG + a];
   const double cost = 0.5 * s[kCost];
-  double dinv[7];
+  real dinv[7];
 #pragma unroll
   for (int a = 0; a < 7; a++)
 #pragma unroll
     for (int c = 0; c < 7; c++) L[a][c] = 0.0;
 #pragma unroll
   for (int k = 0; k < 7; k++) {
-    double d = H[k][k];
+    real d = H[k][k];
 #pragma unroll
     for (int p = 0; p < k; p++) d -= L[k][p] * L[k][p];
-    if (!(d > 0.0)) return kTrackFailed;
+    if (!(d > (real)0)) return kTrackFailed;
+#if M3S_TRK_F32
+    {
+      float r = __builtin_amdgcn_rsqf(d);
+      dinv[k] = r * (1.5f - 0.5f * d * r * r);
+    }
+#else
     dinv[k] = rsqrt_nr(d);
+#endif
     L[k][k] = d * dinv[k];
 #pragma unroll
     for (int i = k + 1; i < 7; i++) {
-      double v = H[i][k];
+      real v = H[i][k];
 #pragma unroll
       for (int p = 0; p < k; p++) v -= L[i][p] * L[k][p];
       L[i][k] = v * dinv[k];
@@ -6615,14 +6672,14 @@ __device__ __forceinline__ int track_update(const double *s, Sim3f &T, double &o
   }
 #pragma unroll
   for (int i = 0; i < 7; i++) {
-    double v = -g[i];
+    real v = -g[i];
 #pragma unroll
     for (int p = 0; p < i; p++) v -= L[i][p] * y[p];
     y[i] = v * dinv[i];
   }
 #pragma unroll
   for (int i = 6; i >= 0; i--) {
-    double v = y[i];
+    real v = y[i];
 #pragma unroll
     for (int p = i + 1; p < 7; p++) v -= L[p][i] * x[p];
     x[i] = v * dinv[i];

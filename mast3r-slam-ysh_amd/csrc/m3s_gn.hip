@@ -481,6 +481,28 @@ __device__ __forceinline__ double sum_xor16_32(double u) {
   xr_swap(true, a, b);
   return a + b;
 }
+// whole-wave sum on every lane by the same exchanges (permlane swaps of the
+// value with itself for xor 32 / 16, then DPP; the xor-4 partner is 7 - i
+// within a half-row): the solve tails' ||dx|| sums (round 5)
+#ifndef M3S_NORM_PL
+#define M3S_NORM_PL 1
+#endif
+__device__ __forceinline__ float wave_sum_pl(float u) {
+#if !M3S_NORM_PL
+  return wave_sum(u);
+#endif
+  float a = u, b = u;
+  xr_swap(true, a, b);
+  u = a + b;
+  a = u, b = u;
+  xr_swap(false, a, b);
+  u = a + b;
+  u += xr_dpp<0x128>(u);
+  u += xr_dpp<0x141>(u);
+  u += xr_dpp<0x4E>(u);
+  u += xr_dpp<0xB1>(u);
+  return u;
+}
 template <int N, bool S32, typename T>
 __device__ __forceinline__ void xr_swap_step(const T (&v)[N], T (&o)[(N + 1) / 2]) {
   constexpr int H = (N + 1) / 2;
@@ -554,8 +576,12 @@ __device__ __forceinline__ T xreduceN_dpp(const T (&v)[N], int lane) {
   xr_dpp_step<S5, 0xB1>(e, f, lane & 1);
   return f[0];
 }
-#ifndef M3S_XRED_DPP_LIN  // the linearize kernels' block partials on xreduce36_dpp (0: xreduce36)
-#define M3S_XRED_DPP_LIN 1
+// the linearize kernels' block partials on xreduce36_dpp (1) or xreduce36 (0):
+// within noise for the packed kernel (an A/B of the first-listed library reads
+// ~2-3% slow in tools/ab_linearize.py either way, profiles/r05/ab_pkw_*.txt),
+// so the round-4 rounding stays
+#ifndef M3S_XRED_DPP_LIN
+#define M3S_XRED_DPP_LIN 0
 #endif
 #ifndef M3S_XRED_DPP  // the tracker's per-iteration reductions on xreduce36_dpp (0: xreduce36)
 #define M3S_XRED_DPP 1
@@ -1339,7 +1365,7 @@ __device__ void finish_step(const double *xs, float *dxs, float *nrm, int n, flo
     dx_out[k] = v;
     part += v * v;
   }
-  part = wave_sum(part);
+  part = wave_sum_pl(part);
   if ((tid & 63) == 0) nrm[tid >> 6] = part;
   __syncthreads();
   for (int p = tid; p < (int)(N - 1); p += nt) {
@@ -2686,7 +2712,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     if (dx_lds) dxl[vo * 7 + q] = v;
     part += v * v;
   }
-  part = wave_sum(part);
+  part = wave_sum_pl(part);
   if (lane == 0) nrm[wave] = part;
   __syncthreads();  // dx_out (global) written by this block is visible to it now
   for (int p = tid; p < m; p += 1024) {
@@ -3283,7 +3309,7 @@ __device__ void col_finish(const ColArgs &C, int lane) {
       }
     }
   }
-  part = wave_sum(part);
+  part = wave_sum_pl(part);
   wave_lds_fence();
   for (int p = lane; p < m; p += 64) {
     const Sim3f T = load_sim3(C.Twc + 8 * (size_t)(p + 1));

@@ -61,8 +61,10 @@ def main():
                                       max_iter=iters, delta_thresh=0.0, dx=dx, info=info, workspace=ws)
             per.append(dict(a=a, keep=keep, Twc=Twc, info=info, dx=dx, t=[]))
         fn = "m3s_gauss_newton_calib" if calib else "m3s_gauss_newton_rays"
+        pairs = list(zip(handles, per))
         for r in range(rounds + 1):
-            for L, d in zip(handles, per):
+            # rotate the order every round (no library always runs first)
+            for L, d in pairs[r % len(pairs):] + pairs[:r % len(pairs)]:
                 d["Twc"].copy_(g.T_init.data)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()

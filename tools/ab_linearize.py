@@ -72,8 +72,11 @@ def main():
     reps, rounds = 20, 5
     times = {p: [] for p in libs}
     first = {p: [] for p in libs}
-    for _ in range(rounds):
-        for p, L, aa in zip(libs, handles, wargs):
+    trio = list(zip(libs, handles, wargs))
+    for rnd in range(rounds):
+        # the list order rotates every round: the first-listed library read
+        # ~2-3 % slow when it always ran first (profiles/r05/ab_pkw_order*.txt)
+        for p, L, aa in trio[rnd % len(trio):] + trio[:rnd % len(trio)]:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             assert L.m3s_gn_prepare(ctypes.byref(aa), st) == 0
             s.record()

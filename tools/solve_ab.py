@@ -37,7 +37,10 @@ def main():
         times = [[] for _ in groups]
         outs = [None] * len(groups)
         for rnd in range(rounds):
-            for gi, grp in enumerate(groups):
+            # rotate the order every round (no setting always runs first)
+            order = list(range(len(groups)))
+            for gi in order[rnd % len(order):] + order[:rnd % len(order)]:
+                grp = groups[gi]
                 old = {k: be.set_knob(k, int(v)) for k, v in grp.items()}
                 Twc = g.T_init.data.clone().contiguous()
                 info = torch.zeros(8, dtype=torch.int32, device=dev)

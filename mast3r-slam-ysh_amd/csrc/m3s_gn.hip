@@ -1797,6 +1797,9 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_LOOKAHEAD  // DIAG(k+1) inside step k's trailing update (dense tail)
 #define M3S_TAIL_LOOKAHEAD 1
 #endif
+#ifndef M3S_BS49  // sparse_llt_kernel's level-synchronous back-substitution on 56 lanes (round 5)
+#define M3S_BS49 1
+#endif
 #ifndef M3S_BS_SYNC  // sparse_llt_kernel: level-synchronous back-substitution (round 5; 0 = dataflow)
 #define M3S_BS_SYNC 1
 #endif
@@ -2655,7 +2658,48 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   // are the dataflow's (sub_matvec in list order): bitwise the same x. The
   // dataflow form paid a flag poll (s_sleep granularity), a release fence and
   // an LDS ticket per column on the chain: ~2k cycles per level at C3.
-  {
+  // M3S_BS49 (round 5, factor in LDS): a column on 56 lanes, lane 8a + b
+  // holding term b of row a: every block's L_ik and x_i entry of the lane in
+  // one LDS load each, all blocks' loads in flight, the products summed over
+  // the blocks per lane, then over b by three DPP steps; W_k^T r the same way
+  // through the wave's scratch. The 7-lane form ran each block as 7 dependent
+  // LDS-operand FMAs and the W product as 7 readlane broadcasts (~2k cycles
+  // per level at C3). Another summation order: x within fp64 round-off.
+  if (M3S_BS49 && !STAGE) {
+    const int32_t *lev_ptr = pl + D.off[4];
+    const int a8 = lane >> 3, b8 = lane & 7;
+    const bool act = a8 < 7 && b8 < 7;
+    const int ac = a8 < 7 ? a8 : 6, bc = b8 < 7 ? b8 : 6;
+    for (int L = D.levels - 1; L >= 0; L--) {
+      for (int c = lev_ptr[L] + wave; c < lev_ptr[L + 1]; c += NW) {
+        const int k = lev_col[c];
+        if (k >= m - D.nc) continue;  // dense tail: done above
+        const int q0 = col_ptr[k], q1 = col_ptr[k + 1];
+        double s0 = 0.0, s1 = 0.0;
+        int q = q0;
+        for (; q + 1 < q1; q += 2) {  // (L_ik^T x_i)[a] = sum_b L_ik[b][a] x_i[b]
+          const double l0 = Lb[(size_t)col_slot[q] * 49 + bc * 7 + ac], l1 = Lb[(size_t)col_slot[q + 1] * 49 + bc * 7 + ac];
+          const double x0 = y[col_row[q] * 7 + bc], x1 = y[col_row[q + 1] * 7 + bc];
+          s0 += l0 * x0;
+          s1 += l1 * x1;
+        }
+        if (q < q1) s0 += Lb[(size_t)col_slot[q] * 49 + bc * 7 + ac] * y[col_row[q] * 7 + bc];
+        double sm = act ? s0 + s1 : 0.0;
+        sm += xr_dpp<0x141>(sm);  // over b: half-row mirror, then quad_perm xor 2, xor 1
+        sm += xr_dpp<0x4E>(sm);
+        sm += xr_dpp<0xB1>(sm);
+        if (b8 == 0 && a8 < 7) scr[a8] = y[k * 7 + a8] - sm;
+        wave_lds_fence();
+        double t = act ? Di[(size_t)k * 49 + bc * 7 + ac] * scr[bc] : 0.0;  // x_k[a] = sum_b W_k[b][a] r[b]
+        t += xr_dpp<0x141>(t);
+        t += xr_dpp<0x4E>(t);
+        t += xr_dpp<0xB1>(t);
+        if (b8 == 0 && a8 < 7) y[k * 7 + a8] = t;
+        wave_lds_fence();  // the scratch is read before the next column rewrites it
+      }
+      __syncthreads();
+    }
+  } else {
     const int32_t *lev_ptr = pl + D.off[4];
     for (int L = D.levels - 1; L >= 0; L--) {
       for (int c = lev_ptr[L] + wave; c < lev_ptr[L + 1]; c += NW) {
@@ -5425,6 +5469,7 @@ struct Knobs {
   std::atomic<int> tail_zinv{0};       // 1: the tail's back-substitution through Z = L^-1 (round 5; measured slower)
   std::atomic<int> gcomb{1};           // 0: col_backsub_kernel after the tail instead of gcol_worker
   std::atomic<int> gcomb_wg{64};       // gcol_worker workgroups (at most; 64 measured best at 128 / 256 KFs)
+  std::atomic<int> gcomb_min_nc{32};   // smallest dense tail (block columns) that takes the workers
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -5447,6 +5492,7 @@ struct Knobs {
     env("M3S_TAIL_ZINV", tail_zinv);
     env("M3S_GCOMB", gcomb);
     env("M3S_GCOMB_WG", gcomb_wg);
+    env("M3S_GCOMB_MIN_NC", gcomb_min_nc);
 #endif
   }
 };
@@ -5469,6 +5515,7 @@ inline bool tail_warm_knob() { return knobs().tail_warm != 0; }
 inline bool tail_zinv_knob() { return knobs().tail_zinv != 0; }
 inline bool gcomb_knob() { return knobs().gcomb != 0; }
 inline int gcomb_wg_knob() { return std::max(1, knobs().gcomb_wg.load()); }
+inline int gcomb_min_nc_knob() { return knobs().gcomb_min_nc.load(); }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -5484,6 +5531,10 @@ constexpr bool tail_warm_knob() { return true; }
 constexpr bool tail_zinv_knob() { return false; }  // (measured slower, tail_zinv_col)
 constexpr bool gcomb_knob() { return true; }
 constexpr int gcomb_wg_knob() { return 64; }
+// the workers pay off once the dense tail's chain is long enough to hide the
+// X_k recursion: 256 KFs (42-column tail) 0.751 -> 0.712 ms per 3-iteration
+// call, 128 KFs (a shorter tail) 0.493 -> 0.501 (profiles/r05/solve_ab_gcomb_rotated.txt)
+constexpr int gcomb_min_nc_knob() { return 32; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -5915,7 +5966,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           G.task = C.ctr + 8, G.comb = C.ctr + 9, G.fin = C.ctr + 10, G.xt_ready = C.ctr + 11;
           G.cnt = Y.tflag + 2 * kTailMaxT;
           int nG = 0;
-          if (gcomb_knob() && tail_pair_path() && !Y.zinv && C.ncols > 0 && !(subtree_path() && meta.n_sub > 0)) {
+          if (gcomb_knob() && meta.nc >= gcomb_min_nc_knob() && tail_pair_path() && !Y.zinv && C.ncols > 0 &&
+              !(subtree_path() && meta.n_sub > 0)) {
             G.X = at<double>(ws, Ly.gx);
             nG = std::max(1, std::min(C.ncols, std::min(gcomb_wg_knob(), 240 - G.n_pairs)));
             gcomb_used = true;
@@ -7488,7 +7540,7 @@ int m3s_set_knob(const char *name, int value) {
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
              {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
-             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}, {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}
+             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}, {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}, {"gcomb_min_nc", &k.gcomb_min_nc}
 #endif
   };
   for (const auto &t : tab)

@@ -728,6 +728,7 @@ def test_sparse_backsub_workers_match_column_tasks(test_lib, be, N, knobs):
     from mast3r_slam_amd import synthetic
 
     g = synthetic.make_graph(N, 12, 16, seed=880 + N)
+    knobs("gcomb_min_nc", "0")  # the workers on every tail size (the product takes them from 32 columns)
     T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
     knobs("gcomb", "0")
     T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
@@ -739,3 +740,25 @@ def test_sparse_backsub_workers_match_column_tasks(test_lib, be, N, knobs):
     T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
     np.testing.assert_array_equal(dx_a, dx_a2)
     np.testing.assert_array_equal(T_a, T_a2)
+
+
+def test_broken_plan_through_workers_is_solve_failure(test_lib, be, knobs):
+    """The bounded waits of the tail launch's back-substitution workers: a
+    dropped leaf DIAG item (df_factor_kernel) with the workers forced on a
+    small tail ends as one failed iteration (dx = 0, poses untouched), and the
+    intact plan then solves (round 5: the finishing wave must see every
+    failure flag, stored before the flags that release the step)."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(140, 12, 16, seed=37)
+    knobs("dense_tail_min", 8)
+    knobs("gcomb_min_nc", "0")
+    knobs("debug_drop_item", "0")
+    T_gpu, dx, info = run_gpu(be, "rays", g, 1, 0.0)
+    assert info[be.INFO_SOLVE_FAIL] == 1 and info[be.INFO_ITERS] == 1
+    assert np.all(dx == 0)
+    np.testing.assert_array_equal(T_gpu, g.T_init.data.numpy())
+    knobs("debug_drop_item", -1)
+    T_ok, _, info = run_gpu(be, "rays", g, 1, 0.0)
+    assert info[be.INFO_SOLVE_FAIL] == 0 and info[be.INFO_ITERS] == 1
+    assert not np.array_equal(T_ok, g.T_init.data.numpy())

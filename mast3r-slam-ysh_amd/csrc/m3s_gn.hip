@@ -1797,6 +1797,12 @@ constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_LOOKAHEAD  // DIAG(k+1) inside step k's trailing update (dense tail)
 #define M3S_TAIL_LOOKAHEAD 1
 #endif
+#ifndef M3S_FORMX4  // the dense tail's back-substitution: x_K's dot products over 4 lane groups (A/B)
+#define M3S_FORMX4 0
+#endif
+#ifndef M3S_FIN_PRELOAD  // col_finish: the wave's poses loaded up front (A/B)
+#define M3S_FIN_PRELOAD 0
+#endif
 #ifndef M3S_BS49  // sparse_llt_kernel's level-synchronous back-substitution on 56 lanes (round 5)
 #define M3S_BS49 1
 #endif
@@ -3327,6 +3333,17 @@ __device__ void col_finish(const ColArgs &C, int lane) {
     }
     return;
   }
+  // the poses this wave retracts, all in flight now (clamped indices, no
+  // guards: a guarded load per pose was one dependent round trip each, round 5)
+#if M3S_FIN_PRELOAD
+  constexpr int kFinP = 8;  // m <= 512 on the chip-wide path
+  Sim3f Tp[kFinP];
+#pragma unroll
+  for (int u = 0; u < kFinP; u++) {
+    const int p = min(lane + 64 * u, m - 1);
+    Tp[u] = load_sim3(C.Twc + 8 * (size_t)(p + 1));
+  }
+#endif
   // every x_k was published before this workgroup's ticket and the caller's
   // agent-scope acquire: plain loads, all in flight at once (one relaxed
   // atomic load per entry was one dependent fabric round trip each: ~28 per
@@ -3355,6 +3372,18 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
   part = wave_sum_pl(part);
   wave_lds_fence();
+#if M3S_FIN_PRELOAD
+#pragma unroll
+  for (int u = 0; u < kFinP; u++) {
+    const int p = lane + 64 * u;
+    if (p < m) {
+      float xi[7];
+#pragma unroll
+      for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
+      store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, Tp[u]));
+    }
+  }
+#else
   for (int p = lane; p < m; p += 64) {
     const Sim3f T = load_sim3(C.Twc + 8 * (size_t)(p + 1));
     float xi[7];
@@ -3362,6 +3391,7 @@ __device__ void col_finish(const ColArgs &C, int lane) {
     for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
     store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, T));
   }
+#endif
   if (lane == 0) {
     C.info[M3S_INFO_ITERS] += 1;
     if (sqrtf(part) < C.delta_thresh) {
@@ -4074,12 +4104,24 @@ __device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSyn
   };
   auto form_x = [&](int K) {  // the owner of row K, all of whose updates are in
     const int jv = min(16, n - 16 * K);
+    // x_K[r] = sum_i W_K^T[r][i] y'_K[i]: lane r + 16 g sums i in [4 g, 4 g + 4),
+    // then the four groups by the permlane swaps (4 dependent FMAs + 2 swap
+    // steps on the chain instead of 16 FMAs, round 5)
+#if M3S_FORMX4
+    const int r16 = lane & 15, g4 = lane >> 4;
+    double x = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) x += WlT[(K * 16 + r16) * 17 + 4 * g4 + i] * yv[16 * K + 4 * g4 + i];
+    x = sum_xor16_32(x);
+    if (lane < 16) xv[16 * K + lane] = lane < jv ? x : 0.0;
+#else
     if (lane < 16) {
       double x = 0.0;
 #pragma unroll
       for (int i = 0; i < 16; i++) x += WlT[(K * 16 + lane) * 17 + i] * yv[16 * K + i];
       xv[16 * K + lane] = lane < jv ? x : 0.0;
     }
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (lane == 0) M3S_CSTAMP(2, 700 + K, 0);
@@ -6890,6 +6932,12 @@ constexpr int kTrkSpins = 1 << 22;
 // iteration instead of three. Measured slower (profiles/r05/
 // trk_ab_flat_REJECTED.txt: 133k -> 117k GN it/s at C2): one CU polling and
 // converting 256 x 12 granules costs more than the shard hop it removes.
+// M3S_TRK_PP (round 5): the per-iteration accumulation on pixel pairs
+// (AccumPP / pixel_contrib2, as the backend's packed kernel) instead of the
+// per-pixel row-pair Accum
+#ifndef M3S_TRK_PP
+#define M3S_TRK_PP 1
+#endif
 #ifndef M3S_TRK_FLAT
 #define M3S_TRK_FLAT 0
 #endif
@@ -6959,6 +7007,34 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
   for (; it < max_iters; it++) {
     M3S_TSTAMP(0)
     const Sim3Mat Tm = sim3_matrix(T);
+    float v[kNP];
+#pragma unroll
+    for (int k = 0; k < kNP; k++) v[k] = 0.0f;
+#if M3S_TRK_PP
+    {  // pixel pairs in the halves of float2 registers (the backend's packed
+       // accumulation, with the cost sum); a lane's pixel past the image takes
+       // a zero weight
+      constexpr int NPL = PixIn<MODE>::kPlanes, SQK = MODE == 2 ? 1 : NPL - 1;
+      AccumPP acc;
+      acc.zero();
+#pragma unroll
+      for (int s = 0; s < PPL; s += 2) {
+        const int s1 = s + 1 < PPL ? s + 1 : s;
+        f32x2 in2[NPL], X2[3], Y2[3];
+#pragma unroll
+        for (int k = 0; k < NPL; k++) {
+          const float lo = (k == SQK && !live[s]) ? 0.0f : in[s].v[k];
+          const float hi = (k == SQK && (!live[s1] || s1 == s)) ? 0.0f : in[s1].v[k];
+          in2[k] = f32x2{lo, hi};
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) X2[k] = f32x2{Xf[s][k], Xf[s1][k]};
+        act2(Tm, X2, Y2);
+        pixel_contrib2<MODE, NPL, true>(acc, A.P, in2, Y2);
+      }
+      acc.fold(v);
+    }
+#else
     Accum<MODE> acc;
     acc.zero();
 #pragma unroll
@@ -6969,10 +7045,8 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         pixel_contrib<MODE>(acc, A.P, in[s], Y);
       }
     }
-    float v[kNP];
-#pragma unroll
-    for (int k = 0; k < kNP; k++) v[k] = 0.0f;
     acc.fold(v);
+#endif
     M3S_TSTAMP(1)
     {
       int idx;

@@ -73,6 +73,9 @@ namespace {
 #ifndef M3S_PK_DEPTH  // packed linearize: trips prefetched ahead through LDS (1 or 2)
 #define M3S_PK_DEPTH 1
 #endif
+#ifndef M3S_PK_SPARSE  // A/B build only: GN iterations 2.. over the valid pixels (linearize_sparse_kernel, slower)
+#define M3S_PK_SPARSE 0
+#endif
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
@@ -113,6 +116,8 @@ inline int64_t chunks_for(int64_t HW, int64_t E_loc, int64_t target = kTargetBlo
   ch = (ch + kBlockPix - 1) / kBlockPix * kBlockPix;
   return (HW + ch - 1) / ch;
 }
+// bytes per edge of the validity nibbles (HW / 4, padded: 8-B loads stay aligned)
+__host__ __device__ inline int64_t vmask_stride(int64_t HW) { return ((HW + 3) / 4 + 8 + 255) / 256 * 256; }
 inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
   int64_t ch = (HW + chunks - 1) / chunks;
   return (ch + kBlockPix - 1) / kBlockPix * kBlockPix;
@@ -137,7 +142,7 @@ inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cy
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      colsync, wgran, tail, gx, eorder, planes, total;
+      colsync, wgran, tail, gx, eorder, planes, vmask, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -202,6 +207,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   // target-side planes of every edge (4 planes = rays / points, the widest modes)
   L.planes = off;
   off = align_up(off + sizeof(float) * 4 * (size_t)E * (size_t)HW, 256);
+  L.vmask = off;  // the planes' pixel validity (linearize_sparse_kernel, A/B build only), 4 bits per byte per edge
+  off = align_up(off + (M3S_PK_SPARSE ? (size_t)vmask_stride(HW) * (size_t)E : 0), 256);
   L.total = off;
   return L;
 }
@@ -241,6 +248,7 @@ struct LinArgs {
   int64_t per, E_loc;      // block_task: 8 runs of `per` blocks; edges of the launch
   uint32_t cnt_base;       // edge_cnt arrivals before this launch in the call (edge_tail)
   float *planes;           // per-edge target-side planes (PixIn), [E_loc][kPlanes][HW]
+  uint8_t *vmask;          // per-edge pixel validity (sq != 0), 4 bits per byte, [E_loc][vmask_stride(HW)]
   float *partials;         // [task][36]
   uint32_t *edge_cnt;      // non-null: the last chunk of an edge to finish also finalizes it into fin
   double *fin;             // [E][kFin] per-edge blocks M L M^T, M g (fused finalize)
@@ -785,6 +793,12 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
           // (first call 258 -> 251 us at C3, 1172 -> 1134 us at 128 KFs rays)
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(pl + (size_t)k * HW + p0));
         }
+        if (A.vmask) {
+          constexpr int SQK = MODE == 2 ? 1 : NPL - 1;
+          A.vmask[(size_t)e_loc * vmask_stride(HW) + (p0 >> 2)] =
+              (uint8_t)((in[0].v[SQK] != 0.0f ? 1 : 0) | (in[1].v[SQK] != 0.0f ? 2 : 0) |
+                        (in[2].v[SQK] != 0.0f ? 4 : 0) | (in[3].v[SQK] != 0.0f ? 8 : 0));
+        }
       }
     }
   } else {
@@ -1250,6 +1264,159 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
       const f32x4 v = {in[0].v[k], in[1].v[k], in[2].v[k], in[3].v[k]};
       __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(pl + (size_t)k * HW + p0));
     }
+    if (A.vmask) {  // the 4 pixels' validity for linearize_sparse_kernel
+      constexpr int SQK = MODE == 2 ? 1 : NPL - 1;
+      const uint8_t nb = (uint8_t)((in[0].v[SQK] != 0.0f ? 1 : 0) | (in[1].v[SQK] != 0.0f ? 2 : 0) |
+                                   (in[2].v[SQK] != 0.0f ? 4 : 0) | (in[3].v[SQK] != 0.0f ? 8 : 0));
+      A.vmask[(size_t)e_loc * vmask_stride(HW) + (p0 >> 2)] = nb;
+    }
+  }
+  float sums[kNP];
+#pragma unroll
+  for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
+  acc.fold(sums);
+  store_partial(sums, A.partials + (size_t)b * kNP);
+  if (A.edge_cnt) edge_tail(A, e_loc, e);
+}
+
+// ------------------------------------------- sparse packed iterations --
+// Round 5 (M3S_PK_SPARSE): GN iterations 2.. of a call over the VALID pixels
+// only. A pixel whose sq plane is 0 (no valid match, Q / C under threshold,
+// calib z_i <= z_eps: a quarter of the C3 pixels) contributes exactly zero in
+// every iteration, yet the dense packed kernel computes it. The gathering
+// first iteration writes each pixel's validity (4 bits per byte, vmask);
+// here a block turns its chunk's bits into a list of valid pixels in LDS
+// (sub-batches of kSpSB pixels, increasing pixel order: deterministic), and
+// each wave takes 128-entry rounds of it (two pixels per lane, the pixel-pair
+// accumulation of the packed kernel): the entries' NPL planes and Xj floats
+// go by 4-B buffer_load ... lds into the wave's double-buffered slot one round
+// ahead, read back by inline-asm ds_reads (no compiler vmcnt wait on a DMA
+// target). A round's unused entries repeat a valid pixel at zero weight.
+// Same per-pixel products as linearize_packed_kernel, another summation
+// order (fp32 round-off). Measured slower, kept as an A/B build only
+// (profiles/r05/ab_lin_sparse_REJECTED.txt: 93 -> 129 us per C3 launch, sums
+// within 2e-8): the VALU it saves is lost to the loads, 2 (NPL + 3) 4-B DMA
+// instructions per two-pixel round where the dense kernel moves four pixels
+// of a plane in one 16-B instruction, and to the list reads between rounds.
+constexpr int kSpSB = 8192;  // pixels per list sub-batch (16 KB of LDS)
+__device__ int block_excl_scan(int v, int *wsum, int *total);
+template <int NF>
+__device__ __forceinline__ void sp_read(uint32_t a, float (&f)[2 * NF]) {  // the slot's 2 NF floats of this lane
+#pragma unroll
+  for (int q = 0; q < 2 * NF; q++) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(f[q]) : "v"(a), "i"(256 * q));
+  // the wait names every destination: no copy of a register before its data lands
+  if constexpr (NF == 6)
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
+                   "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11])
+                 :
+                 : "memory");
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
+                   "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11]), "+v"(f[12]), "+v"(f[13])
+                 :
+                 : "memory");
+}
+__device__ __forceinline__ int sp_list(uint32_t a) {  // one u16 list entry (inline asm: no DMA wait)
+  int v;
+  asm volatile("ds_read_u16 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+template <int MODE>
+__global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_PK_WAVES)
+    linearize_sparse_kernel(LinArgs A) {
+  if (*A.stop) return;
+  const int64_t b = block_task(A);
+  if (b < 0) return;
+  const int64_t e_loc = b / A.chunks;
+  const int64_t c = b - e_loc * A.chunks;
+  const int64_t e = A.edge_begin + e_loc;
+  const int64_t HW = A.HW;
+  const int ri = A.rank_i[e], rj = A.rank_j[e];
+  const Sim3Mat Tm = sim3_matrix(relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj)));
+  const ResidualParams P = kparams(A);
+  constexpr int NPL = PixIn<MODE>::kPlanes, SQK = MODE == 2 ? 1 : NPL - 1, NF = NPL + 3;
+  const float *Xs_j = A.Xs + (size_t)rj * HW * 3;
+  const float *pl = A.planes + (size_t)e_loc * NPL * HW;
+  const uint8_t *vm = A.vmask + (size_t)e_loc * vmask_stride(HW);
+  const int tid = threadIdx.x, ln = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NW = kThreads / 64;
+  __shared__ uint16_t list[kSpSB];
+  __shared__ int wsum[17];
+  __shared__ __attribute__((aligned(16))) float slot[NW][2][2 * NF][64];
+  __amdgpu_buffer_rsrc_t Rp[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; k++)
+    Rp[k] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pl + (size_t)k * HW), 0, (int)(4 * HW), 0x00020000);
+  const __amdgpu_buffer_rsrc_t Rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_j), 0, (int)(12 * HW), 0x00020000);
+  const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint16_t *)list);
+  AccumPP acc;
+  acc.zero();
+  const int p_begin = (int)(c * A.chunk_pix);
+  const int p_end = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
+  for (int sb = p_begin; sb < p_end; sb += kSpSB) {
+    const int sb_end = sb + kSpSB < p_end ? sb + kSpSB : p_end;
+    // 1. this sub-batch's valid pixels (offsets from sb) into the list, in
+    //    pixel order: thread t owns pixels sb + 32 t .. + 31 (8 nibble bytes)
+    const int pb = sb + 32 * tid;
+    uint64_t w8 = 0;
+    if (pb < sb_end) {
+      w8 = *reinterpret_cast<const uint64_t *>(vm + (pb >> 2));
+    }
+    // keep the low nibble of each byte, and only the pixels before sb_end
+    uint32_t bits = 0;  // pixel q of the thread's 32 -> bit q
+#pragma unroll
+    for (int by = 0; by < 8; by++) bits |= (uint32_t)((w8 >> (8 * by)) & 0xfu) << (4 * by);
+    if (pb + 32 > sb_end) bits &= pb < sb_end ? ((1u << (sb_end - pb)) - 1u) : 0u;
+    int tot = 0;
+    int off = block_excl_scan(__builtin_popcount(bits), wsum, &tot);
+    for (uint32_t v = bits; v; v &= v - 1) list[off++] = (uint16_t)(32 * tid + __builtin_ctz(v));
+    __syncthreads();
+    // 2. rounds of 128 entries, wave w taking rounds w, w + NW, ...
+    const int n = tot, R = (n + 127) / 128;
+    auto issue = [&](int r, int buf) {
+      const int e0 = 128 * r + 2 * ln;
+      const int i0 = sp_list(la + 2 * (e0 < n ? e0 : n - 1)), i1 = sp_list(la + 2 * (e0 + 1 < n ? e0 + 1 : n - 1));
+      const int p0 = sb + i0, p1 = sb + i1;
+#pragma unroll
+      for (int k = 0; k < NPL; k++) {
+        buf_lds4_nt(Rp[k], (__attribute__((address_space(3))) void *)(&slot[wv][buf][k][0]), 4 * p0, 0);
+        buf_lds4_nt(Rp[k], (__attribute__((address_space(3))) void *)(&slot[wv][buf][NF + k][0]), 4 * p1, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(Rx, (__attribute__((address_space(3))) void *)(&slot[wv][buf][NPL + k][0]), 4, 12 * p0 + 4 * k, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(Rx, (__attribute__((address_space(3))) void *)(&slot[wv][buf][NF + NPL + k][0]), 4, 12 * p1 + 4 * k, 0, 0, 0);
+      }
+    };
+    int buf = 0;
+    if (wv < R) issue(wv, 0);
+    for (int r = wv; r < R; r += NW, buf ^= 1) {
+      if (r + NW < R) {
+        issue(r + NW, buf ^ 1);
+        if constexpr (NF == 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      float f[2 * NF];
+      sp_read<NF>((uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const float *)&slot[wv][buf][0][ln]), f);
+      const int e0 = 128 * r + 2 * ln;
+      f32x2 in[NPL], X[3];
+#pragma unroll
+      for (int k = 0; k < NPL; k++) in[k] = f32x2{f[k], f[NF + k]};
+      if (e0 >= n) in[SQK].x = 0.0f;  // a repeated entry: zero weight
+      if (e0 + 1 >= n) in[SQK].y = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 3; k++) X[k] = f32x2{f[NPL + k], f[NF + NPL + k]};
+      f32x2 Y[3];
+      act2(Tm, X, Y);
+      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
+    }
+    __syncthreads();  // the list is rewritten by the next sub-batch
   }
   float sums[kNP];
 #pragma unroll
@@ -5430,6 +5597,8 @@ int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipSt
       launch_lin(linearize_kernel<MODE, false, true, true>, g, b, st, L);
     else
       launch_lin(linearize_kernel<MODE, false, false, true>, g, b, st, L);
+  } else if (M3S_PK_SPARSE && L.vmask) {
+    launch_lin(linearize_sparse_kernel<MODE>, g, b, st, L);
   } else {
     launch_lin(linearize_packed_kernel<MODE>, g, b, st, L);
   }
@@ -5726,7 +5895,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   void *ws = a->workspace;
   const int64_t E_loc = ee - eb;
   if (E_loc <= 0) return M3S_OK;
-  LinArgs L;
+  LinArgs L{};
   L.Twc = a->Twc;
   L.T_rel = nullptr;
   L.Xs = a->Xs;
@@ -5741,6 +5910,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
   L.partials = at<float>(ws, Ly.partials);
   L.planes = at<float>(ws, Ly.planes);
+  L.vmask = M3S_PK_SPARSE ? at<uint8_t>(ws, Ly.vmask) : nullptr;
   L.eorder = nullptr;
   L.cnt_base = 0;
   // fused finalize only over the whole edge set (single-GPU solve)
@@ -7381,7 +7551,7 @@ int track_impl(const m3s_track_args *a, int mode, void *stream) {
                                        reinterpret_cast<uint32_t *>(sync), (int)(sizeof(TrackSync) / 4),
                                        reinterpret_cast<u32x4 *>(partials), G * kTrkGran);
   if ((rc = launch_ok())) return rc;
-  LinArgs L;
+  LinArgs L{};
   memset(&L, 0, sizeof L);
   L.T_rel = ts->T_rel;
   L.Xs = a->Xk;

@@ -127,6 +127,10 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 // rows (n + 1 <= 16 kTailMaxT) and its scratch (dense bordered tail, L tiles,
 // W_k); see the kernel
 constexpr int kTailMaxT = 32;
+// border task flags of the concurrent tail launch: nc (nc + 1) / 2 tasks, nc < 16 kTailMaxT / 7
+constexpr int kBtFlagsMax = (16 * kTailMaxT / 7 + 1) * (16 * kTailMaxT / 7 + 2) / 2;
+// their offset in the colsync words (after the X_k chunk counters)
+inline int64_t kColsyncBtOff(int64_t m, int64_t slot_cap) { return 2 * (m + 1) + 16 + slot_cap + 2 * kTailMaxT + (m + 1); }
 inline size_t tail_z_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y', LgT, Z, then the granules
   const size_t nmax = 16 * kTailMaxT;
   return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2 + (size_t)kTailMaxT * 256 + nmax;
@@ -196,8 +200,8 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   L.parts = off;  // split update partials, at most slot_cap of them
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap], tail flags,
-                    // X_k chunk counters [m+1] (epoch-tagged, zeroed per call)
-  off = align_up(off + sizeof(int32_t) * (size_t)(3 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
+                    // X_k chunk counters [m+1], border task flags (epoch-tagged, zeroed per call)
+  off = align_up(off + sizeof(int32_t) * (size_t)(3 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT + kBtFlagsMax), 256);
   L.wgran = off;  // df_factor_kernel: W_k of every column as 16-B tagged granules (zeroed with colsync per call)
   off = align_up(off + (size_t)16 * 49 * (size_t)(m + 1), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
@@ -2360,7 +2364,15 @@ template <bool STAGE, bool SC1 = false>
 __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t *pl, const int *off, double *Lb,
                                             double *y, int r7, int c7, int lane49, int lane, int lane7, bool act49,
                                             double *stg, double *Ad = nullptr, int ld = 0,
-                                            const int32_t *wflag = nullptr, int want = 0, bool *ok = nullptr) {
+                                            const int32_t *wflag = nullptr, int want = 0, bool *ok = nullptr,
+                                            bool wt = false) {
+  // wt: write-through stores (a concurrent tail launch reads them after a flag)
+  auto put = [&](double *p, double v) {
+    if (wt)
+      st_sc1(p, v);
+    else
+      *p = v;
+  };
   const int32_t *dtr_ptr = pl + off[6], *dtr_slot = pl + off[7], *dtr_p = pl + off[8], *task_dst = pl + off[10],
                 *task_tr_ptr = pl + off[12], *tr_a = pl + off[13], *tr_b = pl + off[14];
   const int32_t *clq = pl + off[28];
@@ -2374,18 +2386,18 @@ __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t
     v = sub_products<STAGE, true, SC1>(v, Lb, dtr_slot, dtr_slot, q0, q1, r7, c7, lane49, lane, stg, wflag, want, ok);
     double bb = y[k * 7 + lane7];
     bb = sub_matvec<STAGE, false, SC1>(bb, Lb, dtr_slot, dtr_p, q0, q1, y, lane7, lane49, lane, stg);
-    if (act49) Lb[(size_t)k * 49 + lane] = v;
-    if (lane < 7) y[k * 7 + lane] = bb;
-    if (Ad && act49) Ad[(size_t)(7 * ci + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
+    if (act49) put(Lb + (size_t)k * 49 + lane, v);
+    if (lane < 7) put(y + k * 7 + lane, bb);
+    if (Ad && act49) put(Ad + (size_t)(7 * ci + r7 / 7) * ld + 7 * ci + c7 / 7, v);
   } else {
     const int task = ct0[ci] + ri - ci - 1, dst = task_dst[task];
     const int q0 = task_tr_ptr[task], q1 = bend[ci * nc + ri];
     double v = Lb[(size_t)dst * 49 + lane49];
     v = sub_products<STAGE, false, SC1>(v, Lb, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg, wflag, want, ok);
-    if (act49) Lb[(size_t)dst * 49 + lane] = v;
+    if (act49) put(Lb + (size_t)dst * 49 + lane, v);
     if (Ad && act49) {  // the block and its transpose (tail_llt_kernel reads whole 16x16 tiles)
-      Ad[(size_t)(7 * ri + r7 / 7) * ld + 7 * ci + c7 / 7] = v;
-      Ad[(size_t)(7 * ci + c7 / 7) * ld + 7 * ri + r7 / 7] = v;
+      put(Ad + (size_t)(7 * ri + r7 / 7) * ld + 7 * ci + c7 / 7, v);
+      put(Ad + (size_t)(7 * ci + c7 / 7) * ld + 7 * ri + r7 / 7, v);
     }
   }
 }
@@ -3131,6 +3143,7 @@ struct DfArgs {
   double *tail_A;
   int tail_ld;
   double *Wgr;     // [m][49] W_k as {value, epoch tag} 16-B granules (round 3)
+  int32_t *btflag;  // non-null: border task b publishes btflag[b] = epoch + 1 (the tail runs concurrently)
 };
 constexpr int kDfWaves = 4;
 #ifndef M3S_DF_WGRAN  // df_factor_kernel: OFF items take W_k from tagged granules (one round trip)
@@ -3253,8 +3266,12 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       // at 256 KFs after the last column was published)
       bool ok = true;
       border_task<true, true>(bt, nc, D.c0, pl, D.off, L, D.y, r7, c7, lane49, lane, lane7, act49, stg, D.tail_A,
-                              D.tail_ld, D.sdone, want, &ok);
+                              D.tail_ld, D.sdone, want, &ok, D.btflag != nullptr);
       if (!ok && lane == 0) set_fail(D.flags);
+      if (D.btflag) {  // the concurrent tail launch waits for its columns' border blocks (write-through above)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(D.btflag + bt, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -4121,6 +4138,7 @@ struct TailSync {
   int warm;        // 1: warm the diagonal factor's code on a dummy tile first (tail_diag_warm)
   int zinv;        // 1: back-substitution through Z = L^-1, a column per workgroup (tail_zinv_col, round 5)
   double *Zg;      // the tiles of Z, [tile (I, J)][64 lanes][4] (MFMA C layout)
+  const int32_t *btflag;  // non-null (round 5, concurrent launch): per border task epoch flags of df_factor_kernel
 };
 constexpr size_t kTailGranBytes = (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 64 * 4 * 16;
 
@@ -4645,6 +4663,7 @@ struct GArgs {
   int nx, n_pairs;
   int32_t *task, *comb, *fin, *xt_ready;  // ticket / ticket / counter / flag words (colsync; zeroed per call)
   int32_t *cnt;                           // [m] chunks of X_k done (colsync; zeroed per call)
+  const int32_t *sdone;                   // non-null: df_factor_kernel's slot flags (it runs concurrently)
 };
 constexpr int kGBat = 8;    // sparse ancestors' X_i loads in flight per lane
 constexpr int kGCapS = 24;  // sparse ancestors' L_ik staged in LDS per wave (the rest read from global)
@@ -4718,7 +4737,12 @@ __device__ void gcol_worker(const ColArgs &C, const GArgs &G) {
     }
     ns = min(ns, kGMaxS);
     wave_lds_fence();
-    // the factor is final (earlier launches): the ancestors' L_ik and W_k by plain loads
+    if (G.sdone) {  // df_factor_kernel runs beside this launch: column k's DIAG and blocks first
+      if (!g_poll(G.sdone + k, want) && lane == 0) set_fail(C.flags);
+      if (!g_wait_flags(G.sdone, col_slot, q0, q1, 0x7fffffff, want, lane) && lane == 0) set_fail(C.flags);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    // the factor is final: the ancestors' L_ik and W_k by plain loads
     for (int e = lane; e < 49 * min(ns, kGCapS); e += 64) Lk[e] = C.L[(size_t)col_slot[q0 + sq[e / 49]] * 49 + e % 49];
     if (lane < 49) Wk[lane] = C.Dinv[(size_t)k * 49 + lane];
     const int c = 64 * ch + lane;
@@ -4855,7 +4879,28 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
   };
   if (tid == 0) fail_s = 0, wready[0] = 0, wready[1] = 0, lready = 0;
   for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) yv[q] = 0.0;
+  if (S.btflag && wave == 0) {
+    // round 5, launched beside df_factor_kernel: the border blocks (ri, ci)
+    // of the pair's block columns ci, every row ri >= ci (one contiguous run
+    // of the column-major border tasks), then an acquire for the tile loads
+    const int nc = A.nc, cb0 = (16 * J0) / 7, cb1 = min(nc - 1, (16 * (J0 + jn) - 1) / 7);
+    const int t0 = cb0 * nc - cb0 * (cb0 - 1) / 2, t1 = cb1 * nc - cb1 * (cb1 - 1) / 2 + (nc - 1 - cb1);
+    int spins = 0;
+    for (int tb = t0; tb <= t1; tb += 64) {
+      const int t = tb + lane;
+      for (;;) {
+        const bool ok = t > t1 || __hip_atomic_load(S.btflag + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want;
+        if (__ballot(!ok) == 0) break;
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kColSpins) {
+          if (lane == 0) fail_s = 1;
+          break;
+        }
+      }
+    }
+  }
   __syncthreads();
+  if (S.btflag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // acc0[u]: tile (I, J0)^T; acc1[u]: tile (I, J1)^T (rows I >= J1)
   f64x4 acc0[kRC], acc1[kRC];
 #pragma unroll
@@ -5681,6 +5726,7 @@ struct Knobs {
   std::atomic<int> gcomb{1};           // 0: col_backsub_kernel after the tail instead of gcol_worker
   std::atomic<int> gcomb_wg{64};       // gcol_worker workgroups (at most; 64 measured best at 128 / 256 KFs)
   std::atomic<int> gcomb_min_nc{32};   // smallest dense tail (block columns) that takes the workers
+  std::atomic<int> tail_conc{0};       // 1: the tail launch beside df_factor_kernel on a second stream (slower)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -5704,6 +5750,7 @@ struct Knobs {
     env("M3S_GCOMB", gcomb);
     env("M3S_GCOMB_WG", gcomb_wg);
     env("M3S_GCOMB_MIN_NC", gcomb_min_nc);
+    env("M3S_TAIL_CONC", tail_conc);
 #endif
   }
 };
@@ -5727,6 +5774,7 @@ inline bool tail_zinv_knob() { return knobs().tail_zinv != 0; }
 inline bool gcomb_knob() { return knobs().gcomb != 0; }
 inline int gcomb_wg_knob() { return std::max(1, knobs().gcomb_wg.load()); }
 inline int gcomb_min_nc_knob() { return knobs().gcomb_min_nc.load(); }
+inline bool tail_conc_knob() { return knobs().tail_conc != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -5746,6 +5794,7 @@ constexpr int gcomb_wg_knob() { return 64; }
 // X_k recursion: 256 KFs (42-column tail) 0.751 -> 0.712 ms per 3-iteration
 // call, 128 KFs (a shorter tail) 0.493 -> 0.501 (profiles/r05/solve_ab_gcomb_rotated.txt)
 constexpr int gcomb_min_nc_knob() { return 32; }
+constexpr bool tail_conc_knob() { return false; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -5994,6 +6043,29 @@ void set_lds_attributes_once();
 
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
+// Round 5: the second stream of the concurrent tail launch (per thread and
+// device, created on first use, never destroyed: a stream per thread that
+// calls the backend)
+struct ConcStreams {
+  hipStream_t s2 = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  int dev = -1;
+};
+inline ConcStreams *conc_streams() {
+  thread_local ConcStreams R;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (R.s2 && R.dev == dev) return &R;
+  ConcStreams N;
+  if (hipStreamCreateWithFlags(&N.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&N.a, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&N.b, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  N.dev = dev;
+  R = N;
+  return &R;
+}
+
 int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *partials, int64_t chunks,
                   hipStream_t st, bool fin_ready = false) {
   const Layout Ly = gn_layout(a->N, a->HW, a->E);
@@ -6093,6 +6165,9 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       double *tail = at<double>(ws, Ly.tail);
       const int tld = 16 * kTailMaxT;
       bool gcomb_used = false;  // the tail launch also ran the sparse back-substitution
+      // the factor launches (df_factor_kernel; btf: the border tasks also
+      // publish per-task flags for a tail launch running beside it)
+      auto factor = [&](int32_t *btf) {
       if (df_path()) {
         // every block of the sparse columns and the tail border: one wave-level dataflow
         DfArgs F;
@@ -6114,6 +6189,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         F.tail_A = tail;
         F.tail_ld = tld;
         F.Wgr = at<double>(ws, Ly.wgran);
+        F.btflag = btf;
 #ifdef M3S_TEST_PATHS
         if (subtree_path() && meta.n_sub > 0) {
           // the sparse columns: one LDS workgroup per subtree; df_factor_kernel
@@ -6142,6 +6218,10 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         col_factor_kernel<<<g1, 256, 0, st>>>(C);
 #endif
       }
+      };
+      // the dense tail's launch on stream ts (btf: wait for the border tasks'
+      // flags, df_factor_kernel running beside it)
+      auto tailf = [&](hipStream_t ts, const int32_t *btf) {
       if (meta.nc > 0) {
         D.tail_A = tail;
         D.tail_ld = tld;
@@ -6168,6 +6248,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.warm = tail_warm_knob() ? 1 : 0;
           Y.zinv = tail_zinv_knob() ? 1 : 0;
           Y.Zg = tail + tail_z_offset_doubles();
+          Y.btflag = btf;
           const int TC = (7 * meta.nc + 15) / 16;
           // the sparse back-substitution on extra workgroups of the tail's
           // launch (gcol_worker) when there are sparse columns
@@ -6177,6 +6258,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           G.nx = ((1 + 7 * meta.nc) + 7) / 8 * 8;
           G.task = C.ctr + 8, G.comb = C.ctr + 9, G.fin = C.ctr + 10, G.xt_ready = C.ctr + 11;
           G.cnt = Y.tflag + 2 * kTailMaxT;
+          G.sdone = btf ? cs + 2 * (meta.m + 1) + 16 : nullptr;
           int nG = 0;
           if (gcomb_knob() && meta.nc >= gcomb_min_nc_knob() && tail_pair_path() && !Y.zinv && C.ncols > 0 &&
               !(subtree_path() && meta.n_sub > 0)) {
@@ -6187,14 +6269,41 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           const unsigned gt = (unsigned)(G.n_pairs + nG);
           if (tail_pair_path())
             if (((7 * meta.nc + 16) / 16 + 2) / 3 <= 7)  // tile rows TR: rows per wave of waves 1..3
-              tail_pair_kernel<7><<<gt, 64 * kTailNW, 0, st>>>(T, Y, C, G);
+              tail_pair_kernel<7><<<gt, 64 * kTailNW, 0, ts>>>(T, Y, C, G);
             else
-              tail_pair_kernel<(kTailMaxT + 2) / 3><<<gt, 64 * kTailNW, 0, st>>>(T, Y, C, G);
+              tail_pair_kernel<(kTailMaxT + 2) / 3><<<gt, 64 * kTailNW, 0, ts>>>(T, Y, C, G);
           else
-            tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
+            tail_cyc_kernel<<<TC, 64 * kTailNW, 0, ts>>>(T, Y);
         } else {
-          tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
+          tail_llt_kernel<<<1, 64 * kTailNW, 0, ts>>>(T);
         }
+      }
+      };
+      // Round 5: the tail launch beside df_factor_kernel on a second stream
+      // (knob tail_conc, test build): each tile-column pair starts once ITS
+      // border blocks are published instead of after the whole factor launch;
+      // the workers wait per column for df's slot flags. The tail launch goes
+      // first so its workgroups are resident before df's fill the chip.
+      // Correct (the GPU suite with it on) and slower: 256 KFs 0.717 -> 0.765
+      // ms, 128 KFs 0.500 -> 0.543 ms per 3-iteration call
+      // (profiles/r05/solve_ab_tail_conc_REJECTED.txt): the tail's 74
+      // one-per-CU workgroups and their polls beside df's dataflow, the
+      // write-through border stores and the cross-stream event pair cost more
+      // than the ~15 us of overlap.
+      const bool conc = tail_conc_knob() && df_path() && meta.nc > 0 && tail_cyc() && tail_pair_path() &&
+                        !tail_zinv_knob() && !(subtree_path() && meta.n_sub > 0);
+      ConcStreams *cr = conc ? conc_streams() : nullptr;
+      if (cr) {
+        int32_t *btf = cs + kColsyncBtOff(meta.m, Ly.slot_cap);
+        if (hipEventRecord(cr->a, st) != hipSuccess || hipStreamWaitEvent(cr->s2, cr->a, 0) != hipSuccess)
+          return M3S_ELAUNCH;
+        tailf(cr->s2, btf);
+        factor(btf);
+        if (hipEventRecord(cr->b, cr->s2) != hipSuccess || hipStreamWaitEvent(st, cr->b, 0) != hipSuccess)
+          return M3S_ELAUNCH;
+      } else {
+        factor(nullptr);
+        tailf(st, nullptr);
       }
 #ifdef M3S_TEST_PATHS
       if (subtree_path() && meta.n_sub > 0) {
@@ -7784,7 +7893,7 @@ int m3s_set_knob(const char *name, int value) {
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
              {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
-             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}, {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}, {"gcomb_min_nc", &k.gcomb_min_nc}
+             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}, {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}, {"gcomb_min_nc", &k.gcomb_min_nc}, {"tail_conc", &k.tail_conc}
 #endif
   };
   for (const auto &t : tab)

@@ -762,3 +762,23 @@ def test_broken_plan_through_workers_is_solve_failure(test_lib, be, knobs):
     T_ok, _, info = run_gpu(be, "rays", g, 1, 0.0)
     assert info[be.INFO_SOLVE_FAIL] == 0 and info[be.INFO_ITERS] == 1
     assert not np.array_equal(T_ok, g.T_init.data.numpy())
+
+
+@pytest.mark.parametrize("N", [140, 256])
+def test_tail_beside_factor_matches_sequential(test_lib, be, N, knobs):
+    """Round 5, test build: the dense tail launched on a second stream beside
+    df_factor_kernel (knob tail_conc: every tile-column pair waits for its own
+    border blocks' flags, the workers for df's slot flags) against the
+    sequential launches: the same operations on the same data, so the same
+    result bitwise; no failures."""
+    from mast3r_slam_amd import synthetic
+
+    g = synthetic.make_graph(N, 12, 16, seed=890 + N)
+    knobs("gcomb_min_nc", "0")  # the workers on too
+    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
+    knobs("tail_conc", "1")
+    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
+    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
+    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
+    np.testing.assert_array_equal(dx_a, dx_b)
+    np.testing.assert_array_equal(T_a, T_b)

@@ -207,38 +207,37 @@ __device__ inline Sim3f retract(const float *xi, const Sim3f &T) { return compos
 //   [ s^-1 R          0   0 ]
 //   [ s^-1 [t]x R     R   0 ]
 //   [ s^-1 t^T R      0   1 ]
-__device__ inline void adjT_inv_matrix(const float *Tp, double M[7][7]) {
+// Entry (r, c) of M = Adj(T)^-T (tau 0-2, phi 3-5, sigma 6): one lane per
+// entry (round 5: the edge finalize's 49 lanes form M side by side instead of
+// one lane forming all of it); adjT_inv_matrix is the same entries in a loop.
+__device__ inline double adjT_inv_entry(const float *Tp, int r, int c) {
+  if (r == 6 && c == 6) return 1.0;
+  if (c >= 3 && (r < 3 || r == 6 || c == 6)) return 0.0;
   const double tx = Tp[0], ty = Tp[1], tz = Tp[2];
   const double qx = Tp[3], qy = Tp[4], qz = Tp[5], qw = Tp[6];
-  const double is = 1.0 / (double)Tp[7];
   // rotation matrix of the (not renormalised) quaternion, matching actSO3's
-  // formula X + 2w(v x X) + v x (2 v x X) applied to unit vectors
-  double R[3][3];
-  R[0][0] = 1.0 - 2.0 * (qy * qy + qz * qz);
-  R[0][1] = 2.0 * (qx * qy - qw * qz);
-  R[0][2] = 2.0 * (qx * qz + qw * qy);
-  R[1][0] = 2.0 * (qx * qy + qw * qz);
-  R[1][1] = 1.0 - 2.0 * (qx * qx + qz * qz);
-  R[1][2] = 2.0 * (qy * qz - qw * qx);
-  R[2][0] = 2.0 * (qx * qz - qw * qy);
-  R[2][1] = 2.0 * (qy * qz + qw * qx);
-  R[2][2] = 1.0 - 2.0 * (qx * qx + qy * qy);
+  // formula X + 2w(v x X) + v x (2 v x X) applied to unit vectors (entries
+  // picked by selects, not an indexed array: r, c vary by lane -> scratch)
+  const double R00 = 1.0 - 2.0 * (qy * qy + qz * qz), R01 = 2.0 * (qx * qy - qw * qz),
+               R02 = 2.0 * (qx * qz + qw * qy), R10 = 2.0 * (qx * qy + qw * qz),
+               R11 = 1.0 - 2.0 * (qx * qx + qz * qz), R12 = 2.0 * (qy * qz - qw * qx),
+               R20 = 2.0 * (qx * qz - qw * qy), R21 = 2.0 * (qy * qz + qw * qx),
+               R22 = 1.0 - 2.0 * (qx * qx + qy * qy);
+  const int j = c >= 3 ? c - 3 : c;
+  const double R0 = j == 0 ? R00 : (j == 1 ? R01 : R02);  // column j of R
+  const double R1 = j == 0 ? R10 : (j == 1 ? R11 : R12);
+  const double R2 = j == 0 ? R20 : (j == 1 ? R21 : R22);
+  if (c >= 3) return r == 3 ? R0 : (r == 4 ? R1 : R2);  // the phi block
+  const double is = 1.0 / (double)Tp[7];
+  if (r < 3) return is * (r == 0 ? R0 : (r == 1 ? R1 : R2));
+  if (r == 3) return is * (ty * R2 - tz * R1);  // [t]x R
+  if (r == 4) return is * (tz * R0 - tx * R2);
+  if (r == 5) return is * (tx * R1 - ty * R0);
+  return is * (tx * R0 + ty * R1 + tz * R2);
+}
+__device__ inline void adjT_inv_matrix(const float *Tp, double M[7][7]) {
   for (int r = 0; r < 7; r++)
-    for (int c = 0; c < 7; c++) M[r][c] = 0.0;
-  const double t[3] = {tx, ty, tz};
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) {
-      M[r][c] = is * R[r][c];
-      M[3 + r][3 + c] = R[r][c];
-    }
-  // [t]x R
-  for (int c = 0; c < 3; c++) {
-    M[3][c] = is * (t[1] * R[2][c] - t[2] * R[1][c]);
-    M[4][c] = is * (t[2] * R[0][c] - t[0] * R[2][c]);
-    M[5][c] = is * (t[0] * R[1][c] - t[1] * R[0][c]);
-    M[6][c] = is * (t[0] * R[0][c] + t[1] * R[1][c] + t[2] * R[2][c]);
-  }
-  M[6][6] = 1.0;
+    for (int c = 0; c < 7; c++) M[r][c] = adjT_inv_entry(Tp, r, c);
 }
 
 // ----------------------------------------------------- fast scalar math --
@@ -641,6 +640,9 @@ __device__ __forceinline__ void pixel_contrib(ACC &acc, const ResidualParams &P,
 // scalar. Entries no row of the model touches stay compile-time zeros and
 // take no registers (rays 33, calib 32 live sums). Same per-pixel products as
 // pixel_contrib; the fp32 sums are per half, then combined in fold().
+#ifndef M3S_CAL25  // calib packed iterations: L(2,5) from L(0,3) and L(1,4) (AccumPP::cal25_fixup)
+#define M3S_CAL25 1
+#endif
 struct AccumPP {
   f32x2 s[kNP];
   __device__ __forceinline__ void zero() {
@@ -651,10 +653,19 @@ struct AccumPP {
 #pragma unroll
     for (int k = 0; k < kNP; k++) acc[k] += s[k].x + s[k].y;
   }
+  // Calib (packed backend iterations, M3S_CAL25): L(2,5) is not summed but
+  // formed here as -(L(0,3) + L(1,4)). With zi = 1/z, per pixel the u row
+  // adds -W_u x y zi to L(0,3) and +W_u x y zi to L(2,5), the v row +W_v x y zi
+  // to L(1,4) and -W_v x y zi to L(2,5), and the log-depth row has no column
+  // 5. Two fewer FMAs per pixel pair; only the fp32 rounding of L(2,5) differs.
+  __device__ __forceinline__ void cal25_fixup() {
+    s[kL + tri(2, 5)] = -(s[kL + tri(0, 3)] + s[kL + tri(1, 4)]);
+  }
   // one residual row (non-zero columns M, a[p] = the p-th entry) of both pixels;
   // COST false: no cost sum (the backend's solve never reads it; the tracker's
   // convergence rule does)
-  template <unsigned M, int K, bool COST = true>
+  // SKIP: a sum this row leaves out (one the caller forms afterwards)
+  template <unsigned M, int K, bool COST = true, int SKIP = -1>
   __device__ __forceinline__ void add(const f32x2 (&a)[K], f32x2 w, f32x2 e) {
     f32x2 wa[K];
 #pragma unroll
@@ -664,6 +675,7 @@ struct AccumPP {
 #pragma unroll
       for (int q = p; q < K; q++) {
         const int t = kL + tri(nth_col(M, p), nth_col(M, q));
+        if (t == SKIP) continue;
         s[t] = __builtin_elementwise_fma(wa[p], a[q], s[t]);
       }
     const f32x2 we = w * e;
@@ -796,9 +808,10 @@ __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParam
     const f32x2 au[5] = {zinv, -(x * zinv), -xyp, fma2(x, x, one), -y};  // kCalU: 0 2 3 4 5
     const f32x2 av[5] = {zinv, -(y * zinv), -fma2(y, y, one), xyp, x};  // kCalV: 1 2 3 4 5
     const f32x2 az[4] = {zinv, y, -x, one};                              // kCalZ: 2 3 4 6
-    acc.add<kCalU, 5, COST>(au, Wu, etu);
+    constexpr int kSkip25 = (M3S_CAL25 && !COST) ? kL + tri(2, 5) : -1;  // AccumPP::cal25_fixup
+    acc.add<kCalU, 5, COST, kSkip25>(au, Wu, etu);
     M3S_ROW_BARRIER();
-    acc.add<kCalV, 5, COST>(av, Wv, etv);
+    acc.add<kCalV, 5, COST, kSkip25>(av, Wv, etv);
     M3S_ROW_BARRIER();
     acc.add<kCalZ, 4, COST>(az, Wz, e2);
     M3S_ROW_BARRIER();

@@ -367,12 +367,16 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 // Per edge: H_jj = M L M^T and g_j = M l in fp64 (M = Adj(T_i)^-T), written
 // as fin[0:49] (row-major) and fin[49:56], from the edge's 36 local sums `es`
 // (LDS). Threads 0..63 of the block work; every thread of the block must call
-// it (block barriers).
+// it (block barriers). Mc: M already in LDS (the fused finalize forms it on
+// its second wave while the first loads the partials); else lanes 0..48 form
+// it here, one entry each.
 constexpr int kFin = 56;
-__device__ __forceinline__ void finalize_edge(const double *es, const float *Ti, double *fin) {
-  __shared__ double M[7][7], Lm[7][7], T1[7][7], l[7];
+__device__ __forceinline__ void finalize_edge(const double *es, const float *Ti, double *fin,
+                                              const double (*Mc)[7] = nullptr) {
+  __shared__ double Mo[7][7], Lm[7][7], T1[7][7], l[7];
+  const double(*M)[7] = Mc ? Mc : Mo;
   const int t = threadIdx.x;
-  if (t == 0) adjT_inv_matrix(Ti, M);
+  if (!Mc && t < 49) Mo[t / 7][t % 7] = adjT_inv_entry(Ti, t / 7, t % 7);
   if (t < 49) {
     const int a = t / 7, c = t % 7;
     Lm[a][c] = es[kL + tri(a < c ? a : c, a < c ? c : a)];
@@ -637,7 +641,7 @@ __device__ __forceinline__ void store_partial(const float *acc, float *out) {
 // in chunk order with sc1 loads (the same sums as edge_reduce_kernel /
 // finalize_edges_kernel) and writes fin[e] - the finalize launch disappears.
 __device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64_t e) {
-  __shared__ double esl[kNP];
+  __shared__ double esl[kNP], Ms[7][7];
   __shared__ int last_s;
   const int t = threadIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -665,9 +669,12 @@ __device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64
     for (; c < A.chunks; c++)
       acc += (double)__uint_as_float(__hip_atomic_load(p + (size_t)c * kNP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     esl[t] = acc;
+  } else if (t >= 64 && t < 64 + 49) {  // the second wave forms M under the first's loads
+    const int q = t - 64;
+    Ms[q / 7][q % 7] = adjT_inv_entry(A.Twc + 8 * (size_t)A.rank_i[e], q / 7, q % 7);
   }
   __syncthreads();
-  finalize_edge(esl, A.Twc + 8 * (size_t)A.rank_i[e], A.fin + (size_t)e * kFin);
+  finalize_edge(esl, A.Twc + 8 * (size_t)A.rank_i[e], A.fin + (size_t)e * kFin, Ms);
 }
 
 // Fused tracker solve: the iteration's last chunk to arrive (ticket =
@@ -859,6 +866,10 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t R, __attribute_
                                           int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 16, voff, soff, 0, 0);
 }
+__device__ __forceinline__ void buf_lds16_sc0(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
+                                              int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 16, voff, soff, 0, 1);
+}
 // A buffer offset past every resource's range (num_records < 2^31): the load
 // returns zeros and makes no memory access.
 constexpr int kFarOff = 0x7fff0000;
@@ -993,23 +1004,35 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
     // zeros with no memory access. The buffer range check covers voffset (+
     // the instruction offset), not soffset, so the wave-uniform trip base in
     // soffset alone would let them read past the last plane / pointmap.
-    int vp = vo_p, vx = vo_x;
+    // Round 5: the partial trip has loads of its own with other cache bits
+    // (sc0, no nt): with the same intrinsic calls on both sides the compiler
+    // merged the two paths into per-lane selects of the offsets on every trip
+    // (round 4: 277 -> 283 VALU per calib trip, tools/isa_loop.py).
     if (pw + kPixPerThread * 64 > pend) {  // wave-uniform: the full trips keep the fixed offsets
       const bool out = pw + kPixPerThread * ln >= pend;
-      vp = out ? kFarOff : vo_p;
-      vx = out ? kFarOff : vo_x;
+      const int vp = out ? kFarOff : vo_p, vx = out ? kFarOff : vo_x;
+#pragma unroll
+      for (int k = 0; k < NPL; k++)
+        buf_lds16_sc0(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vp, 4 * pw);
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+        buf_lds16_sc0(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vx, 12 * pw + 16 * k);
+      return;
     }
 #pragma unroll
     for (int k = 0; k < NPL; k++)
-      buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vp, 4 * pw);
+      buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vo_p, 4 * pw);
 #pragma unroll
     for (int k = 0; k < 3; k++)
-      buf_lds16(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vx, 12 * pw + 16 * k);
+      buf_lds16(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vo_x, 12 * pw + 16 * k);
   };
-  int pw = (int)p_begin + kPixPerThread * 64 * wv;
-  if (pw < pend) issue(pw, 0);
-  if (DEPTH > 1 && pw + kBlockPix < pend) issue(pw + kBlockPix, 1 % DEPTH);
-  for (int trip = 0; pw < pend; pw += kBlockPix, trip++) {
+  int pw0 = (int)p_begin + kPixPerThread * 64 * wv;
+  if (pw0 < pend) issue(pw0, 0);
+  if (DEPTH > 1 && pw0 + kBlockPix < pend) issue(pw0 + kBlockPix, 1 % DEPTH);
+  // One trip; PARTIAL: the wave's last trip runs past the chunk's end. The
+  // full trips are a loop of their own and the partial one is peeled after
+  // it, so the full trips carry no per-lane end test (2 VALU per trip).
+  auto trip_body = [&](const int pw, const int trip, const bool PARTIAL) {  // (inlined: PARTIAL folds)
     const int cur = DEPTH > 1 ? (trip & 1) : 0;
     if (DEPTH > 1 && pw + kBlockPix < pend) {
       // this trip's loads are done once at most the next trip's NPL + 3 are in flight
@@ -1020,7 +1043,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
     }
     // lanes past the chunk's end (a partial last trip only) read back zeros
     // from the resources and take no part (their exec bit is off)
-    if (pw + kPixPerThread * ln >= pend) continue;
+    if (PARTIAL && pw + kPixPerThread * ln >= pend) return;
 #if M3S_PP && M3S_PP_LDS
     // each pixel pair's operands are read from the LDS slot just before its
     // math (8-B reads: 2 NPL + 6 VGPRs live instead of 4 (NPL + 3)); the slot
@@ -1069,10 +1092,16 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
     if (pw + DEPTH * kBlockPix < pend) issue(pw + DEPTH * kBlockPix, cur);
     do_trip(pv, xv);
 #endif
-  }
+  };
+  int trip = 0;
+  for (; pw0 + kPixPerThread * 64 <= pend; pw0 += kBlockPix, trip++) trip_body(pw0, trip, false);
+  if (pw0 < pend) trip_body(pw0, trip, true);
   float sums[kNP];
 #pragma unroll
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
+#if M3S_PP
+  if constexpr (MODE == 2 && M3S_CAL25) acc.cal25_fixup();
+#endif
   acc.fold(sums);
   sums[0] += sink;
   store_partial(sums, A.partials + (size_t)b * kNP);
@@ -1425,6 +1454,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   float sums[kNP];
 #pragma unroll
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
+  if constexpr (MODE == 2 && M3S_CAL25) acc.cal25_fixup();
   acc.fold(sums);
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);

@@ -69,7 +69,7 @@ def main():
         d12 = ((es2[:, :35] - es[:, :35]).abs().max() / es[:, :35].abs().max()).item()
         print(f"{os.path.basename(p)}: max rel diff vs first: gathering call {err:.2e}, packed call {err2:.2e};"
               f" packed vs gathering call {d12:.2e}")
-    reps, rounds = 20, 5
+    reps, rounds = 20, int(os.environ.get("AB_ROUNDS", "5"))
     times = {p: [] for p in libs}
     first = {p: [] for p in libs}
     trio = list(zip(libs, handles, wargs))

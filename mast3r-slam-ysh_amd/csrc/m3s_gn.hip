@@ -1132,6 +1132,10 @@ __device__ __forceinline__ void buf_lds4_nt(__amdgpu_buffer_rsrc_t R, __attribut
                                             int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 4, voff, soff, 0, 2);
 }
+__device__ __forceinline__ void buf_lds4_sc0(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
+                                             int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 4, voff, soff, 0, 1);
+}
 struct GSlot {
   uint32_t vb;
   f32x4 q, x0, x1, x2, c;
@@ -1194,16 +1198,18 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
   const int pend = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
   auto issue = [&](int pw, bool far) {  // pw: the wave's first pixel of the trip
     // a partial last trip: its lanes past the chunk's end load from kFar too
-    // (the range check covers voffset, not the trip base in soffset)
+    // (the range check covers voffset, not the trip base in soffset); loads
+    // of their own with other cache bits (sc0, no nt), so that the compiler
+    // does not merge the two paths into per-lane offset selects on every trip
     if (!far && pw + kPixPerThread * 64 > pend) {
       const bool out = pw + kPixPerThread * ln >= pend;
-      buf_lds4_nt(Rv, L3(kGsValid), out ? kFar : v4, pw);
-      buf_lds16_nt(Rq, L3(kGsQ), out ? kFar : v16, 4 * pw);
-      buf_lds16_nt(Ri, L3(kGsIdx), out ? kFar : vi0, (i64 ? 8 : 4) * pw);
-      buf_lds16_nt(Ri, L3(kGsIdx + 1024), out ? kFar : vi1, 8 * pw);
+      buf_lds4_sc0(Rv, L3(kGsValid), out ? kFar : v4, pw);
+      buf_lds16_sc0(Rq, L3(kGsQ), out ? kFar : v16, 4 * pw);
+      buf_lds16_sc0(Ri, L3(kGsIdx), out ? kFar : vi0, (i64 ? 8 : 4) * pw);
+      buf_lds16_sc0(Ri, L3(kGsIdx + 1024), out ? kFar : vi1, 8 * pw);
 #pragma unroll
-      for (int k = 0; k < 3; k++) buf_lds16(Rx, L3(kGsXj + 1024 * k), out ? kFar : v48, 12 * pw + 16 * k);
-      buf_lds16(Rc, L3(kGsCj), out ? kFar : v16, 4 * pw);
+      for (int k = 0; k < 3; k++) buf_lds16_sc0(Rx, L3(kGsXj + 1024 * k), out ? kFar : v48, 12 * pw + 16 * k);
+      buf_lds16_sc0(Rc, L3(kGsCj), out ? kFar : v16, 4 * pw);
       return;
     }
     buf_lds4_nt(Rv, L3(kGsValid), far ? kFar : v4, pw);
@@ -1251,12 +1257,15 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
 #else
       id[s4] = vm[s4] ? (int)ids[s4] : 0;
 #endif
+      // 12 id on the full-rate 24-bit multiply (v_mul_lo_u32 is quarter rate;
+      // the host takes this kernel only for HW <= 2^24)
+      const int o12 = (int)__umul24((unsigned)id[s4], 12u);
       if (MODE == M3S_MODE_CALIB) {
-        gx[s4][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, 12 * id[s4] + 8, 0, 0));
+        gx[s4][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, o12 + 8, 0, 0));
       } else {
 #pragma unroll
         for (int k = 0; k < 3; k++)
-          gx[s4][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, 12 * id[s4] + 4 * k, 0, 0));
+          gx[s4][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, o12 + 4 * k, 0, 0));
       }
       gc[s4] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RCi, 4 * id[s4], 0, 0));
     }
@@ -1273,12 +1282,15 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
       const bool ok = vm[s4] && (qs[s4] > P.Q_thresh) && (gc[s4] > P.C_thresh) && (cjs[s4] > P.C_thresh);
       int u_t = 0, v_t = 0;
       if (MODE == M3S_MODE_CALIB) {  // gather_pixel's ind_Xi % width, ind_Xi / width
+        // products on the full-rate 24-bit multiply (row < 2^15, width <
+        // 2^16), not the quarter-rate v_mul_lo_u32
         const int iid = id[s4];
+        const unsigned w = (unsigned)P.width;
         int vv = (int)((float)iid * (1.0f / (float)P.width));
-        if (vv * P.width > iid) vv--;
-        if ((vv + 1) * P.width <= iid) vv++;
+        if (__umul24((unsigned)vv, w) > iid) vv--;
+        if (__umul24((unsigned)vv + 1u, w) <= iid) vv++;
         v_t = vv;
-        u_t = iid - vv * P.width;
+        u_t = iid - __umul24((unsigned)vv, w);
       }
       in[s4] = make_pixin<MODE>(P, gx[s4], ok, qs[s4], u_t, v_t);
     }
@@ -2073,6 +2085,25 @@ __device__ __forceinline__ bool wait_lanes(const int32_t *flag, int idx, bool ac
 // wflag (staged sc1 path only): wait for each batch's blocks (flag[slot] ==
 // want) just before loading them, so the sums of the blocks that are ready
 // early run while the later ones are still being produced; *ok &= no timeout
+// Slot / vector offsets of the LDS-resident update lists on the full-rate
+// 24-bit multiply: the index load -> address -> block load chain of every
+// update is on the factor's critical path, and v_mul_lo_u32 is quarter rate
+// (slot < 2^24 / 49 for every plan this library builds)
+// (inline asm: from __umul24 the compiler formed a mask and a v_mul_lo_u32
+// of the 392-byte stride again)
+__device__ __forceinline__ uint32_t vmul_u24(uint32_t k, uint32_t a) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(k), "v"(a));
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ const T *blk49(const T *Lb, int s) {  // Lb + 49 s
+  return reinterpret_cast<const T *>(reinterpret_cast<const char *>(Lb) + vmul_u24(49u * sizeof(T), (uint32_t)s));
+}
+template <typename T>
+__device__ __forceinline__ const T *vec7(const T *y, int s) {  // y + 7 s
+  return reinterpret_cast<const T *>(reinterpret_cast<const char *>(y) + vmul_u24(7u * sizeof(T), (uint32_t)s));
+}
 template <bool STAGE, bool SAME, bool SC1 = false>
 __device__ __forceinline__ double sub_products(double v, const double *Lb, const int32_t *sa,
                                                const int32_t *sb, int q0, int q1, int r7, int c7,
@@ -2088,8 +2119,8 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
       const double *A[4], *B[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        A[u] = Lb + (size_t)sa[q + u] * 49;
-        B[u] = SAME ? A[u] : Lb + (size_t)sb[q + u] * 49;
+        A[u] = blk49(Lb, sa[q + u]);
+        B[u] = SAME ? A[u] : blk49(Lb, sb[q + u]);
       }
       double sx[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -2100,8 +2131,8 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
       for (int u = 0; u < 4; u++) v -= sx[u];
     }
     for (; q + 1 < q1; q += 2) {
-      const double *A0 = Lb + (size_t)sa[q] * 49, *A1 = Lb + (size_t)sa[q + 1] * 49;
-      const double *B0 = SAME ? A0 : Lb + (size_t)sb[q] * 49, *B1 = SAME ? A1 : Lb + (size_t)sb[q + 1] * 49;
+      const double *A0 = blk49(Lb, sa[q]), *A1 = blk49(Lb, sa[q + 1]);
+      const double *B0 = SAME ? A0 : blk49(Lb, sb[q]), *B1 = SAME ? A1 : blk49(Lb, sb[q + 1]);
       double s0 = 0.0, s1 = 0.0;
 #pragma unroll
       for (int mm = 0; mm < 7; mm++) {
@@ -2112,7 +2143,7 @@ __device__ __forceinline__ double sub_products(double v, const double *Lb, const
       v -= s1;
     }
     if (q < q1) {
-      const double *A0 = Lb + (size_t)sa[q] * 49, *B0 = SAME ? A0 : Lb + (size_t)sb[q] * 49;
+      const double *A0 = blk49(Lb, sa[q]), *B0 = SAME ? A0 : blk49(Lb, sb[q]);
       double s0 = 0.0;
 #pragma unroll
       for (int mm = 0; mm < 7; mm++) s0 += A0[r7 + mm] * B0[c7 + mm];
@@ -2181,7 +2212,7 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
     for (; q + 3 < q1; q += 4) {  // (as sub_products: four in flight, subtracted in list order)
       const double *A[4], *yv[4];
 #pragma unroll
-      for (int u = 0; u < 4; u++) A[u] = Lb + (size_t)slot[q + u] * 49, yv[u] = y + (size_t)vidx[q + u] * 7;
+      for (int u = 0; u < 4; u++) A[u] = blk49(Lb, slot[q + u]), yv[u] = vec7(y, vidx[q + u]);
       double tx[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int mm = 0; mm < 7; mm++)
@@ -2191,8 +2222,8 @@ __device__ __forceinline__ double sub_matvec(double acc, const double *Lb, const
       for (int u = 0; u < 4; u++) acc -= tx[u];
     }
     for (; q < q1; q++) {
-      const double *A = Lb + (size_t)slot[q] * 49;
-      const double *yv = y + (size_t)vidx[q] * 7;
+      const double *A = blk49(Lb, slot[q]);
+      const double *yv = vec7(y, vidx[q]);
       double t0 = 0.0;
 #pragma unroll
       for (int mm = 0; mm < 7; mm++) t0 += (TRANS ? A[mm * 7 + lane7] : A[lane7 * 7 + mm]) * yv[mm];
@@ -5666,7 +5697,7 @@ int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipSt
     else
       linearize_kernel<MODE, TRACK, false, false><<<g, b, 0, st>>>(L);
   } else if (pack == 1) {
-    if (vec && M3S_GATHER_LDS && gather_lds_path())
+    if (vec && M3S_GATHER_LDS && gather_lds_path() && L.HW <= (int64_t(1) << 24))  // (24-bit index products)
       launch_lin(linearize_gather_kernel<MODE>, g, b, st, L);
     else if (vec)
       launch_lin(linearize_kernel<MODE, false, true, true>, g, b, st, L);

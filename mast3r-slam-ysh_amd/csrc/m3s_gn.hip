@@ -2000,6 +2000,10 @@ __device__ __forceinline__ void wave_lds_fence() {
 #endif
 constexpr int kStage = M3S_STAGE;                  // updates per staged batch
 constexpr int kSplitUpdates = M3S_SPLIT_UPDATES;   // updates per PART item (global factors)
+#ifndef M3S_LDS_SPLIT  // updates per PART item on the LDS-resident path (0: none)
+#define M3S_LDS_SPLIT 0
+#endif
+constexpr int kLdsSplit = M3S_LDS_SPLIT;
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_TR  // dense-tail trailing update tile, in 7x7 blocks
 #define M3S_TAIL_TR 2
@@ -6525,6 +6529,8 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
     const bool chip_path = global_factor && cols_path() && P.m <= 512 && (P.nc == 0 || 7 * P.nc + 1 <= 16 * kTailMaxT);
     if (global_factor && !chip_path)  // split long update lists for the staged global-factor products
       build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1, dense_tail_min(), true);
+    else if (!chip_path && kLdsSplit > 0)  // (A/B: PART items on the LDS-resident path too)
+      build_sparse_plan((int)a->N, ri, rj, P, kLdsSplit, Ly.slot_cap - 1, dense_tail_min(), true);
     else if (!chip_path)
       schedule_plan_items(P);
     PlanImage img;

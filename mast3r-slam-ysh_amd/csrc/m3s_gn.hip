@@ -1132,10 +1132,6 @@ __device__ __forceinline__ void buf_lds4_nt(__amdgpu_buffer_rsrc_t R, __attribut
                                             int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 4, voff, soff, 0, 2);
 }
-__device__ __forceinline__ void buf_lds4_sc0(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
-                                             int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(R, lds, 4, voff, soff, 0, 1);
-}
 struct GSlot {
   uint32_t vb;
   f32x4 q, x0, x1, x2, c;
@@ -1198,18 +1194,19 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
   const int pend = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
   auto issue = [&](int pw, bool far) {  // pw: the wave's first pixel of the trip
     // a partial last trip: its lanes past the chunk's end load from kFar too
-    // (the range check covers voffset, not the trip base in soffset); loads
-    // of their own with other cache bits (sc0, no nt), so that the compiler
-    // does not merge the two paths into per-lane offset selects on every trip
+    // (the range check covers voffset, not the trip base in soffset). (Round
+    // 5: loads of their own here, as in the packed kernel, made the compiler's
+    // counted waits after the refill conservative — vmcnt(3) behind the 8
+    // refill loads, tests/test_isa.py — so this path stays merged.)
     if (!far && pw + kPixPerThread * 64 > pend) {
       const bool out = pw + kPixPerThread * ln >= pend;
-      buf_lds4_sc0(Rv, L3(kGsValid), out ? kFar : v4, pw);
-      buf_lds16_sc0(Rq, L3(kGsQ), out ? kFar : v16, 4 * pw);
-      buf_lds16_sc0(Ri, L3(kGsIdx), out ? kFar : vi0, (i64 ? 8 : 4) * pw);
-      buf_lds16_sc0(Ri, L3(kGsIdx + 1024), out ? kFar : vi1, 8 * pw);
+      buf_lds4_nt(Rv, L3(kGsValid), out ? kFar : v4, pw);
+      buf_lds16_nt(Rq, L3(kGsQ), out ? kFar : v16, 4 * pw);
+      buf_lds16_nt(Ri, L3(kGsIdx), out ? kFar : vi0, (i64 ? 8 : 4) * pw);
+      buf_lds16_nt(Ri, L3(kGsIdx + 1024), out ? kFar : vi1, 8 * pw);
 #pragma unroll
-      for (int k = 0; k < 3; k++) buf_lds16_sc0(Rx, L3(kGsXj + 1024 * k), out ? kFar : v48, 12 * pw + 16 * k);
-      buf_lds16_sc0(Rc, L3(kGsCj), out ? kFar : v16, 4 * pw);
+      for (int k = 0; k < 3; k++) buf_lds16(Rx, L3(kGsXj + 1024 * k), out ? kFar : v48, 12 * pw + 16 * k);
+      buf_lds16(Rc, L3(kGsCj), out ? kFar : v16, 4 * pw);
       return;
     }
     buf_lds4_nt(Rv, L3(kGsValid), far ? kFar : v4, pw);

@@ -286,3 +286,31 @@ def test_tracker_polls_keep_their_loads_without_sleep(tmp_path):
             assert any(SC1_LOAD.match(t) for t in body), f"{name}: poll at {addr:#x} lost its load"
         n += 1
     assert n >= 8, n
+
+
+# ------------------------------------------------- packed-kernel VALU budget --
+# Round 5 (tools/isa_loop.py): the calib trip of
+# linearize_packed_kernel<2> executes 268 VALU instructions per 4-pixel trip
+# (283 in round 4, where a partial-trip guard had been merged into per-lane
+# selects on every trip). This pins the count so that such a regression shows
+# up here instead of in a round's timing: the innermost natural loop around the
+# trip's LDS-DMA refill, without the blocks of the partial trip's own refill
+# (sc0 loads, taken at most once per wave).
+@pytest.mark.parametrize("mode,budget", [(2, 268), (1, 324), (0, 171)])
+def test_packed_trip_valu_budget(disasm, mode, budget):
+    fns = functions(disasm)
+    name = next(n for n in fns if f"linearize_packed_kernelILi{mode}EEEvNS_7LinArgsE" in n)
+    ins = fns[name]
+    blocks, loops = natural_loops(ins)
+    refill = [k for k, (s, e) in enumerate(blocks)
+              if any(VMEM.match(ins[i][1]) and ins[i][1].endswith(" nt lds") for i in range(s, e))]
+    assert refill, "no LDS-DMA refill in the packed kernel"
+    def has_pk(b):
+        return any(ins[i][1].startswith("v_pk_fma_f32") for q in b for i in range(*blocks[q]))
+    around = [b for _, b in loops if any(k in b for k in refill) and has_pk(b)]
+    assert around, "no trip loop around the refill"
+    body = min(around, key=len)
+    rare = {q for q in body if any(ins[i][1].endswith(" sc0 lds") for i in range(*blocks[q]))}
+    valu = sum(1 for q in body - rare for i in range(*blocks[q]) if ins[i][1].startswith("v_"))
+    print(f"mode {mode}: {valu} VALU per trip in the loop's common blocks")
+    assert valu <= budget, (mode, valu, budget)

@@ -200,13 +200,15 @@ int m3s_debug_stamps(int which, int64_t *out);
  * elements, asynchronously on `stream`. Device arrays; Sim3 = 8 floats
  * (t, q_xyzw, s), tangent = 7 floats (tau, phi, sigma), point = 3 floats.
  *   op 0 exp(a: tangent)            -> out Sim3      (expSim3 :323-390)
- *   op 1 retract(a: tangent, b: T)  -> out Exp(a) b  (retrSim3 :392-413)
+ *   op 1 retract(a: tangent, b: T)  -> out Exp(a) b  (retrSim3 :392-413), the
+ *        backend's retraction: evaluated in fp64, rounded once
  *   op 2 compose(a, b)              -> out a * b
  *   op 3 inverse(a)                 -> out a^-1
  *   op 4 relative(a, b)             -> out a^-1 b    (relSim3 :252-272)
  *   op 5 act(a, b: point)           -> out point     (actSim3 :207-219)
  *   op 6 act as the 3x4 matrix form the linearize kernels use -> out point
- *   op 7 Adj(a)^-T as a row-major 7x7 (apply_Sim3_adj_inv :274-297) -> out 49 */
+ *   op 7 Adj(a)^-T as a row-major 7x7 (apply_Sim3_adj_inv :274-297) -> out 49
+ *   op 8 retract as op 1 in the reference's fp32 arithmetic (the tracker's) */
 int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n, void *stream);
 /* Solver knobs (experiments / A/B tests). Defaults are the measured best;
  * the environment (M3S_PLAN_CACHE, M3S_DENSE, M3S_DENSE_TAIL_MIN, M3S_COLS,

@@ -199,8 +199,83 @@ __device__ inline Sim3f exp_sim3(const float *xi) {
   return E;
 }
 
-// T <- Exp(xi) T  (retrSim3 / pose_retr_kernel, gn_kernels.cu:392-453)
+// T <- Exp(xi) T  (retrSim3 / pose_retr_kernel, gn_kernels.cu:392-453), in the
+// reference's fp32 arithmetic: the tracker's update (its parity is pinned by
+// the reference tracker's own outputs, tests/golden)
 __device__ inline Sim3f retract(const float *xi, const Sim3f &T) { return compose(exp_sim3(xi), T); }
+
+// The backend's retraction: the same map, the same branches and formulas,
+// evaluated in fp64 from the fp32 step and pose and rounded once (round 6).
+// The reference's fp32 expSim3 (gn_kernels.cu:323-389) is ill-conditioned
+// for small steps: C = (e^sigma - 1) / sigma keeps the rounding of e^sigma
+// (6e-8) over |sigma|, 0.6 % of C at sigma = 1e-5, so t = W tau moves by up to
+// 6e-3 |tau| with the last bit of sigma; A and B lose more when theta and
+// sigma are both small. In fp64 those terms are exact to ~1e-16 / |sigma|
+// and the pose lands within an fp32 ulp of Exp(xi) T
+// (tests/test_gpu_sim3.py::test_backend_retraction_same_inputs_three_ways).
+// One lane per pose, once per GN iteration: the cost is off the hot loop.
+__device__ inline Sim3f retract_f64(const float *xi, const Sim3f &T) {
+  const double EPSV = 1e-6;
+  const double tau[3] = {xi[0], xi[1], xi[2]};
+  const double phi[3] = {xi[3], xi[4], xi[5]};
+  const double sg = xi[6];
+  const double scale = exp(sg);
+  const double th2 = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  const double th = sqrt(th2);
+  double im, re;
+  if (th2 < EPSV) {
+    const double th4 = th2 * th2;
+    im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
+    re = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
+  } else {
+    im = sin(0.5 * th) / th;
+    re = cos(0.5 * th);
+  }
+  const double eq[4] = {im * phi[0], im * phi[1], im * phi[2], re};
+  double A, B, C;
+  if (fabs(sg) < EPSV) {
+    C = 1.0;
+    if (th < EPSV) {
+      A = 0.5;
+      B = 1.0 / 6.0;
+    } else {
+      A = (1.0 - cos(th)) / th2;
+      B = (th - sin(th)) / (th2 * th);
+    }
+  } else {
+    C = expm1(sg) / sg;
+    if (th < EPSV) {
+      const double sg2 = sg * sg;
+      A = ((sg - 1.0) * scale + 1.0) / sg2;
+      B = (scale * 0.5 * sg2 + scale - 1.0 - sg * scale) / (sg2 * sg);
+    } else {
+      const double a = scale * sin(th), b = scale * cos(th), c = th2 + sg * sg;
+      A = (a * sg + (1.0 - b) * th) / (th * c);
+      B = (C - ((b - 1.0) * sg + a * th) / c) / th2;
+    }
+  }
+  const double p1[3] = {phi[1] * tau[2] - phi[2] * tau[1], phi[2] * tau[0] - phi[0] * tau[2],
+                        phi[0] * tau[1] - phi[1] * tau[0]};
+  const double p2[3] = {phi[1] * p1[2] - phi[2] * p1[1], phi[2] * p1[0] - phi[0] * p1[2],
+                        phi[0] * p1[1] - phi[1] * p1[0]};
+  // compose: q = eq * T.q, t = et + scale R(eq) T.t, s = scale T.s
+  const double bq[4] = {T.q[0], T.q[1], T.q[2], T.q[3]};
+  const double bt[3] = {T.t[0], T.t[1], T.t[2]};
+  Sim3f R;
+  R.q[0] = (float)(eq[3] * bq[0] + eq[0] * bq[3] + eq[1] * bq[2] - eq[2] * bq[1]);
+  R.q[1] = (float)(eq[3] * bq[1] - eq[0] * bq[2] + eq[1] * bq[3] + eq[2] * bq[0]);
+  R.q[2] = (float)(eq[3] * bq[2] + eq[0] * bq[1] - eq[1] * bq[0] + eq[2] * bq[3]);
+  R.q[3] = (float)(eq[3] * bq[3] - eq[0] * bq[0] - eq[1] * bq[1] - eq[2] * bq[2]);
+  const double ux = 2.0 * (eq[1] * bt[2] - eq[2] * bt[1]);
+  const double uy = 2.0 * (eq[2] * bt[0] - eq[0] * bt[2]);
+  const double uz = 2.0 * (eq[0] * bt[1] - eq[1] * bt[0]);
+  const double rt[3] = {bt[0] + eq[3] * ux + (eq[1] * uz - eq[2] * uy),
+                        bt[1] + eq[3] * uy + (eq[2] * ux - eq[0] * uz),
+                        bt[2] + eq[3] * uz + (eq[0] * uy - eq[1] * ux)};
+  for (int c = 0; c < 3; c++) R.t[c] = (float)(C * tau[c] + A * p1[c] + B * p2[c] + scale * rt[c]);
+  R.s = (float)(scale * (double)T.s);
+  return R;
+}
 
 // M = Adj(T_i)^-T as a dense 7x7 (double), so that J_j = M J_local
 // (apply_Sim3_adj_inv, gn_kernels.cu:274-297):

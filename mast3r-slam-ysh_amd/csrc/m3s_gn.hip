@@ -1580,7 +1580,7 @@ __device__ void finish_step(const double *xs, float *dxs, float *nrm, int n, flo
   __syncthreads();
   for (int p = tid; p < (int)(N - 1); p += nt) {
     const Sim3f T = load_sim3(Twc + 8 * (size_t)(p + 1));
-    store_sim3(Twc + 8 * (size_t)(p + 1), retract(dxs + 7 * p, T));
+    store_sim3(Twc + 8 * (size_t)(p + 1), retract_f64(dxs + 7 * p, T));
   }
   if (tid == 0) {
     float s = 0.0f;
@@ -3011,7 +3011,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     float xi[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) xi[q] = dx_lds ? dxl[p * 7 + q] : D.dx_out[p * 7 + q];
-    store_sim3(D.Twc + 8 * (size_t)(p + 1), retract(xi, T));
+    store_sim3(D.Twc + 8 * (size_t)(p + 1), retract_f64(xi, T));
   }
   if (tid == 0) {
     float s2 = 0.0f;
@@ -3626,7 +3626,7 @@ __device__ void col_finish(const ColArgs &C, int lane) {
       float xi[7];
 #pragma unroll
       for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
-      store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, Tp[u]));
+      store_sim3(C.Twc + 8 * (size_t)(p + 1), retract_f64(xi, Tp[u]));
     }
   }
 #else
@@ -3635,7 +3635,7 @@ __device__ void col_finish(const ColArgs &C, int lane) {
     float xi[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
-    store_sim3(C.Twc + 8 * (size_t)(p + 1), retract(xi, T));
+    store_sim3(C.Twc + 8 * (size_t)(p + 1), retract_f64(xi, T));
   }
 #endif
   if (lane == 0) {
@@ -7799,7 +7799,7 @@ __global__ void sim3_debug_kernel(int op, const float *__restrict__ a, const flo
   if (k >= n) return;
   switch (op) {
     case 0: store_sim3(out + 8 * k, exp_sim3(a + 7 * k)); break;
-    case 1: store_sim3(out + 8 * k, retract(a + 7 * k, load_sim3(b + 8 * k))); break;
+    case 1: store_sim3(out + 8 * k, retract_f64(a + 7 * k, load_sim3(b + 8 * k))); break;
     case 2: store_sim3(out + 8 * k, compose(load_sim3(a + 8 * k), load_sim3(b + 8 * k))); break;
     case 3: store_sim3(out + 8 * k, inverse(load_sim3(a + 8 * k))); break;
     case 4: store_sim3(out + 8 * k, relative(load_sim3(a + 8 * k), load_sim3(b + 8 * k))); break;
@@ -7812,6 +7812,7 @@ __global__ void sim3_debug_kernel(int op, const float *__restrict__ a, const flo
         for (int c = 0; c < 7; c++) out[49 * k + 7 * r + c] = (float)M[r][c];
       break;
     }
+    case 8: store_sim3(out + 8 * k, retract(a + 7 * k, load_sim3(b + 8 * k))); break;
     default: break;
   }
 }
@@ -8027,7 +8028,7 @@ int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void 
 }
 
 int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n, void *stream) {
-  if (op < 0 || op > 7 || n < 0 || !a || !out || (op != 0 && op != 3 && op != 7 && !b)) return M3S_EINVAL;
+  if (op < 0 || op > 8 || n < 0 || !a || !out || (op != 0 && op != 3 && op != 7 && !b)) return M3S_EINVAL;
   if (n == 0) return M3S_OK;
   sim3_debug_kernel<<<(unsigned)((n + 255) / 256), 256, 0, S(stream)>>>(op, a, b, out, n);
   return hipGetLastError() == hipSuccess ? M3S_OK : M3S_ELAUNCH;

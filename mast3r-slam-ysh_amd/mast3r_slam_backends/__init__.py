@@ -209,7 +209,8 @@ LAYOUT_SECTIONS = ("flags", "rank_i", "rank_j", "first", "partials", "edge_sums"
 
 
 SIM3_OPS = {"exp": (0, 7, None, 8), "retract": (1, 7, 8, 8), "compose": (2, 8, 8, 8), "inverse": (3, 8, None, 8),
-            "relative": (4, 8, 8, 8), "act": (5, 8, 3, 3), "act_matrix": (6, 8, 3, 3), "adjT_inv": (7, 8, None, 49)}
+            "relative": (4, 8, 8, 8), "act": (5, 8, 3, 3), "act_matrix": (6, 8, 3, 3), "adjT_inv": (7, 8, None, 49),
+            "retract_f32": (8, 7, 8, 8)}
 
 
 def debug_sim3(op: str, a: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor:

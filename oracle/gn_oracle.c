@@ -192,8 +192,71 @@ static void exp_sim3(const float *xi, float *t, float *q, float *s) {
   t[2] += B * tau[2];
 }
 
+/* The exact-arithmetic yardstick's retraction (libgn_oracle_f64.so only,
+ * -DORACLE_EXACT_RETRACT): the same Exp(xi) * T in fp64 from the fp32 step and
+ * pose, rounded once. The fp32 restatement above is the reference's own
+ * arithmetic and keeps its ill-conditioning (C = (e^sigma - 1) / sigma holds
+ * the rounding of e^sigma over |sigma|), which would otherwise move the
+ * yardstick's poses by up to ~1e-3 |tau| per step. */
+static void retract_exact(const float *xi, float *T) {
+  const double EPSV = 1e-6;
+  const double tau[3] = {xi[0], xi[1], xi[2]}, phi[3] = {xi[3], xi[4], xi[5]}, sg = xi[6];
+  const double scale = exp(sg), th2 = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  const double th = sqrt(th2);
+  double im, re, A, B, C;
+  if (th2 < EPSV) {
+    im = 0.5 - th2 / 48.0 + th2 * th2 / 3840.0;
+    re = 1.0 - th2 / 8.0 + th2 * th2 / 384.0;
+  } else {
+    im = sin(0.5 * th) / th;
+    re = cos(0.5 * th);
+  }
+  if (fabs(sg) < EPSV) {
+    C = 1.0;
+    if (th < EPSV) {
+      A = 0.5, B = 1.0 / 6.0;
+    } else {
+      A = (1.0 - cos(th)) / th2;
+      B = (th - sin(th)) / (th2 * th);
+    }
+  } else {
+    C = expm1(sg) / sg;
+    if (th < EPSV) {
+      const double s2 = sg * sg;
+      A = ((sg - 1.0) * scale + 1.0) / s2;
+      B = (scale * 0.5 * s2 + scale - 1.0 - sg * scale) / (s2 * sg);
+    } else {
+      const double a = scale * sin(th), b = scale * cos(th), c = th2 + sg * sg;
+      A = (a * sg + (1.0 - b) * th) / (th * c);
+      B = (C - ((b - 1.0) * sg + a * th) / c) / th2;
+    }
+  }
+  const double e[4] = {im * phi[0], im * phi[1], im * phi[2], re};
+  const double p1[3] = {phi[1] * tau[2] - phi[2] * tau[1], phi[2] * tau[0] - phi[0] * tau[2],
+                        phi[0] * tau[1] - phi[1] * tau[0]};
+  const double p2[3] = {phi[1] * p1[2] - phi[2] * p1[1], phi[2] * p1[0] - phi[0] * p1[2],
+                        phi[0] * p1[1] - phi[1] * p1[0]};
+  const double b[4] = {T[3], T[4], T[5], T[6]}, x[3] = {T[0], T[1], T[2]};
+  const double u[3] = {2.0 * (e[1] * x[2] - e[2] * x[1]), 2.0 * (e[2] * x[0] - e[0] * x[2]),
+                       2.0 * (e[0] * x[1] - e[1] * x[0])};
+  const double r[3] = {x[0] + e[3] * u[0] + (e[1] * u[2] - e[2] * u[1]),
+                       x[1] + e[3] * u[1] + (e[2] * u[0] - e[0] * u[2]),
+                       x[2] + e[3] * u[2] + (e[0] * u[1] - e[1] * u[0])};
+  const double q[4] = {e[3] * b[0] + e[0] * b[3] + e[1] * b[2] - e[2] * b[1],
+                       e[3] * b[1] - e[0] * b[2] + e[1] * b[3] + e[2] * b[0],
+                       e[3] * b[2] + e[0] * b[1] - e[1] * b[0] + e[2] * b[3],
+                       e[3] * b[3] - e[0] * b[0] - e[1] * b[1] - e[2] * b[2]};
+  for (int c = 0; c < 3; c++) T[c] = (float)(C * tau[c] + A * p1[c] + B * p2[c] + scale * r[c]);
+  for (int c = 0; c < 4; c++) T[3 + c] = (float)q[c];
+  T[7] = (float)(scale * (double)T[7]);
+}
+
 /* T <- Exp(xi) * T */
 static void retract(const float *xi, float *T) {
+#ifdef ORACLE_EXACT_RETRACT
+  retract_exact(xi, T);
+  return;
+#endif
   float dt[3], dq[4], ds, q1[4], t1[3];
   exp_sim3(xi, dt, dq, &ds);
   qmul(dq, T + 3, q1);

@@ -140,10 +140,13 @@ def edge_blocks(params, Twc, Xs, Cs, ii, jj, idx, valid, Q):
     return Hs, gs
 
 
-def retract(xi, T):
+def retract(xi, T, f64=False):
+    """T <- Exp(xi) T for one pose. f64=False: the reference's fp32 retrSim3
+    (gn_kernels.cu:323-413); f64=True: the exact-arithmetic yardstick's fp64
+    evaluation of the same map (gn_oracle.c retract_exact)."""
     xi = _c(xi, np.float32).reshape(7)
     T = _c(T, np.float32).reshape(8).copy()
-    lib().oracle_retract(_ptr(xi), _ptr(T))
+    lib(f64).oracle_retract(_ptr(xi), _ptr(T))
     return T
 
 

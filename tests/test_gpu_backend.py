@@ -400,21 +400,23 @@ def test_gn_over_capacity_plan_takes_dense_fallback(be):
     the workspace's sparse-slot capacity (64 m + 4096 + 1), so the call solves
     by the tiled fp64 Cholesky (n = 1400) instead of the block-sparse LLT;
     against the oracle (gn_kernels.cu:57-159 builds the same system as
-    triplets). The yardstick is the oracle with fp64 sums (exact-arithmetic
-    stand-in, as tests/test_gpu_large.py).
+    triplets). The yardstick is the oracle with fp64 sums and the fp64
+    retraction (exact-arithmetic stand-in, as tests/test_gpu_large.py).
 
     Every GN step must be as accurate as the reference's fp32 step from the
     SAME linearisation point: step 1 from the initial poses, and step 2 (the
     packed linearize + the tiled solve of a 2-iteration call) from HIP's own
     poses after step 1, each within the fp32 reference's distance to the
-    exact step + 1e-6. The trajectories themselves are not compared beyond
-    that: the complete graph of a loop trajectory has near-empty edges
-    (poorly conditioned H), and step 2 amplifies the ~1e-6 step-1 rounding
-    ~250x. The same fp32 oracle binary sits 5.8e-4 from the exact poses after
-    two iterations on the build container's CPU and 2.5e-4 on the GPU box's
-    (libm variants differ in the last ulp), so that distance measures the
-    problem, not the solver (round 5)."""
+    exact step + 1e-6. The retraction of step 2 is then checked on identical
+    inputs (T1, dx2) three ways: the device's, the oracle's fp32 restatement
+    of retrSim3 and fp64 expm(generator(dx2)) T1. The reference's fp32 Exp
+    cancels for this graph's small scale steps (C = (e^sigma - 1) / sigma,
+    tests/test_sim3_math.py), which is what moved its poses 1e-5..1e-3 off
+    the exact ones with the last bit of a step (round 5); the backend's
+    retraction is evaluated in fp64 (round 6), so HIP's poses are bounded
+    against the exact ones as its steps are."""
     from mast3r_slam_amd import synthetic
+    from test_sim3_math import generator, pose_err, to_mat
 
     N = 201
     ii_u = [i for j in range(N) for i in range(j)]
@@ -425,9 +427,10 @@ def test_gn_over_capacity_plan_takes_dense_fallback(be):
     # step 1 from the initial poses
     T1_gpu, dx1_gpu, info1 = run_gpu(be, "rays", g, 1, 0.0)
     _, dx1_ref, _, failed = run_oracle("rays", g, 1, 0.0)
-    _, dx1_x, _, failed_x = run_oracle("rays", g, 1, 0.0, f64=True)
+    T1_x, dx1_x, _, failed_x = run_oracle("rays", g, 1, 0.0, f64=True)
     assert failed == 0 == failed_x and info1[be.INFO_SOLVE_FAIL] == 0
     e1_hip, e1_ref = float(np.abs(dx1_gpu - dx1_x).max()), float(np.abs(dx1_ref - dx1_x).max())
+    p1_hip = float(np.abs(T1_gpu - T1_x).max())
     # step 2: a 2-iteration call (its first iteration is bitwise the call above)
     # against the exact and the fp32 reference step from HIP's poses after step 1
     T2_gpu, dx2_gpu, info = run_gpu(be, "rays", g, 2, 0.0)
@@ -437,24 +440,34 @@ def test_gn_over_capacity_plan_takes_dense_fallback(be):
     assert f2 == 0 == f2x
     e2_hip, e2_ref = float(np.abs(dx2_gpu - dx2_x).max()), float(np.abs(dx2_ref - dx2_x).max())
     p2_hip, p2_ref = float(np.abs(T2_gpu - T2_x_h).max()), float(np.abs(T2_ref_h - T2_x_h).max())
-    # the trajectories (reported, see the docstring)
+    # the retraction of step 2 on identical inputs (T1, dx2), three ways
+    xi = torch.from_numpy(dx2_gpu.reshape(m, 7).astype(np.float32))
+    T1p = torch.from_numpy(T1_gpu[1:].astype(np.float32))
+    M_x = torch.linalg.matrix_exp(generator(xi.double())) @ to_mat(T1p.double())
+    T_dev = be.debug_sim3("retract", xi.to(DEV), T1p.to(DEV)).cpu().numpy()
+    T_r32 = np.stack([orc.retract(xi[k].numpy(), T1p[k].numpy()) for k in range(m)])
+    r_dev, r_ref = pose_err(T_dev, M_x), pose_err(T_r32, M_x)
+    np.testing.assert_array_equal(T_dev, T2_gpu[1:])  # the call's own retraction
+    # the trajectories after 2 iterations
     T_ref, _, _, _ = run_oracle("rays", g, 2, 0.0)
     T_x, _, _, _ = run_oracle("rays", g, 2, 0.0, f64=True)
+    t_hip, t_ref = float(np.abs(T2_gpu - T_x).max()), float(np.abs(T_ref - T_x).max())
     print(f"dense fallback N={N}: max|dx - dx_exact| step 1 hip {e1_hip:.3e} ref {e1_ref:.3e}; "
           f"step 2 (from HIP's T1) hip {e2_hip:.3e} ref {e2_ref:.3e}, poses hip {p2_hip:.3e} ref {p2_ref:.3e}; "
-          f"trajectories after 2 iterations max|T - T_exact| hip {np.abs(T2_gpu - T_x).max():.3e} "
-          f"ref {np.abs(T_ref - T_x).max():.3e} (max|dx1| {np.abs(dx1_x).max():.3f})")
+          f"retraction of (T1, dx2) vs fp64 expm: device {r_dev.max():.3e} oracle fp32 {r_ref.max():.3e}; "
+          f"poses after step 1 hip {p1_hip:.3e}; trajectories after 2 iterations max|T - T_exact| "
+          f"hip {t_hip:.3e} ref {t_ref:.3e} (max|dx1| {np.abs(dx1_x).max():.3f})")
     assert e1_hip <= e1_ref + 1e-6
     assert e2_hip <= e2_ref + 1e-6
+    assert np.all(r_dev <= r_ref + 1e-6)
+    assert p2_hip <= p2_ref + 1e-6
+    assert t_hip <= t_ref + 1e-6
     # the second step inside the 2-iteration call (packed linearize) is the step
     # a 1-iteration call takes from HIP's T1 (gathering linearize) to fp32
-    # round-off; the poses are not bounded against the references: the Sim(3)
-    # retraction of this graph's ~0.1-size steps maps a 2e-7 change of dx to
-    # 3e-6..3e-5 in the poses (measured between HIP's own two paths,
-    # tools/diag_dense2.py), so p2 of either implementation swings 10x with
-    # last-bit changes of the sums (round 5) while the steps stay accurate
-    _, dx2_one, _ = run_gpu(be, "rays", g, 1, 0.0, Twc0=T1_gpu)
+    # round-off, and so are the poses it retracts to
+    T2_one, dx2_one, _ = run_gpu(be, "rays", g, 1, 0.0, Twc0=T1_gpu)
     assert float(np.abs(dx2_gpu - dx2_one).max()) <= 1e-6
+    assert float(np.abs(T2_gpu - T2_one).max()) <= 1e-5
 
 
 def test_gn_singular_global_factor_zero_dx(be):

@@ -104,3 +104,35 @@ def test_device_adjoint_maps_local_rows_to_world_rows(be):
         # row k of Adj(T)^-T equals column k of Adj(T)^-1 = Adj(T^-1)
         got = M[:, k, :]
         assert float((got - col).abs().max()) < 5e-6 * (1.0 + float(col.abs().max())), k
+
+
+def test_backend_retraction_same_inputs_three_ways(be):
+    """Identical fp32 (xi, T) in the small-step regime where the reference's
+    fp32 Exp cancels (tests/test_sim3_math.small_steps), retracted by the
+    backend's device retraction (op "retract", fp64 evaluation), by the
+    oracle's fp32 restatement of retrSim3 (gn_kernels.cu:323-413) and in fp64
+    by expm(generator(xi)) T. Per pose |T_hip - T_f64| <= |T_ref32 - T_f64| +
+    1e-6, and T_hip within fp32 rounding of the exact pose. The device's fp32
+    form (op "retract_f32", the tracker's) is the reference's arithmetic: it
+    sits where the oracle's fp32 restatement sits."""
+    from oracle import oracle as orc
+    from test_sim3_math import pose_err, small_steps
+
+    gen = torch.Generator().manual_seed(67)
+    n = 400
+    xi = small_steps(n, gen)
+    T = random_T(n, gen).data.to(torch.float32)
+    M_x = torch.linalg.matrix_exp(generator(xi.to(D))) @ to_mat(T.to(D))
+    T_hip = host64(be.debug_sim3("retract", dev32(xi), dev32(T))).numpy()
+    T_h32 = host64(be.debug_sim3("retract_f32", dev32(xi), dev32(T))).numpy()
+    T_ref = np.stack([orc.retract(xi[k].numpy(), T[k].numpy()) for k in range(n)])
+    e_hip, e_h32, e_ref = pose_err(T_hip, M_x), pose_err(T_h32, M_x), pose_err(T_ref, M_x)
+    scale = 1.0 + M_x[..., :3, :].abs().amax((-2, -1)).numpy()
+    print(f"max|T - T_f64|: hip (fp64 eval) {e_hip.max():.2e}, hip fp32 form {e_h32.max():.2e}, "
+          f"oracle fp32 {e_ref.max():.2e} (median {np.median(e_ref):.2e})")
+    assert np.all(e_hip <= e_ref + 1e-6)
+    assert np.all(e_hip <= 4e-7 * scale)
+    # the device's fp32 form and the oracle's restatement: the same arithmetic,
+    # apart from ulp-level differences of expf/sinf/cosf between the two libms
+    # (each amplified by the same cancellation)
+    assert np.median(np.abs(e_h32 - e_ref)) <= 1e-6

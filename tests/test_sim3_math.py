@@ -157,6 +157,50 @@ def test_left_retraction_is_exp_times_T():
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=0, atol=1e-12)
 
 
+def small_steps(n, gen):
+    """GN-sized steps in the regime where the reference's fp32 Exp cancels:
+    |sigma| log-uniform in [1.5e-6, 1e-3] (just above EPS), theta log-uniform
+    in [2e-6, 3e-2], |tau| ~ 0.1, random signs."""
+    u = torch.rand(n, 2, generator=gen, dtype=D)
+    sig = 10 ** (math.log10(1.5e-6) + u[:, 0] * (math.log10(1e-3) - math.log10(1.5e-6)))
+    th = 10 ** (math.log10(2e-6) + u[:, 1] * (math.log10(3e-2) - math.log10(2e-6)))
+    xi = random_xi(n, gen, 1.0, 0.1, 1.0)
+    xi[:, 3:6] *= th[:, None]
+    xi[:, 6] = sig * torch.sign(torch.randn(n, generator=gen, dtype=D))
+    return xi.to(torch.float32)
+
+
+def pose_err(T, M_exact):
+    """Per-pose max |entry| of the 3x4 [sR | t] difference to the exact matrix."""
+    return (to_mat(torch.as_tensor(np.asarray(T, np.float64))) - M_exact)[..., :3, :].abs().amax((-2, -1)).numpy()
+
+
+def test_oracle_retractions_against_matrix_exponential():
+    """The C oracle's two retractions on identical fp32 (xi, T): the fp32 one
+    (the reference's retrSim3 arithmetic, gn_kernels.cu:323-413) and the fp64
+    one of the exact-arithmetic yardstick (libgn_oracle_f64.so), against
+    expm(generator(xi)) T in fp64. The fp64 one is within fp32 rounding of the
+    pose entries; the fp32 one carries the reference's cancellation,
+    C = (e^sigma - 1) / sigma with the rounding of e^sigma over |sigma|:
+    |dt| ~ 6e-8 |tau| / |sigma|."""
+    from oracle import oracle as orc
+
+    gen = torch.Generator().manual_seed(61)
+    xi = small_steps(400, gen)
+    T = random_T(400, gen).data.to(torch.float32)
+    M_x = torch.linalg.matrix_exp(generator(xi.to(D))) @ to_mat(T.to(D))
+    T32 = np.stack([orc.retract(xi[k].numpy(), T[k].numpy()) for k in range(400)])
+    T64 = np.stack([orc.retract(xi[k].numpy(), T[k].numpy(), f64=True) for k in range(400)])
+    e32, e64 = pose_err(T32, M_x), pose_err(T64, M_x)
+    scale = 1.0 + M_x[..., :3, :].abs().amax((-2, -1)).numpy()
+    model = 6e-8 * xi[:, 0:3].to(D).norm(dim=-1).numpy() / xi[:, 6].abs().to(D).numpy()
+    print(f"fp64 retraction max err {e64.max():.2e}; fp32 (reference arithmetic) max err {e32.max():.2e}, "
+          f"median {np.median(e32):.2e}; cancellation model max {model.max():.2e}")
+    assert np.all(e64 <= 4e-7 * scale)
+    assert np.all(e32 <= 4 * model + 4e-7 * scale)  # the error is the model's, no other
+    assert e32.max() > 30 * e64.max()  # and it is real at these steps
+
+
 def test_exp_log_consistency_small_steps():
     """Exp is a local diffeomorphism: d/dh Exp(h xi)|0 = generator(xi)."""
     gen = torch.Generator().manual_seed(9)

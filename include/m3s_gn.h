@@ -177,15 +177,6 @@ const char *m3s_version(void);
 int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t split,
                               int32_t max_parts, int32_t *out, int64_t cap, int32_t *meta);
 
-/* Diagnostic (tests/test_sparse_plan.py): the subtree image of the chip-wide
- * path (m3s_symbolic.h, build_subtree_image) for N poses and edge ranks
- * (ri, rj), built from the unscheduled plan as the solve builds it; copied
- * to out when cap suffices; meta = {subtrees, factor LDS bytes, back-
- * substitution LDS bytes, dense-tail columns}. Returns its length in int32
- * words. */
-int64_t m3s_subtree_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t *out, int64_t cap,
-                               int64_t *meta);
-
 /* Diagnostic: byte offsets of the workspace sections for (N, HW, E), in the
  * order flags, rank_i, rank_j, first, partials, edge_sums, A, fin, plan, Lblk,
  * Dinv, tail, tasks, planes, total (offs[15]). Returns the total. */
@@ -212,10 +203,10 @@ int m3s_debug_stamps(int which, int64_t *out);
 int m3s_debug_sim3(int op, const float *a, const float *b, float *out, int64_t n, void *stream);
 /* Solver knobs (experiments / A/B tests). Defaults are the measured best;
  * the environment (M3S_PLAN_CACHE, M3S_DENSE, M3S_DENSE_TAIL_MIN, M3S_COLS,
- * M3S_DF, M3S_TAIL_CYC, M3S_TAIL_MFMA, M3S_BORDER_SPLIT, M3S_SUBTREE,
+ * M3S_DF, M3S_TAIL_CYC, M3S_TAIL_MFMA, M3S_BORDER_SPLIT,
  * M3S_TRACK_PERSISTENT, M3S_PROLOGUE) is read once per process; this sets a
  * knob at run time for the calls that follow. Names: plan_cache, dense,
- * dense_tail_min, cols, df, tail_cyc, tail_mfma, border_split, subtree,
+ * dense_tail_min, cols, df, tail_cyc, tail_mfma, border_split,
  * track_persistent, prologue (0: host-side prepare),
  * debug_drop_item (test hook: drop one dispatch item of the one-workgroup
  * LLT so its bounded waits time out). Returns the previous value, or

@@ -91,22 +91,13 @@ __device__ __forceinline__ Sim3Mat sim3_matrix(const Sim3f &T) {
   M.t[0] = T.t[0], M.t[1] = T.t[1], M.t[2] = T.t[2];
   return M;
 }
-#ifndef M3S_PK_ACT
-#define M3S_PK_ACT 1
-#endif
 __device__ __forceinline__ void act(const Sim3Mat &M, const float *X, float *Y) {
-#if M3S_PK_ACT
   // rows 0 and 1 as one float2 chain (v_pk_fma_f32), row 2 scalar
   typedef float v2 __attribute__((ext_vector_type(2)));
   v2 y = __builtin_elementwise_fma(v2{M.m[2], M.m[5]}, v2{X[2], X[2]}, v2{M.t[0], M.t[1]});
   y = __builtin_elementwise_fma(v2{M.m[1], M.m[4]}, v2{X[1], X[1]}, y);
   y = __builtin_elementwise_fma(v2{M.m[0], M.m[3]}, v2{X[0], X[0]}, y);
   Y[0] = y.x, Y[1] = y.y;
-  Y[2] = __builtin_fmaf(M.m[6], X[0], __builtin_fmaf(M.m[7], X[1], __builtin_fmaf(M.m[8], X[2], M.t[2])));
-  return;
-#endif
-  Y[0] = __builtin_fmaf(M.m[0], X[0], __builtin_fmaf(M.m[1], X[1], __builtin_fmaf(M.m[2], X[2], M.t[0])));
-  Y[1] = __builtin_fmaf(M.m[3], X[0], __builtin_fmaf(M.m[4], X[1], __builtin_fmaf(M.m[5], X[2], M.t[1])));
   Y[2] = __builtin_fmaf(M.m[6], X[0], __builtin_fmaf(M.m[7], X[1], __builtin_fmaf(M.m[8], X[2], M.t[2])));
 }
 
@@ -219,19 +210,25 @@ __device__ inline Sim3f retract_f64(const float *xi, const Sim3f &T) {
   const double tau[3] = {xi[0], xi[1], xi[2]};
   const double phi[3] = {xi[3], xi[4], xi[5]};
   const double sg = xi[6];
-  const double scale = exp(sg);
+  // one expm1 and one sincos of theta / 2 carry every transcendental:
+  // e^sigma = 1 + em1, sin theta = 2 sh ch, 1 - cos theta = 2 sh^2 (no
+  // cancellation), 1 - e^sigma cos theta = 2 e^sigma sh^2 - em1
+  const double em1 = expm1(sg), scale = 1.0 + em1;
   const double th2 = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
   const double th = sqrt(th2);
+  double sh, ch;
+  sincos(0.5 * th, &sh, &ch);
   double im, re;
   if (th2 < EPSV) {
     const double th4 = th2 * th2;
     im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
     re = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
   } else {
-    im = sin(0.5 * th) / th;
-    re = cos(0.5 * th);
+    im = sh / th;
+    re = ch;
   }
   const double eq[4] = {im * phi[0], im * phi[1], im * phi[2], re};
+  const double sin_th = 2.0 * sh * ch, omc = 2.0 * sh * sh;  // sin theta, 1 - cos theta
   double A, B, C;
   if (fabs(sg) < EPSV) {
     C = 1.0;
@@ -239,19 +236,19 @@ __device__ inline Sim3f retract_f64(const float *xi, const Sim3f &T) {
       A = 0.5;
       B = 1.0 / 6.0;
     } else {
-      A = (1.0 - cos(th)) / th2;
-      B = (th - sin(th)) / (th2 * th);
+      A = omc / th2;
+      B = (th - sin_th) / (th2 * th);
     }
   } else {
-    C = expm1(sg) / sg;
+    C = em1 / sg;
     if (th < EPSV) {
       const double sg2 = sg * sg;
       A = ((sg - 1.0) * scale + 1.0) / sg2;
       B = (scale * 0.5 * sg2 + scale - 1.0 - sg * scale) / (sg2 * sg);
     } else {
-      const double a = scale * sin(th), b = scale * cos(th), c = th2 + sg * sg;
-      A = (a * sg + (1.0 - b) * th) / (th * c);
-      B = (C - ((b - 1.0) * sg + a * th) / c) / th2;
+      const double a = scale * sin_th, omb = scale * omc - em1, c = th2 + sg * sg;  // omb = 1 - b
+      A = (a * sg + omb * th) / (th * c);
+      B = (C - (a * th - omb * sg) / c) / th2;
     }
   }
   const double p1[3] = {phi[1] * tau[2] - phi[2] * tau[1], phi[2] * tau[0] - phi[0] * tau[2],
@@ -321,33 +318,17 @@ __device__ inline void adjT_inv_matrix(const float *Tp, double M[7][7]) {
 // the difference is below the fp32 summation noise (DESIGN.md tolerances).
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-#ifndef M3S_FAST_LOG
-#define M3S_FAST_LOG 1
-#endif
 // natural log: v_log_f32 (log2, ~1 ulp on normal inputs) * ln 2; callers only
 // use it on z > z_eps (>= FLT_MIN) or select the result away
 __device__ __forceinline__ float flog(float x) {
-#if M3S_FAST_LOG
   return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
-#else
-  return __logf(x);
-#endif
 }
 
 // branch-free: both sides are always computed, then selected
-#ifndef M3S_HUBER_MIN
-#define M3S_HUBER_MIN 1
-#endif
 __device__ __forceinline__ float huber_w(float r, float k) {
-#if M3S_HUBER_MIN
   // min(1, k/|r|): 1 below the threshold (k/|r| > 1 there), k/|r| above; one
   // v_min_f32 instead of a compare and a select
   return fminf(1.0f, k * frcp(fabsf(r)));
-#else
-  const float a = fabsf(r);
-  const float o = k * frcp(a);
-  return a < k ? 1.0f : o;
-#endif
 }
 
 // non-zero patterns of the local Jacobian rows (bits: tau0..2 phi0..2 sigma)
@@ -715,9 +696,6 @@ __device__ __forceinline__ void pixel_contrib(ACC &acc, const ResidualParams &P,
 // scalar. Entries no row of the model touches stay compile-time zeros and
 // take no registers (rays 33, calib 32 live sums). Same per-pixel products as
 // pixel_contrib; the fp32 sums are per half, then combined in fold().
-#ifndef M3S_CAL25  // calib packed iterations: L(2,5) from L(0,3) and L(1,4) (AccumPP::cal25_fixup)
-#define M3S_CAL25 1
-#endif
 struct AccumPP {
   f32x2 s[kNP];
   __device__ __forceinline__ void zero() {
@@ -728,7 +706,7 @@ struct AccumPP {
 #pragma unroll
     for (int k = 0; k < kNP; k++) acc[k] += s[k].x + s[k].y;
   }
-  // Calib (packed backend iterations, M3S_CAL25): L(2,5) is not summed but
+  // Calib (packed backend iterations, round 5): L(2,5) is not summed but
   // formed here as -(L(0,3) + L(1,4)). With zi = 1/z, per pixel the u row
   // adds -W_u x y zi to L(0,3) and +W_u x y zi to L(2,5), the v row +W_v x y zi
   // to L(1,4) and -W_v x y zi to L(2,5), and the log-depth row has no column
@@ -762,14 +740,7 @@ struct AccumPP {
 
 // keeps the scheduler from hoisting the next row's products over this row's
 // sums (register pressure of the pixel-pair kernels)
-#ifndef M3S_ROWBAR
-#define M3S_ROWBAR 1
-#endif
-#if M3S_ROWBAR
 #define M3S_ROW_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define M3S_ROW_BARRIER()
-#endif
 __device__ __forceinline__ f32x2 splat2(float v) { return f32x2{v, v}; }
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 rcp2(f32x2 x) { return f32x2{frcp(x.x), frcp(x.y)}; }
@@ -883,7 +854,7 @@ __device__ __forceinline__ void pixel_contrib2(AccumPP &acc, const ResidualParam
     const f32x2 au[5] = {zinv, -(x * zinv), -xyp, fma2(x, x, one), -y};  // kCalU: 0 2 3 4 5
     const f32x2 av[5] = {zinv, -(y * zinv), -fma2(y, y, one), xyp, x};  // kCalV: 1 2 3 4 5
     const f32x2 az[4] = {zinv, y, -x, one};                              // kCalZ: 2 3 4 6
-    constexpr int kSkip25 = (M3S_CAL25 && !COST) ? kL + tri(2, 5) : -1;  // AccumPP::cal25_fixup
+    constexpr int kSkip25 = !COST ? kL + tri(2, 5) : -1;  // AccumPP::cal25_fixup
     acc.add<kCalU, 5, COST, kSkip25>(au, Wu, etu);
     M3S_ROW_BARRIER();
     acc.add<kCalV, 5, COST, kSkip25>(av, Wv, etv);

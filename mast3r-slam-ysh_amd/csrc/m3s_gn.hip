@@ -55,27 +55,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-#ifndef M3S_PP  // packed linearize: two pixels per float2 (AccumPP) instead of row pairs
-#define M3S_PP 1
-#endif
-#ifndef M3S_GATHER_PP  // gathering (first-iteration) kernel on the pixel-pair accumulator too
-#define M3S_GATHER_PP 0
-#endif
-#ifndef M3S_PP_LDS  // PP: operands read from the LDS slot per pixel pair
-#define M3S_PP_LDS 1
-#endif
-#ifndef M3S_PK_PAIRBAR  // packed linearize: no scheduling across the two pixel pairs of a trip
-#define M3S_PK_PAIRBAR 0
-#endif
-#ifndef M3S_PK_XASM  // packed linearize: Xj floats read one by one into their pair halves
-#define M3S_PK_XASM 1
-#endif
-#ifndef M3S_PK_DEPTH  // packed linearize: trips prefetched ahead through LDS (1 or 2)
-#define M3S_PK_DEPTH 1
-#endif
-#ifndef M3S_PK_SPARSE  // A/B build only: GN iterations 2.. over the valid pixels (linearize_sparse_kernel, slower)
-#define M3S_PK_SPARSE 0
-#endif
 constexpr int kThreads = 256;        // linearize block
 constexpr int kPixPerThread = 4;     // one 16-B vector group
 constexpr int kBlockPix = kThreads * kPixPerThread;  // 1024 pixels per block sweep
@@ -117,7 +96,6 @@ inline int64_t chunks_for(int64_t HW, int64_t E_loc, int64_t target = kTargetBlo
   return (HW + ch - 1) / ch;
 }
 // bytes per edge of the validity nibbles (HW / 4, padded: 8-B loads stay aligned)
-__host__ __device__ inline int64_t vmask_stride(int64_t HW) { return ((HW + 3) / 4 + 8 + 255) / 256 * 256; }
 inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
   int64_t ch = (HW + chunks - 1) / chunks;
   return (ch + kBlockPix - 1) / kBlockPix * kBlockPix;
@@ -127,16 +105,9 @@ inline int64_t chunk_pixels(int64_t HW, int64_t chunks) {
 // rows (n + 1 <= 16 kTailMaxT) and its scratch (dense bordered tail, L tiles,
 // W_k); see the kernel
 constexpr int kTailMaxT = 32;
-// border task flags of the concurrent tail launch: nc (nc + 1) / 2 tasks, nc < 16 kTailMaxT / 7
-constexpr int kBtFlagsMax = (16 * kTailMaxT / 7 + 1) * (16 * kTailMaxT / 7 + 2) / 2;
-// their offset in the colsync words (after the X_k chunk counters)
-inline int64_t kColsyncBtOff(int64_t m, int64_t slot_cap) { return 2 * (m + 1) + 16 + slot_cap + 2 * kTailMaxT + (m + 1); }
-inline size_t tail_z_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y', LgT, Z, then the granules
+inline size_t tail_gran_offset_doubles() {  // tail scratch: dense tail, Lg, Wg, y', LgT, then the granules
   const size_t nmax = 16 * kTailMaxT;
   return nmax * nmax + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256 * 2 + (size_t)kTailMaxT * 256 + nmax;
-}
-inline size_t tail_gran_offset_doubles() {  // + the tiles of Z = L^-1 (tail_zinv_col, round 5)
-  return tail_z_offset_doubles() + (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 256;
 }
 constexpr int kGNx = 16 * kTailMaxT + 8;  // columns of X_k: a_k and one per tail dof (gcol_worker), padded
 inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cyc_kernel)
@@ -146,7 +117,7 @@ inline size_t tail_scratch_doubles() {  // dense tail, L tiles, W_k, y' (tail_cy
 
 struct Layout {
   size_t flags, rank_i, rank_j, first, edge_cnt, partials, edge_sums, A, fin, plan, Lblk, Dinv, rhs, parts,
-      colsync, wgran, tail, gx, eorder, planes, vmask, total;
+      colsync, wgran, tail, gx, eorder, planes, total;
   int64_t n, ld;          // system size 7(N-1); leading dim of the RHS-augmented matrix
   int64_t plan_cap, slot_cap;  // sparse-LLT capacities (int32 plan words, 7x7 slots)
 };
@@ -201,7 +172,7 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   off = align_up(off + sizeof(double) * 56 * (size_t)L.slot_cap, 256);
   L.colsync = off;  // column tasks: done[m+1], done2[m+1], tickets, slot flags [slot_cap], tail flags,
                     // X_k chunk counters [m+1], border task flags (epoch-tagged, zeroed per call)
-  off = align_up(off + sizeof(int32_t) * (size_t)(3 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT + kBtFlagsMax), 256);
+  off = align_up(off + sizeof(int32_t) * (size_t)(3 * (m + 1) + 16 + L.slot_cap + 2 * kTailMaxT), 256);
   L.wgran = off;  // df_factor_kernel: W_k of every column as 16-B tagged granules (zeroed with colsync per call)
   off = align_up(off + (size_t)16 * 49 * (size_t)(m + 1), 256);
   L.tail = off;  // tail_llt_kernel scratch: dense bordered tail, L tiles, W_k
@@ -211,8 +182,6 @@ inline Layout gn_layout(int64_t N, int64_t HW, int64_t E) {
   // target-side planes of every edge (4 planes = rays / points, the widest modes)
   L.planes = off;
   off = align_up(off + sizeof(float) * 4 * (size_t)E * (size_t)HW, 256);
-  L.vmask = off;  // the planes' pixel validity (linearize_sparse_kernel, A/B build only), 4 bits per byte per edge
-  off = align_up(off + (M3S_PK_SPARSE ? (size_t)vmask_stride(HW) * (size_t)E : 0), 256);
   L.total = off;
   return L;
 }
@@ -252,7 +221,6 @@ struct LinArgs {
   int64_t per, E_loc;      // block_task: 8 runs of `per` blocks; edges of the launch
   uint32_t cnt_base;       // edge_cnt arrivals before this launch in the call (edge_tail)
   float *planes;           // per-edge target-side planes (PixIn), [E_loc][kPlanes][HW]
-  uint8_t *vmask;          // per-edge pixel validity (sq != 0), 4 bits per byte, [E_loc][vmask_stride(HW)]
   float *partials;         // [task][36]
   uint32_t *edge_cnt;      // non-null: the last chunk of an edge to finish also finalizes it into fin
   double *fin;             // [E][kFin] per-edge blocks M L M^T, M g (fused finalize)
@@ -299,9 +267,6 @@ __device__ __forceinline__ PixIn<MODE> gather_pixel(const LinArgs &A, const floa
   return make_pixin<MODE>(A.P, Xi, ok, q, u_t, v_t);
 }
 
-#ifndef M3S_EORDER  // linearize task order: edges grouped by KF j (0) or by KF i (1, A/B)
-#define M3S_EORDER 0
-#endif
 // block -> task (e_loc * chunks + c). The E_loc x chunks tasks sorted by
 // (chunk, KF j) are cut into 8 contiguous runs and run x is dealt to blocks
 // x, x + 8, x + 16, ...: the edges that stream the same Xj chunk run back to
@@ -500,13 +465,7 @@ __device__ __forceinline__ double sum_xor16_32(double u) {
 // whole-wave sum on every lane by the same exchanges (permlane swaps of the
 // value with itself for xor 32 / 16, then DPP; the xor-4 partner is 7 - i
 // within a half-row): the solve tails' ||dx|| sums (round 5)
-#ifndef M3S_NORM_PL
-#define M3S_NORM_PL 1
-#endif
 __device__ __forceinline__ float wave_sum_pl(float u) {
-#if !M3S_NORM_PL
-  return wave_sum(u);
-#endif
   float a = u, b = u;
   xr_swap(true, a, b);
   u = a + b;
@@ -596,19 +555,9 @@ __device__ __forceinline__ T xreduceN_dpp(const T (&v)[N], int lane) {
 // within noise for the packed kernel (an A/B of the first-listed library reads
 // ~2-3% slow in tools/ab_linearize.py either way, profiles/r05/ab_pkw_*.txt),
 // so the round-4 rounding stays
-#ifndef M3S_XRED_DPP_LIN
-#define M3S_XRED_DPP_LIN 0
-#endif
-#ifndef M3S_XRED_DPP  // the tracker's per-iteration reductions on xreduce36_dpp (0: xreduce36)
-#define M3S_XRED_DPP 1
-#endif
 template <typename T>
 __device__ __forceinline__ T xreduce36_trk(const T (&v)[kNP], int lane, int &idx, bool &valid) {
-#if M3S_XRED_DPP
   return xreduce36_dpp(v, lane, idx, valid);
-#else
-  return xreduce36(v, lane, idx, valid);
-#endif
 }
 
 __device__ __forceinline__ void store_partial(const float *acc, float *out) {
@@ -619,11 +568,7 @@ __device__ __forceinline__ void store_partial(const float *acc, float *out) {
   for (int k = 0; k < kNP; k++) v[k] = acc[k];
   int idx;
   bool valid;
-#if M3S_XRED_DPP_LIN
-  const float s = xreduce36_dpp(v, lane, idx, valid);
-#else
   const float s = xreduce36(v, lane, idx, valid);
-#endif
   if (valid) red[wave][idx] = s;
   __syncthreads();
   if (threadIdx.x < kNP) {
@@ -733,12 +678,7 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
   float *__restrict__ pl = WPACK ? A.planes + (size_t)e_loc * NPL * HW : nullptr;
 
   // scalar accumulators here: 4 pixels of raw inputs stay live in this kernel
-  // (M3S_GATHER_PP: the pixel-pair accumulator of the packed kernel, backend only)
-#if M3S_GATHER_PP
-  typename std::conditional<TRACK, AccumFlat, AccumPP>::type acc;
-#else
   AccumFlat acc;
-#endif
   acc.zero();
 
   const int64_t p_begin = c * A.chunk_pix;
@@ -774,20 +714,6 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
       for (int s = 0; s < 4; s++)
         in[s] = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p0 + s, ((vb >> (8 * s)) & 0xffu) != 0, ids[s],
                                           qs[s], cjs[s]);
-#if M3S_GATHER_PP
-      if constexpr (!TRACK) {
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          f32x2 in2[NPL], X2[3], Y2[3];
-#pragma unroll
-          for (int k = 0; k < NPL; k++) in2[k] = f32x2{in[2 * h].v[k], in[2 * h + 1].v[k]};
-#pragma unroll
-          for (int k = 0; k < 3; k++) X2[k] = f32x2{Xj[2 * h][k], Xj[2 * h + 1][k]};
-          act2(Tm, X2, Y2);
-          pixel_contrib2<MODE, NPL>(acc, P, in2, Y2);
-        }
-      } else
-#endif
       {
 #pragma unroll
         for (int s = 0; s < 4; s++) {
@@ -804,12 +730,6 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
           // (first call 258 -> 251 us at C3, 1172 -> 1134 us at 128 KFs rays)
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(pl + (size_t)k * HW + p0));
         }
-        if (A.vmask) {
-          constexpr int SQK = MODE == 2 ? 1 : NPL - 1;
-          A.vmask[(size_t)e_loc * vmask_stride(HW) + (p0 >> 2)] =
-              (uint8_t)((in[0].v[SQK] != 0.0f ? 1 : 0) | (in[1].v[SQK] != 0.0f ? 2 : 0) |
-                        (in[2].v[SQK] != 0.0f ? 4 : 0) | (in[3].v[SQK] != 0.0f ? 8 : 0));
-        }
       }
     }
   } else {
@@ -819,18 +739,6 @@ __global__ void __launch_bounds__(kThreads) linearize_kernel(LinArgs A) {
       const float Xj[3] = {Xs_j[3 * p], Xs_j[3 * p + 1], Xs_j[3 * p + 2]};
       const float cj = TRACK ? 0.0f : Cs_j[p];
       const PixIn<MODE> in = gather_pixel<MODE, TRACK>(A, Xs_i, Cs_i, p, vm, id, Qe[p], cj);
-#if M3S_GATHER_PP
-      if constexpr (!TRACK) {  // the pixel in .x; .y the same pixel with weight 0
-        constexpr int sqk = MODE == 2 ? 1 : NPL - 1;  // the sqrt(q) plane (make_pixin)
-        f32x2 in2[NPL], X2[3], Y2[3];
-#pragma unroll
-        for (int k = 0; k < NPL; k++) in2[k] = f32x2{in.v[k], k == sqk ? 0.0f : in.v[k]};
-#pragma unroll
-        for (int k = 0; k < 3; k++) X2[k] = f32x2{Xj[k], Xj[k]};
-        act2(Tm, X2, Y2);
-        pixel_contrib2<MODE, NPL>(acc, P, in2, Y2);
-      } else
-#endif
       {
         float Y[3];
         act(Tm, Xj, Y);
@@ -892,10 +800,10 @@ __device__ __forceinline__ void lds_xj6(const float *xs, int h, float (&xf)[6]) 
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xf[0]), "+v"(xf[1]), "+v"(xf[2]), "+v"(xf[3]), "+v"(xf[4]), "+v"(xf[5]));
 }
 #ifndef M3S_PK_WAVES  // packed linearize: minimum waves per SIMD (register bound 512 / w)
-#define M3S_PK_WAVES (M3S_PP ? 3 : 4)
+#define M3S_PK_WAVES 3
 #endif
 #ifndef M3S_PK_WAVES_RAYS
-#define M3S_PK_WAVES_RAYS (M3S_PP ? 2 : 1)
+#define M3S_PK_WAVES_RAYS 2
 #endif
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_PK_WAVES)
@@ -915,64 +823,11 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   constexpr int NPL = PixIn<MODE>::kPlanes;
   const float *__restrict__ pl = A.planes + (size_t)e_loc * NPL * HW;
 
-#if M3S_PP
   AccumPP acc;
-#else
-  Accum<MODE> acc;
-#endif
   acc.zero();
   const int64_t p_begin = c * A.chunk_pix;
   const int64_t p_end = (p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW;
-  // one trip = 4 pixels per lane: NPL plane vectors + 3 Xj vectors (16 B each)
-  auto load_trip = [&](int64_t q, f32x4 *pv, f32x4 *xv) {
-#pragma unroll
-    for (int k = 0; k < NPL; k++) pv[k] = ld_stream(reinterpret_cast<const f32x4 *>(pl + (size_t)k * HW + q));
-    const f32x4 *xj4 = reinterpret_cast<const f32x4 *>(Xs_j + 3 * q);
-    xv[0] = xj4[0], xv[1] = xj4[1], xv[2] = xj4[2];
-  };
-  float sink = 0.0f;  // 0 experiment only
-#if M3S_PP
-  // pixel pairs (0, 1) and (2, 3) in the halves of float2 registers; Xj of the
-  // 4 pixels arrives interleaved: x0 y0 z0 x1 | y1 z1 x2 y2 | z2 x3 y3 z3
-  auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
-    {
-      const f32x2 X[3] = {{xv[0].x, xv[0].w}, {xv[0].y, xv[1].x}, {xv[0].z, xv[1].y}};
-      f32x2 in[NPL];
-#pragma unroll
-      for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].x, pv[k].y};
-      f32x2 Y[3];
-      act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    {
-      const f32x2 X[3] = {{xv[1].z, xv[2].y}, {xv[1].w, xv[2].z}, {xv[2].x, xv[2].w}};
-      f32x2 in[NPL];
-#pragma unroll
-      for (int k = 0; k < NPL; k++) in[k] = f32x2{pv[k].z, pv[k].w};
-      f32x2 Y[3];
-      act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-#else
-  auto do_trip = [&](const f32x4 *pv, const f32x4 *xv) {
-    const float Xj[4][3] = {{xv[0].x, xv[0].y, xv[0].z}, {xv[0].w, xv[1].x, xv[1].y},
-                            {xv[1].z, xv[1].w, xv[2].x}, {xv[2].y, xv[2].z, xv[2].w}};
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      PixIn<MODE> in;
-#pragma unroll
-      for (int k = 0; k < NPL; k++) in.v[k] = pv[k][s];
-      float Y[3];
-      act(Tm, Xj[s], Y);
-      pixel_contrib<MODE>(acc, P, in, Y);
-      // one pixel at a time: keeps the packed kernel at ~90 VGPRs (5 waves/SIMD)
-      if ((s + 1) % 1 == 0) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-#endif
+  float sink = 0.0f;  // the memory-floor build only (M3S_PK_FLOOR=1)
   // Prefetch one trip ahead through LDS with no VGPR cost: each wave's next
   // trip (NPL plane vectors + 3 Xj vectors, 16 B per lane each) is loaded by
   // buffer_load_dwordx4 ... lds into the wave's own LDS slot while the wave
@@ -982,8 +837,8 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   // and per-lane voffsets fixed for the whole kernel, and the LDS slot (m0)
   // from a wave-uniform wave index: no per-load VALU address arithmetic
   // (17 VALU per trip before). One resource per plane, sized HW floats.
-  // M3S_PK_DEPTH slots per wave: trip t lands in slot t % DEPTH
-  constexpr int DEPTH = M3S_PK_DEPTH;
+  // one slot per wave (a 2-deep prefetch measured slower)
+  constexpr int DEPTH = 1;
   __shared__ __attribute__((aligned(16))) f32x4 stage[DEPTH][kThreads / 64][NPL + 3][64];
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), ln = threadIdx.x & 63;
   __amdgpu_buffer_rsrc_t Rp[NPL];
@@ -1044,7 +899,6 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
     // lanes past the chunk's end (a partial last trip only) read back zeros
     // from the resources and take no part (their exec bit is off)
     if (PARTIAL && pw + kPixPerThread * ln >= pend) return;
-#if M3S_PP && M3S_PP_LDS
     // each pixel pair's operands are read from the LDS slot just before its
     // math (8-B reads: 2 NPL + 6 VGPRs live instead of 4 (NPL + 3)); the slot
     // is refilled once the second pair's operands are in registers
@@ -1057,15 +911,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       // Xj of pixels 2h, 2h + 1: floats 6h .. 6h + 5 of the lane's 12
       const float *xs = sl + 256 * NPL;
       float xf[6];
-#if M3S_PK_XASM
       lds_xj6(xs, h, xf);
-#else
-#pragma unroll
-      for (int q = 0; q < 6; q++) {
-        const int f = 6 * h + q;
-        xf[q] = xs[256 * (f >> 2) + (f & 3)];
-      }
-#endif
       X[0] = f32x2{xf[0], xf[3]}, X[1] = f32x2{xf[1], xf[4]}, X[2] = f32x2{xf[2], xf[5]};
       if (h == 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
@@ -1078,20 +924,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       act2(Tm, X, Y);
       pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
 #endif
-#if M3S_PK_PAIRBAR
-      __builtin_amdgcn_sched_barrier(0);
-#endif
     }
-#else
-    f32x4 pv[NPL], xv[3];
-#pragma unroll
-    for (int k = 0; k < NPL; k++) pv[k] = stage[cur][wv][k][ln];
-#pragma unroll
-    for (int k = 0; k < 3; k++) xv[k] = stage[cur][wv][NPL + k][ln];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read back before it is refilled
-    if (pw + DEPTH * kBlockPix < pend) issue(pw + DEPTH * kBlockPix, cur);
-    do_trip(pv, xv);
-#endif
   };
   int trip = 0;
   for (; pw0 + kPixPerThread * 64 <= pend; pw0 += kBlockPix, trip++) trip_body(pw0, trip, false);
@@ -1099,9 +932,7 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
   float sums[kNP];
 #pragma unroll
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
-#if M3S_PP
-  if constexpr (MODE == 2 && M3S_CAL25) acc.cal25_fixup();
-#endif
+  if constexpr (MODE == 2) acc.cal25_fixup();
   acc.fold(sums);
   sums[0] += sink;
   store_partial(sums, A.partials + (size_t)b * kNP);
@@ -1120,12 +951,6 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 // flight), the pose-only math, the rest, the plane stores. Same arithmetic per
 // pixel as linearize_kernel<MODE, false, true, true> (gather_pixel +
 // make_pixin + pixel_contrib): bitwise the same planes, partials and sums.
-#ifndef M3S_DIAG_RL
-#define M3S_DIAG_RL 1  // sparse_llt_kernel's 7x7 DIAG factor: column broadcast by readlanes (0: through LDS, A/B)
-#endif
-#ifndef M3S_GATHER_LDS  // pipelined gathering launch (0: linearize_kernel's VGPR-staged loop)
-#define M3S_GATHER_LDS 1
-#endif
 // per-wave slot (bytes): valid u8x4 | Q | idx (int64: two 1-KB rows; int32: one) | Xj (3 rows) | Cj
 constexpr int kGsValid = 0, kGsQ = 256, kGsIdx = 1280, kGsXj = 3328, kGsCj = 6400, kGsBytes = 7424;
 __device__ __forceinline__ void buf_lds4_nt(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
@@ -1306,164 +1131,10 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
       const f32x4 v = {in[0].v[k], in[1].v[k], in[2].v[k], in[3].v[k]};
       __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(pl + (size_t)k * HW + p0));
     }
-    if (A.vmask) {  // the 4 pixels' validity for linearize_sparse_kernel
-      constexpr int SQK = MODE == 2 ? 1 : NPL - 1;
-      const uint8_t nb = (uint8_t)((in[0].v[SQK] != 0.0f ? 1 : 0) | (in[1].v[SQK] != 0.0f ? 2 : 0) |
-                                   (in[2].v[SQK] != 0.0f ? 4 : 0) | (in[3].v[SQK] != 0.0f ? 8 : 0));
-      A.vmask[(size_t)e_loc * vmask_stride(HW) + (p0 >> 2)] = nb;
-    }
   }
   float sums[kNP];
 #pragma unroll
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
-  acc.fold(sums);
-  store_partial(sums, A.partials + (size_t)b * kNP);
-  if (A.edge_cnt) edge_tail(A, e_loc, e);
-}
-
-// ------------------------------------------- sparse packed iterations --
-// Round 5 (M3S_PK_SPARSE): GN iterations 2.. of a call over the VALID pixels
-// only. A pixel whose sq plane is 0 (no valid match, Q / C under threshold,
-// calib z_i <= z_eps: a quarter of the C3 pixels) contributes exactly zero in
-// every iteration, yet the dense packed kernel computes it. The gathering
-// first iteration writes each pixel's validity (4 bits per byte, vmask);
-// here a block turns its chunk's bits into a list of valid pixels in LDS
-// (sub-batches of kSpSB pixels, increasing pixel order: deterministic), and
-// each wave takes 128-entry rounds of it (two pixels per lane, the pixel-pair
-// accumulation of the packed kernel): the entries' NPL planes and Xj floats
-// go by 4-B buffer_load ... lds into the wave's double-buffered slot one round
-// ahead, read back by inline-asm ds_reads (no compiler vmcnt wait on a DMA
-// target). A round's unused entries repeat a valid pixel at zero weight.
-// Same per-pixel products as linearize_packed_kernel, another summation
-// order (fp32 round-off). Measured slower, kept as an A/B build only
-// (profiles/r05/ab_lin_sparse_REJECTED.txt: 93 -> 129 us per C3 launch, sums
-// within 2e-8): the VALU it saves is lost to the loads, 2 (NPL + 3) 4-B DMA
-// instructions per two-pixel round where the dense kernel moves four pixels
-// of a plane in one 16-B instruction, and to the list reads between rounds.
-constexpr int kSpSB = 8192;  // pixels per list sub-batch (16 KB of LDS)
-__device__ int block_excl_scan(int v, int *wsum, int *total);
-template <int NF>
-__device__ __forceinline__ void sp_read(uint32_t a, float (&f)[2 * NF]) {  // the slot's 2 NF floats of this lane
-#pragma unroll
-  for (int q = 0; q < 2 * NF; q++) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(f[q]) : "v"(a), "i"(256 * q));
-  // the wait names every destination: no copy of a register before its data lands
-  if constexpr (NF == 6)
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
-                   "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11])
-                 :
-                 : "memory");
-  else
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
-                   "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11]), "+v"(f[12]), "+v"(f[13])
-                 :
-                 : "memory");
-}
-__device__ __forceinline__ int sp_list(uint32_t a) {  // one u16 list entry (inline asm: no DMA wait)
-  int v;
-  asm volatile("ds_read_u16 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-  return v;
-}
-template <int MODE>
-__global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_PK_WAVES)
-    linearize_sparse_kernel(LinArgs A) {
-  if (*A.stop) return;
-  const int64_t b = block_task(A);
-  if (b < 0) return;
-  const int64_t e_loc = b / A.chunks;
-  const int64_t c = b - e_loc * A.chunks;
-  const int64_t e = A.edge_begin + e_loc;
-  const int64_t HW = A.HW;
-  const int ri = A.rank_i[e], rj = A.rank_j[e];
-  const Sim3Mat Tm = sim3_matrix(relative(load_sim3(A.Twc + 8 * ri), load_sim3(A.Twc + 8 * rj)));
-  const ResidualParams P = kparams(A);
-  constexpr int NPL = PixIn<MODE>::kPlanes, SQK = MODE == 2 ? 1 : NPL - 1, NF = NPL + 3;
-  const float *Xs_j = A.Xs + (size_t)rj * HW * 3;
-  const float *pl = A.planes + (size_t)e_loc * NPL * HW;
-  const uint8_t *vm = A.vmask + (size_t)e_loc * vmask_stride(HW);
-  const int tid = threadIdx.x, ln = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int NW = kThreads / 64;
-  __shared__ uint16_t list[kSpSB];
-  __shared__ int wsum[17];
-  __shared__ __attribute__((aligned(16))) float slot[NW][2][2 * NF][64];
-  __amdgpu_buffer_rsrc_t Rp[NPL];
-#pragma unroll
-  for (int k = 0; k < NPL; k++)
-    Rp[k] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(pl + (size_t)k * HW), 0, (int)(4 * HW), 0x00020000);
-  const __amdgpu_buffer_rsrc_t Rx =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_j), 0, (int)(12 * HW), 0x00020000);
-  const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint16_t *)list);
-  AccumPP acc;
-  acc.zero();
-  const int p_begin = (int)(c * A.chunk_pix);
-  const int p_end = (int)((p_begin + A.chunk_pix < HW) ? p_begin + A.chunk_pix : HW);
-  for (int sb = p_begin; sb < p_end; sb += kSpSB) {
-    const int sb_end = sb + kSpSB < p_end ? sb + kSpSB : p_end;
-    // 1. this sub-batch's valid pixels (offsets from sb) into the list, in
-    //    pixel order: thread t owns pixels sb + 32 t .. + 31 (8 nibble bytes)
-    const int pb = sb + 32 * tid;
-    uint64_t w8 = 0;
-    if (pb < sb_end) {
-      w8 = *reinterpret_cast<const uint64_t *>(vm + (pb >> 2));
-    }
-    // keep the low nibble of each byte, and only the pixels before sb_end
-    uint32_t bits = 0;  // pixel q of the thread's 32 -> bit q
-#pragma unroll
-    for (int by = 0; by < 8; by++) bits |= (uint32_t)((w8 >> (8 * by)) & 0xfu) << (4 * by);
-    if (pb + 32 > sb_end) bits &= pb < sb_end ? ((1u << (sb_end - pb)) - 1u) : 0u;
-    int tot = 0;
-    int off = block_excl_scan(__builtin_popcount(bits), wsum, &tot);
-    for (uint32_t v = bits; v; v &= v - 1) list[off++] = (uint16_t)(32 * tid + __builtin_ctz(v));
-    __syncthreads();
-    // 2. rounds of 128 entries, wave w taking rounds w, w + NW, ...
-    const int n = tot, R = (n + 127) / 128;
-    auto issue = [&](int r, int buf) {
-      const int e0 = 128 * r + 2 * ln;
-      const int i0 = sp_list(la + 2 * (e0 < n ? e0 : n - 1)), i1 = sp_list(la + 2 * (e0 + 1 < n ? e0 + 1 : n - 1));
-      const int p0 = sb + i0, p1 = sb + i1;
-#pragma unroll
-      for (int k = 0; k < NPL; k++) {
-        buf_lds4_nt(Rp[k], (__attribute__((address_space(3))) void *)(&slot[wv][buf][k][0]), 4 * p0, 0);
-        buf_lds4_nt(Rp[k], (__attribute__((address_space(3))) void *)(&slot[wv][buf][NF + k][0]), 4 * p1, 0);
-      }
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(Rx, (__attribute__((address_space(3))) void *)(&slot[wv][buf][NPL + k][0]), 4, 12 * p0 + 4 * k, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(Rx, (__attribute__((address_space(3))) void *)(&slot[wv][buf][NF + NPL + k][0]), 4, 12 * p1 + 4 * k, 0, 0, 0);
-      }
-    };
-    int buf = 0;
-    if (wv < R) issue(wv, 0);
-    for (int r = wv; r < R; r += NW, buf ^= 1) {
-      if (r + NW < R) {
-        issue(r + NW, buf ^ 1);
-        if constexpr (NF == 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      float f[2 * NF];
-      sp_read<NF>((uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const float *)&slot[wv][buf][0][ln]), f);
-      const int e0 = 128 * r + 2 * ln;
-      f32x2 in[NPL], X[3];
-#pragma unroll
-      for (int k = 0; k < NPL; k++) in[k] = f32x2{f[k], f[NF + k]};
-      if (e0 >= n) in[SQK].x = 0.0f;  // a repeated entry: zero weight
-      if (e0 + 1 >= n) in[SQK].y = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; k++) X[k] = f32x2{f[NPL + k], f[NF + NPL + k]};
-      f32x2 Y[3];
-      act2(Tm, X, Y);
-      pixel_contrib2<MODE, NPL, false>(acc, P, in, Y);
-    }
-    __syncthreads();  // the list is rewritten by the next sub-batch
-  }
-  float sums[kNP];
-#pragma unroll
-  for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
-  if constexpr (MODE == 2 && M3S_CAL25) acc.cal25_fixup();
   acc.fold(sums);
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
@@ -1997,31 +1668,12 @@ __device__ __forceinline__ void wave_lds_fence() {
 #endif
 constexpr int kStage = M3S_STAGE;                  // updates per staged batch
 constexpr int kSplitUpdates = M3S_SPLIT_UPDATES;   // updates per PART item (global factors)
-#ifndef M3S_LDS_SPLIT  // updates per PART item on the LDS-resident path (0: none)
-#define M3S_LDS_SPLIT 0
-#endif
-constexpr int kLdsSplit = M3S_LDS_SPLIT;
 constexpr int kStageDoubles = 2 * kStage * 49;  // per wave
 #ifndef M3S_TAIL_TR  // dense-tail trailing update tile, in 7x7 blocks
 #define M3S_TAIL_TR 2
 #endif
 #ifndef M3S_TAIL_TC
 #define M3S_TAIL_TC 2
-#endif
-#ifndef M3S_TAIL_LOOKAHEAD  // DIAG(k+1) inside step k's trailing update (dense tail)
-#define M3S_TAIL_LOOKAHEAD 1
-#endif
-#ifndef M3S_FORMX4  // the dense tail's back-substitution: x_K's dot products over 4 lane groups (A/B)
-#define M3S_FORMX4 0
-#endif
-#ifndef M3S_FIN_PRELOAD  // col_finish: the wave's poses loaded up front (A/B)
-#define M3S_FIN_PRELOAD 0
-#endif
-#ifndef M3S_BS49  // sparse_llt_kernel's level-synchronous back-substitution on 56 lanes (round 5)
-#define M3S_BS49 1
-#endif
-#ifndef M3S_BS_SYNC  // sparse_llt_kernel: level-synchronous back-substitution (round 5; 0 = dataflow)
-#define M3S_BS_SYNC 1
 #endif
 
 // Cross-workgroup hand-off of doubles (column-task kernels): write-through
@@ -2426,15 +2078,8 @@ template <bool STAGE, bool SC1 = false>
 __device__ __forceinline__ void border_task(int t, int nc, int c0, const int32_t *pl, const int *off, double *Lb,
                                             double *y, int r7, int c7, int lane49, int lane, int lane7, bool act49,
                                             double *stg, double *Ad = nullptr, int ld = 0,
-                                            const int32_t *wflag = nullptr, int want = 0, bool *ok = nullptr,
-                                            bool wt = false) {
-  // wt: write-through stores (a concurrent tail launch reads them after a flag)
-  auto put = [&](double *p, double v) {
-    if (wt)
-      st_sc1(p, v);
-    else
-      *p = v;
-  };
+                                            const int32_t *wflag = nullptr, int want = 0, bool *ok = nullptr) {
+  auto put = [&](double *p, double v) { *p = v; };
   const int32_t *dtr_ptr = pl + off[6], *dtr_slot = pl + off[7], *dtr_p = pl + off[8], *task_dst = pl + off[10],
                 *task_tr_ptr = pl + off[12], *tr_a = pl + off[13], *tr_b = pl + off[14];
   const int32_t *clq = pl + off[28];
@@ -2670,7 +2315,7 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       M3S_POLL(q0, q1, flag_set(&sdone[dtr_slot[q]]), (v = sub_products<STAGE, true>(v, Lb, dtr_slot, dtr_slot, qa, qb, r7, c7, lane49, lane, stg)));
       M3S_LSTAMP(it, 1);
       double wcol[7];
-      const bool bad = diag_factor<false, M3S_DIAG_RL>(v, k, Lb, Di, scr, lane, l7, wcol);
+      const bool bad = diag_factor<false, true>(v, k, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;  // still published: no waiter hangs
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sdone[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2753,24 +2398,18 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     auto tail_diag = [&](int kk) {
       const double v = Lb[(size_t)kk * 49 + lane49];
       double wcol[7];
-      const bool bad = diag_factor<false, M3S_DIAG_RL>(v, kk, Lb, Di, scr, lane, l7, wcol);
+      const bool bad = diag_factor<false, true>(v, kk, Lb, Di, scr, lane, l7, wcol);
       if (bad && lane == 0) fail_s = 1;
       fwd_solve_store(y[kk * 7 + lane7], wcol, scr, y + (size_t)kk * 7, lane);
     };
-#if M3S_TAIL_LOOKAHEAD
     // look-ahead: DIAG(k+1) runs on wave 0 inside step k's trailing update,
     // right after its first tile (which holds block (k+1, k+1)), so each
     // column costs two workgroup barriers instead of three
     if (wave == 0) tail_diag(c0);
     __syncthreads();
-#endif
     for (int ci = 0; ci < nc; ci++) {
       const int k = c0 + ci;
       const int col0 = cbase + ci * nc - ci * (ci + 1) / 2;  // slot of L_{k+1, k}
-#if !M3S_TAIL_LOOKAHEAD
-      if (wave == 0) tail_diag(k);
-      __syncthreads();
-#endif
       const int nr = nc - ci - 1;
       for (int rr = wave; rr < nr; rr += NW) {
         const int dst = col0 + rr;
@@ -2804,13 +2443,9 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
       const int nrt = (nr + kTR - 1) / kTR, nct = (nr + kTC - 1) / kTC;
       int ntile = 0;
       for (int ct = 0; ct < nct; ct++) ntile += nrt - ct * kTC / kTR;
-#if M3S_TAIL_LOOKAHEAD
       // tile 0 holds block (k+1, k+1): wave 0 takes it, then runs DIAG(k+1),
       // then joins the others on the ticketed remaining tiles
       for (int t = wave == 0 ? 0 : wave_ticket(&next_tile); t < ntile; t = wave_ticket(&next_tile)) {
-#else
-      for (int t = wave; t < ntile; t += NW) {
-#endif
         int ct = 0, rem = t;  // t -> (ct, rt), rt >= ct * kTC / kTR, column-major
         while (rem >= nrt - ct * kTC / kTR) rem -= nrt - ct * kTC / kTR, ct++;
         const int r_0 = kTR * (ct * kTC / kTR + rem), c_0 = kTC * ct;
@@ -2853,12 +2488,10 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
           for (int q = 0; q < kTB; q++)
             if (r_0 + q / kTC < nr && c_0 + q % kTC <= r_0 + q / kTC) Lb[(size_t)sd[q] * 49 + lane] = vd[q];
         }
-#if M3S_TAIL_LOOKAHEAD
         if (t == 0) {  // wave 0: block (k+1, k+1) is final (this tile, rr = cc = 0)
           wave_lds_fence();
           tail_diag(k + 1);
         }
-#endif
       }
       __syncthreads();
     }
@@ -2898,21 +2531,20 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
   if (tid < m) T_pre = load_sim3(D.Twc + 8 * (size_t)(tid + 1));
 
   // 2. back-substitution L^T x = y in reverse level order (x overwrites y).
-#if M3S_BS_SYNC
   // Level-synchronous (round 5): the columns of one elimination-tree level
   // run side by side on the waves, a workgroup barrier between levels (every
   // row of struct(k) is an ancestor, at a higher level). The per-column sums
   // are the dataflow's (sub_matvec in list order): bitwise the same x. The
   // dataflow form paid a flag poll (s_sleep granularity), a release fence and
   // an LDS ticket per column on the chain: ~2k cycles per level at C3.
-  // M3S_BS49 (round 5, factor in LDS): a column on 56 lanes, lane 8a + b
+  // Round 5 (factor in LDS): a column on 56 lanes, lane 8a + b
   // holding term b of row a: every block's L_ik and x_i entry of the lane in
   // one LDS load each, all blocks' loads in flight, the products summed over
   // the blocks per lane, then over b by three DPP steps; W_k^T r the same way
   // through the wave's scratch. The 7-lane form ran each block as 7 dependent
   // LDS-operand FMAs and the W product as 7 readlane broadcasts (~2k cycles
   // per level at C3). Another summation order: x within fp64 round-off.
-  if (M3S_BS49 && !STAGE) {
+  if (!STAGE) {
     const int32_t *lev_ptr = pl + D.off[4];
     const int a8 = lane >> 3, b8 = lane & 7;
     const bool act = a8 < 7 && b8 < 7;
@@ -2963,12 +2595,6 @@ __global__ void __launch_bounds__(1024) sparse_llt_kernel(SparseDev D) {
     }
   }
   for (; false;) {
-#else
-  // dataflow: column k waits for x_i of every i in struct(k)
-  // columns are taken dynamically in reverse level order; the x_i terms are
-  // applied as they arrive (lane-parallel flag polling, list order)
-  for (;;) {
-#endif
     const int t = wave_ticket(&next_col);
     if (t >= m) break;
     const int k = lev_col[m - 1 - t];
@@ -3205,12 +2831,8 @@ struct DfArgs {
   double *tail_A;
   int tail_ld;
   double *Wgr;     // [m][49] W_k as {value, epoch tag} 16-B granules (round 3)
-  int32_t *btflag;  // non-null: border task b publishes btflag[b] = epoch + 1 (the tail runs concurrently)
 };
 constexpr int kDfWaves = 4;
-#ifndef M3S_DF_WGRAN  // df_factor_kernel: OFF items take W_k from tagged granules (one round trip)
-#define M3S_DF_WGRAN 1
-#endif
 
 __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
   if (D.flags[kFlagStop]) return;
@@ -3261,7 +2883,7 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       if (lane == 0) M3S_CSTAMP(0, k, 2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(D.sdone + k, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (M3S_DF_WGRAN && lane < 7) {
+      if (lane < 7) {
         // W_k as tagged granules (after the drain: an OFF item that sees a
         // tag also sees y_k and L_kk): entry qq * 7 + lane of Dinv[k]
         const __amdgpu_buffer_rsrc_t RG =
@@ -3284,7 +2906,6 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       double v = L[(size_t)dst * 49 + lane49];
       v = sub_products<true, false, true>(v, L, tr_a, tr_b, q0, q1, r7, c7, lane49, lane, stg, D.sdone, want, &ok);
       if (lane == 0) M3S_CSTAMP(3, dst, 1);
-#if M3S_DF_WGRAN
       {  // W_k from its tagged granules: the poll and the payload are one load
         const __amdgpu_buffer_rsrc_t RG =
             __builtin_amdgcn_make_buffer_rsrc(D.Wgr, 0, (int)(16 * 49 * (D.m + 1)), 0x00020000);
@@ -3304,12 +2925,6 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       }
       if (!ok && lane == 0) set_fail(D.flags);
       if (lane == 0) M3S_CSTAMP(3, dst, 2);
-#else
-      ok &= wait_flags(D.sdone, task_col, code, code + 1, BIG, want, lane);  // DIAG(k)
-      if (!ok && lane == 0) set_fail(D.flags);
-      if (lane == 0) M3S_CSTAMP(3, dst, 2);
-      if (act49) W[lane] = ld_sc1(D.Dinv + (size_t)k * 49 + lane);
-#endif
       if (act49) scr[lane] = v;
       wave_lds_fence();
       double x = 0.0;
@@ -3328,239 +2943,19 @@ __global__ void __launch_bounds__(64 * kDfWaves) df_factor_kernel(DfArgs D) {
       // at 256 KFs after the last column was published)
       bool ok = true;
       border_task<true, true>(bt, nc, D.c0, pl, D.off, L, D.y, r7, c7, lane49, lane, lane7, act49, stg, D.tail_A,
-                              D.tail_ld, D.sdone, want, &ok, D.btflag != nullptr);
+                              D.tail_ld, D.sdone, want, &ok);
       if (!ok && lane == 0) set_fail(D.flags);
-      if (D.btflag) {  // the concurrent tail launch waits for its columns' border blocks (write-through above)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(D.btflag + bt, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
   }
 }
 
-#ifdef M3S_TEST_PATHS  // A/B path (M3S_SUBTREE=1): measured slower than df_factor_kernel
-// ---------------------------------------- subtrees in LDS (round 4) --
-// Large graphs: the sparse columns below the dense tail split into subtrees
-// whose update lists stay inside the subtree (every row of struct(k) is an
-// etree ancestor of k; m3s_symbolic.h, build_subtree_image). One 1024-thread
-// workgroup per subtree runs its DIAG / OFF items as a dataflow over LDS
-// completion flags, with W_k, y_k and the blocks that fit in LDS (the rest,
-// border rows first, in global memory), instead of df_factor_kernel's
-// cross-CU hand-offs (~2 per etree level at ~1-3 us each). Every finished
-// block, W_k and y_k also goes to the global factor (write-through stores,
-// drained, then the slot's epoch flag), so the border tasks, the dense tail
-// and the column back-substitution read exactly what df_factor_kernel leaves
-// there. Per block the same products in the same order (the global plan's
-// ascending-p update lists, diag_factor without readlanes): bitwise the same
-// factor as df_factor_kernel. (SimplicialLLT's factor, gn_kernels.cu:132-153.)
-struct SubArgs {
-  const int32_t *sub;  // subtree image (in the plan upload)
-  double *L, *Dinv, *y;  // global factor: slots (assembled values in, L out), W_k, RHS in / y out
-  int32_t *sdone;        // [S] slot epoch flags (diagonal slot k: W_k and y_k)
-  int want;
-  int32_t *flags;
-  double *Wgr;           // [m][49] W_k as tagged granules (df_factor_kernel's border OFF items read them)
-  int m;
-};
-constexpr int kSubWaves = 16;
 
-// entry e of local block b: LDS (b < nlds) or the global slot (sc1: another
-// wave of this workgroup wrote it write-through; L1 may hold a stale line)
-__device__ __forceinline__ double sub_blk(const double *Bl, const double *Lg, const int32_t *gsl, int nlds, int b,
-                                          int e) {
-  return b < nlds ? Bl[b * 49 + e] : ld_sc1(Lg + (size_t)gsl[b] * 49 + e);
-}
-
-// the update sums of subtree_factor_kernel over the ready entries [qa, qb):
-// DIAG v -= L_kp L_kp^T (entry layout), forward bb -= L_kp y_p (row layout),
-// OFF v -= L_ip L_kp^T; per block the sub_products / sub_matvec sums
-__device__ __forceinline__ double sub_upd_diag(double v, const double *Bl, const double *Lg, const int32_t *gsl,
-                                               int nlds, const int32_t *dlist, int qa, int qb, int r7, int c7) {
-  for (int qq = qa; qq < qb; qq++) {
-    const int b = dlist[2 * qq];
-    double s0 = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < 7; mm++) s0 += sub_blk(Bl, Lg, gsl, nlds, b, r7 + mm) * sub_blk(Bl, Lg, gsl, nlds, b, c7 + mm);
-    v -= s0;
-  }
-  return v;
-}
-__device__ __forceinline__ double sub_upd_fwd(double bb, const double *Bl, const double *Lg, const int32_t *gsl,
-                                              int nlds, const int32_t *dlist, const double *yl, int qa, int qb,
-                                              int l7) {
-  for (int qq = qa; qq < qb; qq++) {
-    const int b = dlist[2 * qq], pp = dlist[2 * qq + 1];
-    double t0 = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < 7; mm++) t0 += sub_blk(Bl, Lg, gsl, nlds, b, l7 + mm) * yl[pp * 7 + mm];
-    bb -= t0;
-  }
-  return bb;
-}
-__device__ __forceinline__ double sub_upd_off(double v, const double *Bl, const double *Lg, const int32_t *gsl,
-                                              int nlds, const int32_t *tlist, int qa, int qb, int r7, int c7) {
-  for (int qq = qa; qq < qb; qq++) {
-    const int ba = tlist[2 * qq], bb2 = tlist[2 * qq + 1];
-    double s0 = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < 7; mm++)
-      s0 += sub_blk(Bl, Lg, gsl, nlds, ba, r7 + mm) * sub_blk(Bl, Lg, gsl, nlds, bb2, c7 + mm);
-    v -= s0;
-  }
-  return v;
-}
-
-__global__ void __launch_bounds__(64 * kSubWaves) subtree_factor_kernel(SubArgs A) {
-  if (A.flags[kFlagStop]) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ double wsc[kSubWaves][64];
-  __shared__ int tk[2], fail_s;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int32_t *rec = A.sub + A.sub[1 + blockIdx.x];
-  const int ncol = rec[0], nblk = rec[1], nlds = rec[2], nA = rec[3], nB = rec[4], nwA = rec[14];
-  const int32_t *cols = A.sub + rec[5], *gsl = A.sub + rec[6], *itA = A.sub + rec[7], *itB = A.sub + rec[8],
-                *dptr = A.sub + rec[9], *dlist = A.sub + rec[10], *tcol = A.sub + rec[11], *tptr = A.sub + rec[12],
-                *tlist = A.sub + rec[13];
-  double *Wl = smem, *yl = Wl + (size_t)ncol * 49;
-  int32_t *bfl = reinterpret_cast<int32_t *>(yl + (size_t)ncol * 7), *wfl = bfl + nblk, *yfl = wfl + ncol;
-  double *Bl = reinterpret_cast<double *>(yfl + ncol + ((nblk + 2 * ncol) & 1));  // 8-B aligned
-  for (int q = tid; q < nblk + 2 * ncol; q += 64 * kSubWaves) bfl[q] = 0;
-  if (tid == 0) tk[0] = 0, tk[1] = 0, fail_s = 0;
-  double *L = A.L;
-  // the assembled values (assemble_slots_kernel) of the LDS blocks, the
-  // diagonal blocks (into the W area, which DIAG(c) overwrites with W_k) and
-  // the RHS (into y), every load of a batch in flight: no item then waits on
-  // a global load of its own input
-  {
-    const int nb49 = nlds * 49, nd49 = ncol * 49, ny = ncol * 7, tot = nb49 + nd49 + ny;
-    for (int i0 = 0; i0 < tot; i0 += 8 * 64 * kSubWaves) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * 64 * kSubWaves + tid;
-        if (i < nb49) v[u] = L[(size_t)gsl[i / 49] * 49 + i % 49];
-        else if (i < nb49 + nd49) v[u] = L[(size_t)cols[(i - nb49) / 49] * 49 + (i - nb49) % 49];
-        else if (i < tot) v[u] = A.y[(size_t)cols[(i - nb49 - nd49) / 7] * 7 + (i - nb49 - nd49) % 7];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * 64 * kSubWaves + tid;
-        if (i < nb49) Bl[i] = v[u];
-        else if (i < nb49 + nd49) Wl[i - nb49] = v[u];
-        else if (i < tot) yl[i - nb49 - nd49] = v[u];
-      }
-    }
-  }
-  __syncthreads();
-  const int r = lane / 7, c = lane % 7;
-  const bool act49 = lane < 49;
-  const int lane49 = act49 ? lane : 0, r7 = act49 ? r * 7 : 0, c7 = act49 ? c * 7 : 0;
-  const int lane7 = lane < 7 ? lane : 0, l7 = lane7 * 7;
-  double *scr = wsc[wave];
-  // lists: waves [0, nwA) start on A (DIAG + internal OFF), the others on B
-  // (border OFF); an exhausted list sends its waves to the other one. A items
-  // never wait for B items, so A always completes, then B.
-  int lst = wave < nwA ? 0 : 1;
-  bool other_tried = false;
-  for (;;) {
-    const int t = wave_ticket(&tk[lst]);
-    if (t >= (lst ? nB : nA)) {
-      if (other_tried) break;
-      other_tried = true;
-      lst ^= 1;
-      continue;
-    }
-    const int code = lst ? itB[t] : itA[t];
-    if (code < 0) {  // DIAG(c): D_k - sum_p L_kp L_kp^T -> L_kk, W_k; then y_k
-      const int cc = -1 - code, k = cols[cc];
-      if (lane == 0) M3S_CSTAMP(0, k, 0);
-      double v = Wl[cc * 49 + lane49];  // assembled D_k (staged)
-      const int q0 = dptr[cc], q1 = dptr[cc + 1];
-      M3S_POLL(q0, q1, flag_set(&bfl[dlist[2 * q]]), (v = sub_upd_diag(v, Bl, L, gsl, nlds, dlist, qa, qb, r7, c7)));
-      if (lane == 0) M3S_CSTAMP(0, k, 1);
-      double wcol[7];
-      const bool bad = diag_factor<true>(v, k, L, A.Dinv, scr, lane, l7, wcol, Wl + (size_t)cc * 49);
-      if (bad && lane == 0) set_fail(A.flags);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&wfl[cc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (lane == 0) M3S_CSTAMP(0, k, 2);
-      // forward step y_k = W_k (b_k - sum_p L_kp y_p)
-      double bb = yl[cc * 7 + lane7];  // b_k (staged)
-      M3S_POLL(q0, q1, flag_set(&yfl[dlist[2 * q + 1]]), (bb = sub_upd_fwd(bb, Bl, L, gsl, nlds, dlist, yl, qa, qb, l7)));
-      // y_k = W_k bb (fwd_solve_store's sums), to LDS and the global RHS
-      if (lane < 7) {
-#pragma unroll
-        for (int rr = 0; rr < 7; rr++) scr[rr * 7 + lane] = wcol[rr] * bb;
-      }
-      wave_lds_fence();
-      if (lane < 7) {
-        double yo = 0.0;
-#pragma unroll
-        for (int q = 0; q < 7; q++) yo += scr[lane * 7 + q];
-        yl[cc * 7 + lane] = yo;
-        st_sc1(A.y + (size_t)k * 7 + lane, yo);
-      }
-      wave_lds_fence();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&yfl[cc], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (lane < 7) {
-        // W_k as tagged granules for the border-row OFF items (df_factor_kernel,
-        // the next launch; the global slot flags are set at this kernel's end)
-        const __amdgpu_buffer_rsrc_t RG =
-            __builtin_amdgcn_make_buffer_rsrc(A.Wgr, 0, (int)(16 * 49 * (A.m + 1)), 0x00020000);
-#pragma unroll
-        for (int qq = 0; qq < 7; qq++) {
-          const unsigned long long bw = (unsigned long long)__double_as_longlong(wcol[qq]);
-          const u32x4 gw = {(unsigned)(bw & 0xffffffffu), (unsigned)(bw >> 32), (unsigned)A.want, 0u};
-          __builtin_amdgcn_raw_buffer_store_b128(gw, RG, (k * 49 + qq * 7 + lane) * 16, 0, 16);
-        }
-      }
-      if (lane == 0) M3S_CSTAMP(0, k, 3);
-    } else {  // OFF(b): L_ik = (A_ik - sum_p L_ip L_kp^T) W_k^T
-      const int b = code, cc = tcol[b], dst = gsl[b];
-      if (lane == 0) M3S_CSTAMP(3, dst, 0);
-      double v = b < nlds ? Bl[b * 49 + lane49] : L[(size_t)dst * 49 + lane49];  // assembled A_ik (staged)
-      const int q0 = tptr[b], q1 = tptr[b + 1];
-      M3S_POLL(q0, q1, flag_set(&bfl[tlist[2 * q]]) && flag_set(&bfl[tlist[2 * q + 1]]),
-               (v = sub_upd_off(v, Bl, L, gsl, nlds, tlist, qa, qb, r7, c7)));
-      if (lane == 0) M3S_CSTAMP(3, dst, 1);
-      wait_flag(&wfl[cc], &fail_s);  // W_k
-      if (lane == 0) M3S_CSTAMP(3, dst, 2);
-      if (act49) scr[lane] = v;
-      wave_lds_fence();
-      double x = 0.0;
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) x += scr[r7 + mm] * Wl[cc * 49 + c7 + mm];
-      wave_lds_fence();
-      if (act49) {
-        if (b < nlds) Bl[b * 49 + lane] = x;
-        st_sc1(L + (size_t)dst * 49 + lane, x);
-      }
-      // a block in LDS is published at once; a global-only block once its
-      // write-through copy has left (other waves read it with sc1 loads)
-      if (b >= nlds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) {
-        __hip_atomic_store(&bfl[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        M3S_CSTAMP(3, dst, 3);
-      }
-    }
-  }
-  // every internal block, W_k and y_k of this subtree is final: the global
-  // slot flags that df_factor_kernel's border items poll (next launch; the
-  // border blocks themselves are its items, so their flags stay unset)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int n_int = rec[19];
-  for (int b = tid; b < n_int + ncol; b += 64 * kSubWaves)
-    __hip_atomic_store(A.sdone + (b < n_int ? gsl[b] : cols[b - n_int]), A.want, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (tid == 0 && fail_s) set_fail(A.flags);
-}
-#endif  // M3S_TEST_PATHS
-
-// dx = -x (original order), retraction, ||dx|| test (one wave; x in y, sc1)
+// dx = -x (original order), retraction, ||dx|| test (one wave). x is read
+// from C.y with plain loads: the acquire below makes every other workgroup's
+// released x visible, whichever caller this is (the callers also acquire
+// after their final ticket; a kernel boundary precedes the ncols == 0 call).
 __device__ void col_finish(const ColArgs &C, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __shared__ float dxs[7 * 512];
   const int32_t *perm = C.plan + C.off[0];
   const int m = C.m;
@@ -3581,15 +2976,6 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
   // the poses this wave retracts, all in flight now (clamped indices, no
   // guards: a guarded load per pose was one dependent round trip each, round 5)
-#if M3S_FIN_PRELOAD
-  constexpr int kFinP = 8;  // m <= 512 on the chip-wide path
-  Sim3f Tp[kFinP];
-#pragma unroll
-  for (int u = 0; u < kFinP; u++) {
-    const int p = min(lane + 64 * u, m - 1);
-    Tp[u] = load_sim3(C.Twc + 8 * (size_t)(p + 1));
-  }
-#endif
   // every x_k was published before this workgroup's ticket and the caller's
   // agent-scope acquire: plain loads, all in flight at once (one relaxed
   // atomic load per entry was one dependent fabric round trip each: ~28 per
@@ -3618,18 +3004,6 @@ __device__ void col_finish(const ColArgs &C, int lane) {
   }
   part = wave_sum_pl(part);
   wave_lds_fence();
-#if M3S_FIN_PRELOAD
-#pragma unroll
-  for (int u = 0; u < kFinP; u++) {
-    const int p = lane + 64 * u;
-    if (p < m) {
-      float xi[7];
-#pragma unroll
-      for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
-      store_sim3(C.Twc + 8 * (size_t)(p + 1), retract_f64(xi, Tp[u]));
-    }
-  }
-#else
   for (int p = lane; p < m; p += 64) {
     const Sim3f T = load_sim3(C.Twc + 8 * (size_t)(p + 1));
     float xi[7];
@@ -3637,7 +3011,6 @@ __device__ void col_finish(const ColArgs &C, int lane) {
     for (int q = 0; q < 7; q++) xi[q] = dxs[p * 7 + q];
     store_sim3(C.Twc + 8 * (size_t)(p + 1), retract_f64(xi, T));
   }
-#endif
   if (lane == 0) {
     C.info[M3S_INFO_ITERS] += 1;
     if (sqrtf(part) < C.delta_thresh) {
@@ -3646,128 +3019,6 @@ __device__ void col_finish(const ColArgs &C, int lane) {
     }
   }
 }
-
-#ifdef M3S_TEST_PATHS
-// Back-substitution of the subtrees (round 4; replaces col_backsub_kernel on
-// the subtree path): one 1024-thread workgroup per subtree. The tail's x is
-// final (tail_cyc_kernel), so every border term L_ik^T x_i (i in the tail) is
-// formed up front, all in flight at once, together with W_k and the internal
-// blocks into LDS; then the columns run from the subtree's root down as a
-// dataflow over LDS flags (x_k = W_k^T (y_k - sum_i L_ik^T x_i), rows
-// ascending: col_backsub_kernel's per-block sums in its order, bitwise the
-// same x). The workgroup that finishes last writes dx, retracts and tests
-// ||dx|| (col_finish), as col_backsub_kernel's last column did.
-struct SubBsArgs {
-  const int32_t *sub;
-  int ns;
-  int32_t *fin_ctr;  // workgroups finished, epoch-based
-  ColArgs C;
-};
-
-__global__ void __launch_bounds__(64 * kSubWaves) subtree_backsub_kernel(SubBsArgs A) {
-  const ColArgs &C = A.C;
-  if (C.flags[kFlagStop]) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int tk, last_s, fail_s;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int32_t *rec = A.sub + A.sub[1 + blockIdx.x];
-  const int ncol = rec[0], nblk = rec[1], n_int = rec[19], n_li = rec[20], nbd = nblk - n_int;
-  const int32_t *cols = A.sub + rec[5], *gsl = A.sub + rec[6], *ci = A.sub + rec[15], *cb = A.sub + rec[16],
-                *brow = A.sub + rec[17], *corder = A.sub + rec[18];
-  double *Wt = smem, *xl = Wt + (size_t)ncol * 49, *tb = xl + (size_t)ncol * 7, *Li = tb + (size_t)nbd * 7;
-  int32_t *xfl = reinterpret_cast<int32_t *>(Li + (size_t)n_li * 49);
-  const double *L = C.L;
-  // phase 0: W_k and the internal blocks to LDS, the border terms (every load
-  // of a batch in flight); the factor and the tail's x are final (earlier launches)
-  for (int i0 = 0; i0 < ncol * 49; i0 += 4096) {
-    double v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + u * 1024 + tid;
-      if (i < ncol * 49) v[u] = C.Dinv[(size_t)cols[i / 49] * 49 + i % 49];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + u * 1024 + tid;
-      if (i < ncol * 49) Wt[i] = v[u];
-    }
-  }
-  for (int i0 = 0; i0 < n_li * 49; i0 += 4096) {
-    double v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + u * 1024 + tid;
-      if (i < n_li * 49) v[u] = L[(size_t)gsl[i / 49] * 49 + i % 49];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + u * 1024 + tid;
-      if (i < n_li * 49) Li[i] = v[u];
-    }
-  }
-  for (int i = tid; i < nbd * 7; i += 1024) {  // (border block, entry): L_ik^T x_i, sub_matvec<TRANS>'s sum
-    const int b = n_int + i / 7, l = i % 7;
-    const double *Lb = L + (size_t)gsl[b] * 49;
-    const double *xi = C.y + (size_t)brow[b] * 7;
-    double t0 = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < 7; mm++) t0 += Lb[mm * 7 + l] * xi[mm];
-    tb[i] = t0;
-  }
-  for (int i = tid; i < ncol * 7; i += 1024) xl[i] = C.y[(size_t)cols[i / 7] * 7 + i % 7];  // y_k (x_k later)
-  for (int q = tid; q < ncol; q += 1024) xfl[q] = 0;
-  if (tid == 0) tk = 0, last_s = 0, fail_s = 0;
-  __syncthreads();
-  const int lane7 = lane < 7 ? lane : 0;
-  for (;;) {
-    const int t = wave_ticket(&tk);
-    if (t >= ncol) break;
-    const int c = corder[ncol - 1 - t], k = cols[c];
-    if (lane == 0) M3S_CSTAMP(1, k, 0);
-    double rr = xl[c * 7 + lane7];  // y_k (staged)
-    for (int b = ci[c]; b < ci[c + 1]; b++) {
-      const int pc = brow[b];
-      wait_flag(&xfl[pc], &fail_s);
-      double t0 = 0.0;
-      if (b < n_li) {
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) t0 += Li[b * 49 + mm * 7 + lane7] * xl[pc * 7 + mm];
-      } else {
-        const double *Lb = L + (size_t)gsl[b] * 49;
-#pragma unroll
-        for (int mm = 0; mm < 7; mm++) t0 += Lb[mm * 7 + lane7] * xl[pc * 7 + mm];
-      }
-      rr -= t0;
-    }
-    if (lane == 0) M3S_CSTAMP(1, k, 1);
-    for (int b = cb[c]; b < cb[c + 1]; b++) rr -= tb[(b - n_int) * 7 + lane7];
-    double xk = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < 7; mm++) xk += Wt[c * 49 + mm * 7 + lane7] * readlane_d(rr, mm);
-    if (lane < 7) {
-      xl[c * 7 + lane] = xk;
-      st_sc1(C.y + (size_t)k * 7 + lane, xk);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(&xfl[c], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (lane == 0) M3S_CSTAMP(1, k, 2);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's x stores have left
-  __syncthreads();
-  if (tid == 0 && fail_s) set_fail(C.flags);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the failure flag before the arrival)
-  // the workgroup that finishes last finishes the step
-  if (tid == 0) {
-    const int f = __hip_atomic_fetch_add(A.fin_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = (f - C.epoch * A.ns == A.ns - 1);
-  }
-  __syncthreads();
-  if (last_s && wave == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    col_finish(C, lane);
-  }
-}
-#endif  // M3S_TEST_PATHS
 
 constexpr int kBsCap = 40;  // L_ik blocks of a column prefetched into LDS (the rest staged)
 __global__ void __launch_bounds__(64) col_backsub_kernel(ColArgs C) {
@@ -4198,9 +3449,6 @@ struct TailSync {
   double *LgT;     // the L tiles again, L(I,J) (not transposed) in the MFMA C layout, [tile][2][64 lanes][2] (back-substitution A operands)
   double *LgG;     // the L tiles as tagged granules, [tile][4][64 lanes] x {double, epoch tag, 0} (16 B; zeroed per call)
   int warm;        // 1: warm the diagonal factor's code on a dummy tile first (tail_diag_warm)
-  int zinv;        // 1: back-substitution through Z = L^-1, a column per workgroup (tail_zinv_col, round 5)
-  double *Zg;      // the tiles of Z, [tile (I, J)][64 lanes][4] (MFMA C layout)
-  const int32_t *btflag;  // non-null (round 5, concurrent launch): per border task epoch flags of df_factor_kernel
 };
 constexpr size_t kTailGranBytes = (size_t)kTailMaxT * (kTailMaxT + 1) / 2 * 64 * 4 * 16;
 
@@ -4354,21 +3602,12 @@ __device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSyn
     // x_K[r] = sum_i W_K^T[r][i] y'_K[i]: lane r + 16 g sums i in [4 g, 4 g + 4),
     // then the four groups by the permlane swaps (4 dependent FMAs + 2 swap
     // steps on the chain instead of 16 FMAs, round 5)
-#if M3S_FORMX4
-    const int r16 = lane & 15, g4 = lane >> 4;
-    double x = 0.0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) x += WlT[(K * 16 + r16) * 17 + 4 * g4 + i] * yv[16 * K + 4 * g4 + i];
-    x = sum_xor16_32(x);
-    if (lane < 16) xv[16 * K + lane] = lane < jv ? x : 0.0;
-#else
     if (lane < 16) {
       double x = 0.0;
 #pragma unroll
       for (int i = 0; i < 16; i++) x += WlT[(K * 16 + lane) * 17 + i] * yv[16 * K + i];
       xv[16 * K + lane] = lane < jv ? x : 0.0;
     }
-#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(xflag + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (lane == 0) M3S_CSTAMP(2, 700 + K, 0);
@@ -4423,88 +3662,6 @@ __device__ __forceinline__ void tail_backsub_wg(const TailArgs &A, const TailSyn
   if (tid == 0) M3S_CSTAMP(2, 511, 0);
 }
 
-// Round 5: the back-substitution without its chain. x = L^-T y' is Z^T y'
-// with Z = L^-1, and column J of Z needs only the factor:
-//   Z(J, J) = W_J,   Z(I, J) = -W_I sum_{K = J..I-1} L(I, K) Z(K, J)  (I > J),
-// a recursion down the rows that trails the factorisation by one tile
-// column (row I waits for column I's flag: W_I and the L(I, K) granules).
-// Every column runs on its own wave as soon as its workgroup's factor work
-// is done, so x_J = sum_I Z(I, J)^T y'_I follows the last column's flag after
-// a few MFMAs, where tail_backsub_wg ran a 1-2 us step per tile column after
-// it (~26 us at 256 KFs). The fp64 sums differ from the substitution's (the
-// explicit inverse of the triangular factor): dx agrees to fp64 round-off.
-// MEASURED SLOWER, test build only (knob tail_zinv): 256-KF calib 0.764 ->
-// 0.842 ms per 3-iteration call, 128 KFs 0.508 -> 0.514
-// (profiles/r05/solve_ab_zinv_REJECTED.txt). Column J's chain loads the
-// granule tiles L(I, J..I-1) of every row below it, one wave per column:
-// O(TC^3 / 6) tile reads (~1140 at 19 tiles against 171 distinct tiles), so
-// the early columns' chains fall behind the factor and the launch ends on
-// them instead of on the substitution it replaced.
-// L(I, K) as the A operand is its granule tile (the C layout of L^T); Z(K, J)
-// as the B operand is its C layout (register q = rows 4q..); -W_I as the A
-// operand is Wg's W^T read by (column, row); Z tiles live in global scratch
-// (each lane re-reads its own stores: per-thread order, no hand-off).
-__device__ __forceinline__ void tail_zinv_col(const TailArgs &A, const TailSync &S, int J, const double (*Wk)[17],
-                                              int lane) {
-  const int n = 7 * A.nc, TC = (n + 15) / 16;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int want = S.epoch + 1;
-  const __amdgpu_buffer_rsrc_t R = gran_rsrc(S.LgG);
-  f64x4 *Z = reinterpret_cast<f64x4 *>(S.Zg);
-  f64x4 z;
-#pragma unroll
-  for (int r = 0; r < 4; r++) z[r] = Wk[lk + 4 * r][lr];  // Z(J, J) = W_J
-  Z[tail_tile(J, J) * 64 + lane] = z;
-  bool ok = true;
-  for (int I = J + 1; I < TC && ok; I++) {
-    {  // column I's flag: W_I, y'_I and the L(I', I) granules are out
-      int spins = 0;
-      while (__hip_atomic_load(S.tflag + I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > kColSpins) {
-          ok = false;
-          break;
-        }
-      }
-    }
-    // the W_I operands first (their latency behind the sum)
-    double wa[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) wa[q] = -ld_sc1(A.Wg + (size_t)I * 256 + 16 * (4 * q + lk) + lr);
-    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    for (int K = J; K < I; K++) {
-      GranTile g;
-      gran_load(R, tail_tile(I, K), lane, g);  // final: tag want (column K's flag was seen)
-      const f64x4 a = gran_val(g);
-      const f64x4 zk = K == I - 1 ? z : Z[tail_tile(K, J) * 64 + lane];
-      f64x4 &acc = (K - J) & 1 ? acc1 : acc0;
-#pragma unroll
-      for (int q = 0; q < 4; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], zk[q], acc, 0, 0, 0);
-    }
-    const f64x4 sm = acc0 + acc1;
-    f64x4 zn = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < 4; q++) zn = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], sm[q], zn, 0, 0, 0);
-    z = zn;
-    Z[tail_tile(I, J) * 64 + lane] = z;
-  }
-  if (!ok) {
-    if (lane == 0) __hip_atomic_store(A.flags + kFlagSplitFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // x_J = sum_I Z(I, J)^T y'_I over the real rows (every column flag was seen)
-  double part = 0.0;
-  for (int I = J; I < TC; I++) {
-    const f64x4 zi = I == TC - 1 ? z : Z[tail_tile(I, J) * 64 + lane];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int row = 16 * I + lk + 4 * r;
-      part += row < n ? zi[r] * ld_sc1(S.ypg + row) : 0.0;
-    }
-  }
-  part = sum_xor16_32(part);
-  if (lane < 16 && 16 * J + lane < n) A.rhs[7 * A.c0 + 16 * J + lane] = part;
-}
 
 // Round 2: the L tiles go from workgroup to workgroup as tagged granules
 // (one hop = one store + one polled load), the panel follows the updates
@@ -4685,10 +3842,6 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_cyc_kernel(TailArgs A, T
     __hip_atomic_store(S.tflag + J, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     M3S_CSTAMP(2, J, 3);
   }
-  if (S.zinv) {
-    if (wave == 0) tail_zinv_col(A, S, J, Wk, lane);
-    return;
-  }
   if (J != TC - 1) return;
   tail_backsub_wg(A, S, yv, xv);
 }
@@ -4725,7 +3878,6 @@ struct GArgs {
   int nx, n_pairs;
   int32_t *task, *comb, *fin, *xt_ready;  // ticket / ticket / counter / flag words (colsync; zeroed per call)
   int32_t *cnt;                           // [m] chunks of X_k done (colsync; zeroed per call)
-  const int32_t *sdone;                   // non-null: df_factor_kernel's slot flags (it runs concurrently)
 };
 constexpr int kGBat = 8;    // sparse ancestors' X_i loads in flight per lane
 constexpr int kGCapS = 24;  // sparse ancestors' L_ik staged in LDS per wave (the rest read from global)
@@ -4799,11 +3951,6 @@ __device__ void gcol_worker(const ColArgs &C, const GArgs &G) {
     }
     ns = min(ns, kGMaxS);
     wave_lds_fence();
-    if (G.sdone) {  // df_factor_kernel runs beside this launch: column k's DIAG and blocks first
-      if (!g_poll(G.sdone + k, want) && lane == 0) set_fail(C.flags);
-      if (!g_wait_flags(G.sdone, col_slot, q0, q1, 0x7fffffff, want, lane) && lane == 0) set_fail(C.flags);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
     // the factor is final: the ancestors' L_ik and W_k by plain loads
     for (int e = lane; e < 49 * min(ns, kGCapS); e += 64) Lk[e] = C.L[(size_t)col_slot[q0 + sq[e / 49]] * 49 + e % 49];
     if (lane < 49) Wk[lane] = C.Dinv[(size_t)k * 49 + lane];
@@ -4941,28 +4088,7 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
   };
   if (tid == 0) fail_s = 0, wready[0] = 0, wready[1] = 0, lready = 0;
   for (int q = tid; q < 16 * kTailMaxT; q += 64 * kTailNW) yv[q] = 0.0;
-  if (S.btflag && wave == 0) {
-    // round 5, launched beside df_factor_kernel: the border blocks (ri, ci)
-    // of the pair's block columns ci, every row ri >= ci (one contiguous run
-    // of the column-major border tasks), then an acquire for the tile loads
-    const int nc = A.nc, cb0 = (16 * J0) / 7, cb1 = min(nc - 1, (16 * (J0 + jn) - 1) / 7);
-    const int t0 = cb0 * nc - cb0 * (cb0 - 1) / 2, t1 = cb1 * nc - cb1 * (cb1 - 1) / 2 + (nc - 1 - cb1);
-    int spins = 0;
-    for (int tb = t0; tb <= t1; tb += 64) {
-      const int t = tb + lane;
-      for (;;) {
-        const bool ok = t > t1 || __hip_atomic_load(S.btflag + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want;
-        if (__ballot(!ok) == 0) break;
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > kColSpins) {
-          if (lane == 0) fail_s = 1;
-          break;
-        }
-      }
-    }
-  }
   __syncthreads();
-  if (S.btflag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // acc0[u]: tile (I, J0)^T; acc1[u]: tile (I, J1)^T (rows I >= J1)
   f64x4 acc0[kRC], acc1[kRC];
 #pragma unroll
@@ -5113,9 +4239,6 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&wready[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (tid == 0) M3S_CSTAMP(2, J1, 2);
-      // the pair's own sub-diagonal tile as granules too: no other workgroup's
-      // factor reads it, but the Z recursion of column J0 does (tail_zinv_col)
-      if (S.zinv) gran_store(R, tail_tile(J1, J0), lane, d, want);
     }
     // W^T of each column ([16][16] row-major: element e = 16 l + r holds
     // W[r][l]): four stores of 64 consecutive elements, whole lines each
@@ -5265,10 +4388,6 @@ __global__ void __launch_bounds__(64 * kTailNW, 1) tail_pair_kernel(TailArgs A, 
     }
     for (int j = 0; j < jn; j++) __hip_atomic_store(S.tflag + J0 + j, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int j = 0; j < jn; j++) M3S_CSTAMP(2, J0 + j, 3);
-  }
-  if (S.zinv) {  // the pair's columns on waves 0 and 1
-    if (wave < jn) tail_zinv_col(A, S, J0 + wave, Wk[wave], lane);
-    return;
   }
   if ((int)blockIdx.x != (G.X ? G.n_pairs : (int)gridDim.x) - 1) return;
   tail_backsub_wg(A, S, yv, xv);
@@ -5563,7 +4682,7 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
       if (e < E) {
         const int ri = rank(ei[u]), rj = rank(ej[u]);
         A.rank_i[e] = ri, A.rank_j[e] = rj;
-        erj[e] = M3S_EORDER ? ri : rj;
+        erj[e] = rj;
       }
     }
   } else {
@@ -5594,7 +4713,7 @@ __global__ void __launch_bounds__(kProThreads) gn_prologue_kernel(ProArgs A) {
       if (e < E) {
         const int ri = lower_bound_i64(uniq, nu, ei[u]), rj = lower_bound_i64(uniq, nu, ej[u]);
         A.rank_i[e] = ri, A.rank_j[e] = rj;
-        erj[e] = M3S_EORDER ? ri : rj;
+        erj[e] = rj;
       }
     }
   }
@@ -5698,14 +4817,12 @@ int launch_linearize(const LinArgs &L, int64_t blocks, bool vec, int pack, hipSt
     else
       linearize_kernel<MODE, TRACK, false, false><<<g, b, 0, st>>>(L);
   } else if (pack == 1) {
-    if (vec && M3S_GATHER_LDS && gather_lds_path() && L.HW <= (int64_t(1) << 24))  // (24-bit index products)
+    if (vec && gather_lds_path() && L.HW <= (int64_t(1) << 24))  // (24-bit index products)
       launch_lin(linearize_gather_kernel<MODE>, g, b, st, L);
     else if (vec)
       launch_lin(linearize_kernel<MODE, false, true, true>, g, b, st, L);
     else
       launch_lin(linearize_kernel<MODE, false, false, true>, g, b, st, L);
-  } else if (M3S_PK_SPARSE && L.vmask) {
-    launch_lin(linearize_sparse_kernel<MODE>, g, b, st, L);
   } else {
     launch_lin(linearize_packed_kernel<MODE>, g, b, st, L);
   }
@@ -5781,14 +4898,11 @@ struct Knobs {
   std::atomic<int> border_split{1};    // M3S_BORDER_SPLIT: 0 = tail border in the one-workgroup kernel
   std::atomic<int> debug_drop_item{-1};  // drop one LLT dispatch item (bounded-wait test)
   std::atomic<int> gather_lds{1};      // 0: the round-2 VGPR-staged gathering kernel (bitwise reference)
-  std::atomic<int> subtree{0};         // 1: the subtree kernels (one LDS workgroup per subtree; measured slower)
   std::atomic<int> tail_pair{1};       // 0: tail_cyc_kernel (one tile column per workgroup)
   std::atomic<int> tail_warm{1};       // 0: no warm-up of the tail's diagonal factor code
-  std::atomic<int> tail_zinv{0};       // 1: the tail's back-substitution through Z = L^-1 (round 5; measured slower)
   std::atomic<int> gcomb{1};           // 0: col_backsub_kernel after the tail instead of gcol_worker
   std::atomic<int> gcomb_wg{64};       // gcol_worker workgroups (at most; 64 measured best at 128 / 256 KFs)
   std::atomic<int> gcomb_min_nc{32};   // smallest dense tail (block columns) that takes the workers
-  std::atomic<int> tail_conc{0};       // 1: the tail launch beside df_factor_kernel on a second stream (slower)
 #endif
   Knobs() {
     auto env = [](const char *name, std::atomic<int> &v) {
@@ -5805,14 +4919,11 @@ struct Knobs {
     env("M3S_TAIL_CYC", tail_cyc);
     env("M3S_TAIL_MFMA", tail_mfma);
     env("M3S_BORDER_SPLIT", border_split);
-    env("M3S_SUBTREE", subtree);
     env("M3S_TAIL_PAIR", tail_pair);
     env("M3S_TAIL_WARM", tail_warm);
-    env("M3S_TAIL_ZINV", tail_zinv);
     env("M3S_GCOMB", gcomb);
     env("M3S_GCOMB_WG", gcomb_wg);
     env("M3S_GCOMB_MIN_NC", gcomb_min_nc);
-    env("M3S_TAIL_CONC", tail_conc);
 #endif
   }
 };
@@ -5829,14 +4940,11 @@ inline bool border_split() { return knobs().border_split != 0; }
 inline bool force_dense_knob() { return knobs().dense == 1; }
 inline int drop_item_knob() { return knobs().debug_drop_item; }
 bool gather_lds_path() { return knobs().gather_lds != 0; }
-inline bool subtree_path() { return knobs().subtree != 0; }
 inline bool tail_pair_path() { return knobs().tail_pair != 0; }
 inline bool tail_warm_knob() { return knobs().tail_warm != 0; }
-inline bool tail_zinv_knob() { return knobs().tail_zinv != 0; }
 inline bool gcomb_knob() { return knobs().gcomb != 0; }
 inline int gcomb_wg_knob() { return std::max(1, knobs().gcomb_wg.load()); }
 inline int gcomb_min_nc_knob() { return knobs().gcomb_min_nc.load(); }
-inline bool tail_conc_knob() { return knobs().tail_conc != 0; }
 #else
 constexpr bool cols_path() { return true; }
 constexpr bool df_path() { return true; }
@@ -5846,17 +4954,14 @@ constexpr bool border_split() { return true; }
 constexpr bool force_dense_knob() { return false; }
 constexpr int drop_item_knob() { return -1; }
 bool gather_lds_path() { return true; }
-constexpr bool subtree_path() { return false; }
 constexpr bool tail_pair_path() { return true; }
 constexpr bool tail_warm_knob() { return true; }
-constexpr bool tail_zinv_knob() { return false; }  // (measured slower, tail_zinv_col)
 constexpr bool gcomb_knob() { return true; }
 constexpr int gcomb_wg_knob() { return 64; }
 // the workers pay off once the dense tail's chain is long enough to hide the
 // X_k recursion: 256 KFs (42-column tail) 0.751 -> 0.712 ms per 3-iteration
 // call, 128 KFs (a shorter tail) 0.493 -> 0.501 (profiles/r05/solve_ab_gcomb_rotated.txt)
 constexpr int gcomb_min_nc_knob() { return 32; }
-constexpr bool tail_conc_knob() { return false; }
 #endif
 inline int dense_tail_min() { return knobs().dense_tail_min; }
 
@@ -5870,9 +4975,6 @@ struct PlanMeta {
   int nnz = 0;  // off-diagonal blocks (col_ptr[m])
   int off_dfitems = 0, n_dfitems = 0;  // df_factor_kernel dispatch list (appended to the plan image)
   int n_dfsparse = 0;                  // its sparse-column items (the border items follow)
-  int off_dfb = 0, n_dfb = 0;          // subtree path: border-row OFF tasks + tail border tasks
-  int off_sub = 0, n_sub = 0;          // subtree image (appended), subtrees (subtree_factor_kernel)
-  int64_t sub_lds = 0, sub_bs_lds = 0;  // dynamic LDS bytes: subtree factor, back-substitution
   PlanImage img;  // offsets (data vector cleared after upload)
   // linearize state of this solve call: edge ranks, the task table of the
   // edge range last linearized (host copy stays alive for the async upload)
@@ -5906,9 +5008,7 @@ PlanMeta solve_view(const PlanMeta &M) {
   v.m = M.m, v.S = M.S, v.levels = M.levels, v.plan_len = M.plan_len, v.n_items = M.n_items;
   v.n_tasks = M.n_tasks, v.n_parts = M.n_parts, v.nc = M.nc, v.off_dfitems = M.off_dfitems;
   v.n_dfitems = M.n_dfitems;
-  v.n_dfsparse = M.n_dfsparse, v.off_sub = M.off_sub, v.n_sub = M.n_sub, v.sub_lds = M.sub_lds;
-  v.sub_bs_lds = M.sub_bs_lds;
-  v.off_dfb = M.off_dfb, v.n_dfb = M.n_dfb;
+  v.n_dfsparse = M.n_dfsparse;
   v.nnz = M.nnz;
   v.img = M.img;  // offsets (its data vector is empty in the registry)
   v.plan_pending = M.plan_pending;
@@ -6021,7 +5121,6 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.stop = at<int32_t>(ws, Ly.flags) + kFlagStop;
   L.partials = at<float>(ws, Ly.partials);
   L.planes = at<float>(ws, Ly.planes);
-  L.vmask = M3S_PK_SPARSE ? at<uint8_t>(ws, Ly.vmask) : nullptr;
   L.eorder = nullptr;
   L.cnt_base = 0;
   // fused finalize only over the whole edge set (single-GPU solve)
@@ -6054,7 +5153,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
       M.range_b = eb, M.range_e = ee, M.planes_ok = false, M.order_ok = false;
       if ((int64_t)M.rj.size() >= ee) {
         std::vector<int32_t> order;
-        build_eorder(M3S_EORDER ? M.h_ri : M.rj, eb, E_loc, order);
+        build_eorder(M.rj, eb, E_loc, order);
         // uploaded from pinned staging guarded by an event, so the registry
         // entry owns no host memory a queued copy still reads (m3s_gn_release
         // need not synchronise)
@@ -6099,34 +5198,11 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
 }
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;
-constexpr int64_t kSubLdsCap = 140 * 1024;  // subtree_factor_kernel's dynamic LDS (+ 8.2 KB static)
 int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st);
 void set_lds_attributes_once();
 
 // edge_sums: per-edge local sums (stepwise API), or NULL with `partials` of
 // `chunks` chunks per edge (single-GPU call: no separate reduce launch).
-// Round 5: the second stream of the concurrent tail launch (per thread and
-// device, created on first use, never destroyed: a stream per thread that
-// calls the backend)
-struct ConcStreams {
-  hipStream_t s2 = nullptr;
-  hipEvent_t a = nullptr, b = nullptr;
-  int dev = -1;
-};
-inline ConcStreams *conc_streams() {
-  thread_local ConcStreams R;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  if (R.s2 && R.dev == dev) return &R;
-  ConcStreams N;
-  if (hipStreamCreateWithFlags(&N.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  if (hipEventCreateWithFlags(&N.a, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&N.b, hipEventDisableTiming) != hipSuccess)
-    return nullptr;
-  N.dev = dev;
-  R = N;
-  return &R;
-}
 
 int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *partials, int64_t chunks,
                   hipStream_t st, bool fin_ready = false) {
@@ -6227,9 +5303,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
       double *tail = at<double>(ws, Ly.tail);
       const int tld = 16 * kTailMaxT;
       bool gcomb_used = false;  // the tail launch also ran the sparse back-substitution
-      // the factor launches (df_factor_kernel; btf: the border tasks also
-      // publish per-task flags for a tail launch running beside it)
-      auto factor = [&](int32_t *btf) {
+      // the factor launch (df_factor_kernel)
       if (df_path()) {
         // every block of the sparse columns and the tail border: one wave-level dataflow
         DfArgs F;
@@ -6251,27 +5325,6 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         F.tail_A = tail;
         F.tail_ld = tld;
         F.Wgr = at<double>(ws, Ly.wgran);
-        F.btflag = btf;
-#ifdef M3S_TEST_PATHS
-        if (subtree_path() && meta.n_sub > 0) {
-          // the sparse columns: one LDS workgroup per subtree; df_factor_kernel
-          // then runs only the dense tail's border tasks (if any)
-          SubArgs SA;
-          SA.sub = D.plan + meta.off_sub;
-          SA.L = D.L;
-          SA.Dinv = D.Dinv;
-          SA.y = C.y;
-          SA.sdone = F.sdone;
-          SA.want = meta.epoch + 1;
-          SA.flags = flags;
-          SA.Wgr = F.Wgr;
-          SA.m = meta.m;
-          set_lds_attributes_once();
-          subtree_factor_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_lds, st>>>(SA);
-          F.items = D.plan + meta.off_dfb;
-          F.n_items = meta.n_dfb;
-        }
-#endif
         const int nw = std::max(1, std::min(F.n_items, 1024));
         if (F.n_items > 0) df_factor_kernel<<<(nw + kDfWaves - 1) / kDfWaves, 64 * kDfWaves, 0, st>>>(F);
       } else {
@@ -6280,10 +5333,7 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         col_factor_kernel<<<g1, 256, 0, st>>>(C);
 #endif
       }
-      };
-      // the dense tail's launch on stream ts (btf: wait for the border tasks'
-      // flags, df_factor_kernel running beside it)
-      auto tailf = [&](hipStream_t ts, const int32_t *btf) {
+      // the dense tail's launch
       if (meta.nc > 0) {
         D.tail_A = tail;
         D.tail_ld = tld;
@@ -6308,9 +5358,6 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           Y.LgT = Y.ypg + 16 * kTailMaxT;
           Y.LgG = tail + tail_gran_offset_doubles();
           Y.warm = tail_warm_knob() ? 1 : 0;
-          Y.zinv = tail_zinv_knob() ? 1 : 0;
-          Y.Zg = tail + tail_z_offset_doubles();
-          Y.btflag = btf;
           const int TC = (7 * meta.nc + 15) / 16;
           // the sparse back-substitution on extra workgroups of the tail's
           // launch (gcol_worker) when there are sparse columns
@@ -6320,10 +5367,8 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           G.nx = ((1 + 7 * meta.nc) + 7) / 8 * 8;
           G.task = C.ctr + 8, G.comb = C.ctr + 9, G.fin = C.ctr + 10, G.xt_ready = C.ctr + 11;
           G.cnt = Y.tflag + 2 * kTailMaxT;
-          G.sdone = btf ? cs + 2 * (meta.m + 1) + 16 : nullptr;
           int nG = 0;
-          if (gcomb_knob() && meta.nc >= gcomb_min_nc_knob() && tail_pair_path() && !Y.zinv && C.ncols > 0 &&
-              !(subtree_path() && meta.n_sub > 0)) {
+          if (gcomb_knob() && meta.nc >= gcomb_min_nc_knob() && tail_pair_path() && C.ncols > 0) {
             G.X = at<double>(ws, Ly.gx);
             nG = std::max(1, std::min(C.ncols, std::min(gcomb_wg_knob(), 240 - G.n_pairs)));
             gcomb_used = true;
@@ -6331,52 +5376,15 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
           const unsigned gt = (unsigned)(G.n_pairs + nG);
           if (tail_pair_path())
             if (((7 * meta.nc + 16) / 16 + 2) / 3 <= 7)  // tile rows TR: rows per wave of waves 1..3
-              tail_pair_kernel<7><<<gt, 64 * kTailNW, 0, ts>>>(T, Y, C, G);
+              tail_pair_kernel<7><<<gt, 64 * kTailNW, 0, st>>>(T, Y, C, G);
             else
-              tail_pair_kernel<(kTailMaxT + 2) / 3><<<gt, 64 * kTailNW, 0, ts>>>(T, Y, C, G);
+              tail_pair_kernel<(kTailMaxT + 2) / 3><<<gt, 64 * kTailNW, 0, st>>>(T, Y, C, G);
           else
-            tail_cyc_kernel<<<TC, 64 * kTailNW, 0, ts>>>(T, Y);
+            tail_cyc_kernel<<<TC, 64 * kTailNW, 0, st>>>(T, Y);
         } else {
-          tail_llt_kernel<<<1, 64 * kTailNW, 0, ts>>>(T);
+          tail_llt_kernel<<<1, 64 * kTailNW, 0, st>>>(T);
         }
       }
-      };
-      // Round 5: the tail launch beside df_factor_kernel on a second stream
-      // (knob tail_conc, test build): each tile-column pair starts once ITS
-      // border blocks are published instead of after the whole factor launch;
-      // the workers wait per column for df's slot flags. The tail launch goes
-      // first so its workgroups are resident before df's fill the chip.
-      // Correct (the GPU suite with it on) and slower: 256 KFs 0.717 -> 0.765
-      // ms, 128 KFs 0.500 -> 0.543 ms per 3-iteration call
-      // (profiles/r05/solve_ab_tail_conc_REJECTED.txt): the tail's 74
-      // one-per-CU workgroups and their polls beside df's dataflow, the
-      // write-through border stores and the cross-stream event pair cost more
-      // than the ~15 us of overlap.
-      const bool conc = tail_conc_knob() && df_path() && meta.nc > 0 && tail_cyc() && tail_pair_path() &&
-                        !tail_zinv_knob() && !(subtree_path() && meta.n_sub > 0);
-      ConcStreams *cr = conc ? conc_streams() : nullptr;
-      if (cr) {
-        int32_t *btf = cs + kColsyncBtOff(meta.m, Ly.slot_cap);
-        if (hipEventRecord(cr->a, st) != hipSuccess || hipStreamWaitEvent(cr->s2, cr->a, 0) != hipSuccess)
-          return M3S_ELAUNCH;
-        tailf(cr->s2, btf);
-        factor(btf);
-        if (hipEventRecord(cr->b, cr->s2) != hipSuccess || hipStreamWaitEvent(st, cr->b, 0) != hipSuccess)
-          return M3S_ELAUNCH;
-      } else {
-        factor(nullptr);
-        tailf(st, nullptr);
-      }
-#ifdef M3S_TEST_PATHS
-      if (subtree_path() && meta.n_sub > 0) {
-        SubBsArgs B;
-        B.sub = D.plan + meta.off_sub;
-        B.ns = meta.n_sub;
-        B.fin_ctr = C.ctr + 5;
-        B.C = C;
-        subtree_backsub_kernel<<<meta.n_sub, 64 * kSubWaves, (size_t)meta.sub_bs_lds, st>>>(B);
-      } else
-#endif
       if (!gcomb_used) {
         const int g4 = std::max(1, std::min(C.ncols, 256));
         col_backsub_kernel<<<g4, 64, 0, st>>>(C);
@@ -6501,12 +5509,6 @@ void set_lds_attributes_once() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gn_prologue_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-#ifdef M3S_TEST_PATHS
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(subtree_factor_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSubLdsCap);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(subtree_backsub_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSubLdsCap);
-#endif
   });
 }
 
@@ -6526,8 +5528,6 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
     const bool chip_path = global_factor && cols_path() && P.m <= 512 && (P.nc == 0 || 7 * P.nc + 1 <= 16 * kTailMaxT);
     if (global_factor && !chip_path)  // split long update lists for the staged global-factor products
       build_sparse_plan((int)a->N, ri, rj, P, kSplitUpdates, Ly.slot_cap - 1, dense_tail_min(), true);
-    else if (!chip_path && kLdsSplit > 0)  // (A/B: PART items on the LDS-resident path too)
-      build_sparse_plan((int)a->N, ri, rj, P, kLdsSplit, Ly.slot_cap - 1, dense_tail_min(), true);
     else if (!chip_path)
       schedule_plan_items(P);
     PlanImage img;
@@ -6542,28 +5542,6 @@ PlanMeta build_plan_meta(const m3s_gn_args *a, const Layout &Ly, const std::vect
     meta.n_dfsparse = (int)img.data.size() - meta.off_dfitems;
     for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
     meta.n_dfitems = (int)img.data.size() - meta.off_dfitems;
-#ifdef M3S_TEST_PATHS
-    if (chip_path) {
-      // the subtree path's df_factor_kernel list: the OFF tasks of the sparse
-      // columns' border rows (rows in the dense tail) in level order, then the
-      // dense-tail border tasks; the subtrees' internal blocks are
-      // subtree_factor_kernel's (one LDS workgroup per subtree)
-      const int c0 = P.m - P.nc;
-      meta.off_dfb = (int)img.data.size();
-      for (int32_t k : P.corder)
-        for (int q = 0; q < P.col_ptr[k + 1] - P.col_ptr[k]; q++)
-          if (P.col_row[P.col_ptr[k] + q] >= c0) img.data.push_back(P.ctask0[k] + q);
-      for (int b = 0; b < P.nc * (P.nc + 1) / 2; b++) img.data.push_back((int32_t)P.task_dst.size() + b);
-      meta.n_dfb = (int)img.data.size() - meta.off_dfb;
-      SubtreeImage SI;
-      build_subtree_image(P, kSubLdsCap, SI);
-      meta.off_sub = (int)img.data.size();
-      meta.n_sub = SI.ns;
-      meta.sub_lds = SI.lds_bytes;
-      meta.sub_bs_lds = SI.bs_lds_bytes;
-      img.data.insert(img.data.end(), SI.data.begin(), SI.data.end());
-    }
-#endif
     const bool fits = (int64_t)img.data.size() <= Ly.plan_cap && P.S <= Ly.slot_cap;
     if (fits && !force_dense) {
       meta.sparse = true;
@@ -6655,16 +5633,6 @@ bool upload_plan(Staging *SG, PlanMeta &M, char *dst, hipStream_t st) {
 void apply_drop_item(PlanMeta &M) {
   const int d = drop_item_knob();
   if (d < 0 || !M.sparse || M.h_plan.empty()) return;
-  if (M.store == 0 && M.n_sub > 0 && subtree_path()) {  // list A of the first subtree
-    int32_t *sub = M.h_plan.data() + M.off_sub;
-    int32_t *rec = sub + sub[1];
-    int32_t *ia = sub + rec[7];
-    if (d < rec[3]) {
-      for (int t = d; t + 1 < rec[3]; t++) ia[t] = ia[t + 1];
-      rec[3] -= 1;
-    }
-    return;
-  }
   if (M.store == 0 && M.n_dfitems > 0) {
     int32_t *di = M.h_plan.data() + M.off_dfitems;
     if (d < M.n_dfitems) {
@@ -6723,14 +5691,14 @@ int gn_prepare_impl(const m3s_gn_args *a, hipStream_t st) {
       }
     }
   }
-  if (hit && E > 0 && meta.eorder.empty()) build_eorder(M3S_EORDER ? meta.h_ri : meta.rj, 0, E, meta.eorder);  // cached by the prologue path
+  if (hit && E > 0 && meta.eorder.empty()) build_eorder(meta.rj, 0, E, meta.eorder);  // cached by the prologue path
   if (!hit) {
     // ranks and the full-range task table now (the first linearize needs
     // them); the symbolic plan is built by the first solve of this call,
     // while the first linearize kernel runs (finish_plan)
     meta.h_ri = ri;
     meta.rj = rj;
-    if (E > 0) build_eorder(M3S_EORDER ? meta.h_ri : meta.rj, 0, E, meta.eorder);
+    if (E > 0) build_eorder(meta.rj, 0, E, meta.eorder);
     meta.sparse = !bad && !force_dense && a->N > 1;  // the expected outcome (the dense path reads partials either way)
     meta.plan_pending = !bad && a->N > 1;
     meta.force_dense = force_dense;
@@ -6810,9 +5778,7 @@ int finish_plan(const m3s_gn_args *a, const Layout &Ly, hipStream_t st) {
   M.m = built.m, M.S = built.S, M.levels = built.levels, M.plan_len = built.plan_len;
   M.n_items = built.n_items, M.n_tasks = built.n_tasks, M.n_parts = built.n_parts, M.nc = built.nc;
   M.off_dfitems = built.off_dfitems, M.n_dfitems = built.n_dfitems, M.nnz = built.nnz;
-  M.n_dfsparse = built.n_dfsparse, M.off_sub = built.off_sub, M.n_sub = built.n_sub, M.sub_lds = built.sub_lds;
-  M.off_dfb = built.off_dfb, M.n_dfb = built.n_dfb;
-  M.sub_bs_lds = built.sub_bs_lds;
+  M.n_dfsparse = built.n_dfsparse;
   M.img = built.img;
   M.h_plan = std::move(built.h_plan);
   M.plan_pending = false;
@@ -6906,9 +5872,7 @@ int host_finish(const m3s_gn_args *a, hipStream_t st) {
   M.m = hitm.m, M.S = hitm.S, M.levels = hitm.levels, M.plan_len = hitm.plan_len;
   M.n_items = hitm.n_items, M.n_tasks = hitm.n_tasks, M.n_parts = hitm.n_parts, M.nc = hitm.nc;
   M.off_dfitems = hitm.off_dfitems, M.n_dfitems = hitm.n_dfitems, M.nnz = hitm.nnz;
-  M.n_dfsparse = hitm.n_dfsparse, M.off_sub = hitm.off_sub, M.n_sub = hitm.n_sub, M.sub_lds = hitm.sub_lds;
-  M.off_dfb = hitm.off_dfb, M.n_dfb = hitm.n_dfb;
-  M.sub_bs_lds = hitm.sub_bs_lds;
+  M.n_dfsparse = hitm.n_dfsparse;
   M.img = hitm.img;
   M.h_plan = std::move(hitm.h_plan);
   M.plan_pending = false;
@@ -7090,16 +6054,9 @@ constexpr int kTrackContinue = 0, kTrackConverged = 1, kTrackFailed = 2;
 // A/B: the tracker's 7x7 Cholesky solve in fp32 (the reference's precision,
 // tracker.py:168) instead of fp64: +1% GN it/s at C2
 // (profiles/r05/trk_ab_f32_solve_REJECTED.txt), not worth the precision
-#ifndef M3S_TRK_F32
-#define M3S_TRK_F32 0
-#endif
 __device__ __forceinline__ int track_update(const double *s, Sim3f &T, double &old_cost, float rel_error,
                                             float delta_norm) {
-#if M3S_TRK_F32
-  typedef float real;
-#else
   typedef double real;
-#endif
   real H[7][7], L[7][7], g[7], y[7], x[7];
   for (int a = 0; a < 7; a++)
     for (int c = 0; c < 7; c++) H[a][c] = (real)s[kL + tri(a < c ? a : c, a < c ? c : a)];
@@ -7116,14 +6073,7 @@ __device__ __forceinline__ int track_update(const double *s, Sim3f &T, double &o
 #pragma unroll
     for (int p = 0; p < k; p++) d -= L[k][p] * L[k][p];
     if (!(d > (real)0)) return kTrackFailed;
-#if M3S_TRK_F32
-    {
-      float r = __builtin_amdgcn_rsqf(d);
-      dinv[k] = r * (1.5f - 0.5f * d * r * r);
-    }
-#else
     dinv[k] = rsqrt_nr(d);
-#endif
     L[k][k] = d * dinv[k];
 #pragma unroll
     for (int i = k + 1; i < 7; i++) {
@@ -7253,38 +6203,11 @@ constexpr int kTrkMaxBlocks = 256;
 constexpr int kTrkShards = 8;
 constexpr int kTrkGran = kNP / 3;  // 16-B granules per workgroup partial (3 sums + tag)
 constexpr int kTrkSpins = 1 << 22;
-// M3S_TRK_TOPALL (round 5, default): no record hand-off. Every workgroup
-// polls the 8 shard sums itself, sums them in shard order and runs the same
-// 7x7 update (the same fp64 sums in the same order: every workgroup gets the
-// bitwise same pose, the one workgroup 0 published before). The shard sums
-// are double-buffered by iteration parity: shard s writes iteration it + 1
-// into the buffer of it - 1 only after its members' it + 1 partials, and
-// every workgroup of every shard has read iteration it - 1's sums by then
-// (its iteration-it partial, which the other shard reducers waited for,
-// follows its read of them). Measured no faster than the record protocol
-// (profiles/r05/trk_ab_topall.txt: 120-122k GN it/s at C2 for both, the 8 x
-// 36-granule load on every workgroup costs what the record hop saved), so
-// the default stays the round-4 record protocol (0).
-#ifndef M3S_TRK_TOPALL
-#define M3S_TRK_TOPALL 0
-#endif
-// M3S_TRK_FLAT (round 5): no shard level. Workgroup 0 polls every
-// workgroup's partial granules on all its waves (wave w: members 64 w ..
-// 64 w + 63, one per lane), reduces them per wave and then across the waves
-// (fixed order), updates and publishes the record: two fabric hops per
-// iteration instead of three. Measured slower (profiles/r05/
-// trk_ab_flat_REJECTED.txt: 133k -> 117k GN it/s at C2): one CU polling and
-// converting 256 x 12 granules costs more than the shard hop it removes.
-// M3S_TRK_PP (round 5): the per-iteration accumulation on pixel pairs
-// (AccumPP / pixel_contrib2, as the backend's packed kernel) instead of the
-// per-pixel row-pair Accum
-#ifndef M3S_TRK_PP
-#define M3S_TRK_PP 1
-#endif
-#ifndef M3S_TRK_FLAT
-#define M3S_TRK_FLAT 0
-#endif
-constexpr int kTrkShBufs = M3S_TRK_TOPALL ? 2 : 1;
+// The per-iteration accumulation runs on pixel pairs (AccumPP /
+// pixel_contrib2, as the backend's packed kernel; round 5). Measured and
+// removed (DESIGN.md §4 Tracker): every workgroup running the top level
+// itself, and no shard level.
+constexpr int kTrkShBufs = 1;
 struct TrackSync {
   uint32_t rec[32];  // the published record: 4 tagged 16-B granules (pose 0-7, status 8, cost 9-10 | tag)
   uint32_t shard_sum[kTrkShBufs][kTrkShards][kNP][4];  // level-1 sums (fp64), tagged 16-B granules {lo, hi, tag, 0}
@@ -7317,7 +6240,6 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
   const int G = (int)gridDim.x, b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
   constexpr int NW = TH / 64;
   __shared__ float redf[NW][kNP];
-  __shared__ double redd[NW][kNP];
   __shared__ double s_sum[kNP];
   // the iteration's record: pose (0-7), status (8: kTrackContinue /
   // kTrackConverged / kTrackFailed / 3 = barrier timeout), cost (9-10)
@@ -7353,7 +6275,6 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
     float v[kNP];
 #pragma unroll
     for (int k = 0; k < kNP; k++) v[k] = 0.0f;
-#if M3S_TRK_PP
     {  // pixel pairs in the halves of float2 registers (the backend's packed
        // accumulation, with the cost sum); a lane's pixel past the image takes
        // a zero weight
@@ -7377,19 +6298,6 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
       }
       acc.fold(v);
     }
-#else
-    Accum<MODE> acc;
-    acc.zero();
-#pragma unroll
-    for (int s = 0; s < PPL; s++) {
-      if (live[s]) {
-        float Y[3];
-        act(Tm, Xf[s], Y);
-        pixel_contrib<MODE>(acc, A.P, in[s], Y);
-      }
-    }
-    acc.fold(v);
-#endif
     M3S_TSTAMP(1)
     {
       int idx;
@@ -7415,8 +6323,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         __builtin_amdgcn_raw_buffer_store_b128(w, Rpart, lane < kTrkGran ? (b * kTrkGran + lane) * 16 : kPartFar, 0, 16);
       }
       M3S_TSTAMP(2)
-#if !M3S_TRK_FLAT
-      const int shb = M3S_TRK_TOPALL ? (it & 1) : 0;  // the shard-sum buffer of this iteration
+      const int shb = 0;  // the shard-sum buffer
       // level 1: workgroup s < 8 reduces shard s = {s, s + 8, ...}: lane j
       // polls member s + 8 j's granules, then the 36 sums are reduced across
       // the lanes in a fixed order (fp64)
@@ -7459,59 +6366,6 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
         // granules land
         top_last = sh == 0;
       }
-#if M3S_TRK_TOPALL
-      (void)top_last;
-      {
-        M3S_TSTAMP(3)
-        // level 2 on every workgroup: lanes j < n_top poll the last granule of
-        // shard j (cheap passes while the shards are still summing), then all
-        // 36 x n_top granules are loaded together and their tags checked
-        u32x4 g[kTrkShards];
-        int spins = 0;
-        for (;;) {
-          const u32x4 t35 = poll_b128(Rsh, lane < (int)n_top ? ((shb * kTrkShards + lane) * kNP + kNP - 1) * 16 : kShFar);
-          if (__ballot(lane < (int)n_top && t35.z != (unsigned)(it + 1)) == 0) break;
-          trk_pause();
-          if (++spins > kTrkSpins) break;
-        }
-        for (;;) {
-#pragma unroll
-          for (int j = 0; j < kTrkShards; j++)
-            g[j] = poll_b128(Rsh, (lane < kNP && j < (int)n_top) ? ((shb * kTrkShards + j) * kNP + lane) * 16 : kShFar);
-          bool ok = true;
-#pragma unroll
-          for (int j = 0; j < kTrkShards; j++) ok &= lane >= kNP || j >= (int)n_top || g[j].z == (unsigned)(it + 1);
-          if (__ballot(!ok) == 0) break;
-          trk_pause();
-          if (++spins > kTrkSpins) break;
-        }
-        if (lane < kNP) {
-          double x = 0.0;
-#pragma unroll
-          for (int j = 0; j < kTrkShards; j++)
-            x += j < (int)n_top ? __longlong_as_double((long long)(((unsigned long long)g[j].y << 32) | g[j].x)) : 0.0;
-          s_sum[lane] = x;
-        }
-        const bool timed_out = spins > kTrkSpins;  // bounded wait: status 3
-        wave_lds_fence();
-        M3S_TSTAMP(4)
-        if (lane == 0) {
-          double oc = it == 0 ? __builtin_inf()
-                              : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
-          Sim3f Tn = T;
-          const int r = timed_out ? 3 : track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
-          M3S_TSTAMP(6)
-          if (r != kTrackContinue && r != kTrackConverged) Tn = T;
-          float rec[8];
-          store_sim3(rec, Tn);
-#pragma unroll
-          for (int k = 0; k < 8; k++) pub_s[k] = __float_as_uint(rec[k]);
-          const unsigned long long ob = (unsigned long long)__double_as_longlong(oc);
-          pub_s[8] = (uint32_t)r, pub_s[9] = (uint32_t)(ob & 0xffffffffull), pub_s[10] = (uint32_t)(ob >> 32);
-          pub_s[11] = 0;
-        }
-      }
-#else
       if (top_last) {
         M3S_TSTAMP(3)
         u32x4 g[kTrkShards];
@@ -7573,88 +6427,7 @@ __global__ void __launch_bounds__(TH) track_persistent_kernel(LinArgs A, int max
           pub_s[3 * lane] = g.x, pub_s[3 * lane + 1] = g.y, pub_s[3 * lane + 2] = g.z;
         }
       }
-#endif
-#endif  // !M3S_TRK_FLAT
     }
-#if M3S_TRK_FLAT
-    if (b == 0) {
-      // one level: wave w polls the partial granules of members 64 w + lane,
-      // reduces its 64 members in fp64 (lane order), and wave 0 sums the
-      // waves in order, updates and publishes the record
-      u32x4 g[kTrkGran];
-      int spins = 0;
-      for (;;) {
-#pragma unroll
-        for (int k = 0; k < kTrkGran; k++) g[k] = poll_b128(Rpart, t < G ? (t * kTrkGran + k) * 16 : kPartFar);
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < kTrkGran; k++) ok &= t >= G || g[k].w == (unsigned)(it + 1);
-        if (__ballot(!ok) == 0) break;
-        trk_pause();
-        if (++spins > kTrkSpins) break;
-      }
-      double a[kNP];
-#pragma unroll
-      for (int k = 0; k < kTrkGran; k++) {
-        a[3 * k] = (double)__uint_as_float(g[k].x);
-        a[3 * k + 1] = (double)__uint_as_float(g[k].y);
-        a[3 * k + 2] = (double)__uint_as_float(g[k].z);
-      }
-      if (spins > kTrkSpins) a[0] = __builtin_nan("");  // the update then fails (status 2)
-      {
-        int idx;
-        bool ok;
-        const double x = xreduce36_trk(a, lane, idx, ok);
-        if (ok) redd[wv][idx] = x;
-      }
-      __syncthreads();
-      if (wv == 0) {
-        M3S_TSTAMP(3)
-        if (lane < kNP) {
-          double x = 0.0;
-#pragma unroll
-          for (int w = 0; w < NW; w++) x += redd[w][lane];
-          s_sum[lane] = x;
-        }
-        wave_lds_fence();
-        M3S_TSTAMP(4)
-        if (lane == 0) {
-          double oc = it == 0 ? __builtin_inf()
-                              : __longlong_as_double((long long)(((unsigned long long)pub_s[10] << 32) | pub_s[9]));
-          Sim3f Tn = T;
-          const int r = track_update(s_sum, Tn, oc, A.rel_error, A.delta_norm);
-          M3S_TSTAMP(6)
-          if (r != kTrackContinue && r != kTrackConverged) Tn = T;
-          float rec[8];
-          store_sim3(rec, Tn);
-#pragma unroll
-          for (int k = 0; k < 8; k++) pub_s[k] = __float_as_uint(rec[k]);
-          const unsigned long long ob = (unsigned long long)__double_as_longlong(oc);
-          pub_s[8] = (uint32_t)r, pub_s[9] = (uint32_t)(ob & 0xffffffffull), pub_s[10] = (uint32_t)(ob >> 32);
-          pub_s[11] = 0;
-        }
-        wave_lds_fence();
-        const int q = lane < 4 ? 3 * lane : 0;
-        const u32x4 w = {pub_s[q], pub_s[q + 1], pub_s[q + 2], (unsigned)(it + 1)};
-        __builtin_amdgcn_raw_buffer_store_b128(w, Rrec, lane * 16, 0, 16);
-      }
-    } else if (wv == 0) {
-      int spins = 0;
-      u32x4 g;
-      for (;;) {
-        g = poll_b128(Rrec, lane * 16);
-        if (__ballot(lane < 4 && g.w != (unsigned)(it + 1)) == 0) break;
-        trk_pause();
-        if (++spins > kTrkSpins) break;
-      }
-      M3S_TSTAMP(4)
-      if (spins > kTrkSpins) {
-        if (lane == 0) pub_s[8] = 3;
-      } else if (lane < 4) {
-        pub_s[3 * lane] = g.x, pub_s[3 * lane + 1] = g.y, pub_s[3 * lane + 2] = g.z;
-      }
-    }
-#endif
     M3S_TSTAMP(5)
     __syncthreads();
     status = (int)pub_s[8];
@@ -7901,19 +6674,6 @@ int64_t m3s_sparse_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int
   return n;
 }
 
-int64_t m3s_subtree_plan_debug(int32_t N, int64_t E, const int32_t *ri, const int32_t *rj, int32_t *out, int64_t cap,
-                               int64_t *meta) {
-  std::vector<int32_t> a(ri, ri + E), b(rj, rj + E);
-  SparsePlan P;
-  build_sparse_plan(N, a, b, P, 0, 0, dense_tail_min(), false);  // as the chip-wide path builds it
-  SubtreeImage SI;
-  build_subtree_image(P, kSubLdsCap, SI);
-  if (meta) meta[0] = SI.ns, meta[1] = SI.lds_bytes, meta[2] = SI.bs_lds_bytes, meta[3] = P.nc;
-  const int64_t n = (int64_t)SI.data.size();
-  if (out && cap >= n) std::copy(SI.data.begin(), SI.data.end(), out);
-  return n;
-}
-
 // Instrumented builds only (tools/trk_stamps.py, tools/col_stamps.py):
 // which = 0: persistent tracker phase stamps [2][16][8] (-DM3S_TRK_STAMPS);
 // which = 1: column-task stamps [4][2048][4] (-DM3S_COL_STAMPS: factor
@@ -7957,8 +6717,8 @@ int m3s_set_knob(const char *name, int value) {
 #ifdef M3S_TEST_PATHS
              {"dense", &k.dense}, {"cols", &k.cols}, {"df", &k.df}, {"tail_cyc", &k.tail_cyc},
              {"tail_mfma", &k.tail_mfma}, {"border_split", &k.border_split}, {"debug_drop_item", &k.debug_drop_item},
-             {"gather_lds", &k.gather_lds}, {"subtree", &k.subtree},
-             {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm}, {"tail_zinv", &k.tail_zinv}, {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}, {"gcomb_min_nc", &k.gcomb_min_nc}, {"tail_conc", &k.tail_conc}
+             {"gather_lds", &k.gather_lds}, {"tail_pair", &k.tail_pair}, {"tail_warm", &k.tail_warm},
+             {"gcomb", &k.gcomb}, {"gcomb_wg", &k.gcomb_wg}, {"gcomb_min_nc", &k.gcomb_min_nc}
 #endif
   };
   for (const auto &t : tab)

@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
 #define M3S_REF_ROWS 1
 #endif
 typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
-constexpr int kRefFar = 0x7ffffff0;  // past any descriptor image (< 2^31 B): loads return zeros
+constexpr int kRefFar = 0x7fff0000;  // past any descriptor image (the kernel takes images < 2^30 B): loads return zeros, and o + 16 l stays below 2^31
 
 // Two candidates' scores, each the sequential fp16 FMA chain of the
 // reference in feature order (the low halves of v_pk_fma_f16: one rounding

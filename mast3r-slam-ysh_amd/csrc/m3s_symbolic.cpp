@@ -610,137 +610,6 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
   }
 }
 
-void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImage &out, bool with_border) {
-  out = SubtreeImage();
-  const int m = P.m, c0 = m - P.nc;
-  std::vector<int> parent(m, -1), root(m, -1), level(m, 0);
-  for (int k = 0; k < m; k++)
-    if (P.col_ptr[k + 1] > P.col_ptr[k]) parent[k] = P.col_row[P.col_ptr[k]];
-  for (int k = 0; k < c0; k++)  // children before parents (parent > child)
-    if (parent[k] >= 0 && parent[k] < c0) level[parent[k]] = std::max(level[parent[k]], level[k] + 1);
-  std::vector<int> roots;
-  for (int k = c0 - 1; k >= 0; k--) {
-    root[k] = (parent[k] < 0 || parent[k] >= c0) ? k : root[parent[k]];
-    if (root[k] == k) roots.push_back(k);
-  }
-  std::vector<std::vector<int>> cols_of(m);
-  for (int k = 0; k < c0; k++) cols_of[root[k]].push_back(k);  // ascending k
-  // largest first: the longest subtree starts on the first workgroup
-  std::stable_sort(roots.begin(), roots.end(), [&](int a, int b) { return cols_of[a].size() > cols_of[b].size(); });
-  const int ns = (int)roots.size();
-  std::vector<int32_t> &D = out.data;
-  D.assign(2 + ns, 0);
-  D[0] = ns;
-  out.ns = ns;
-  std::vector<int32_t> lblk(P.S, -1), lcol(m, -1);
-  // column k's OFF task (global) of its q-th row: ctask0[k] + q
-  for (int s = 0; s < ns; s++) {
-    const std::vector<int> &cols = cols_of[roots[s]];
-    const int ncol = (int)cols.size();
-    for (int c = 0; c < ncol; c++) lcol[cols[c]] = c;
-    std::vector<int32_t> gsl, bq, bk;  // global slot, row entry q and column k of each local block
-    for (int pass = 0; pass < 2; pass++)
-      for (int k : cols)
-        for (int q = P.col_ptr[k]; q < P.col_ptr[k + 1]; q++)
-          if ((P.col_row[q] >= c0) == (pass == 1)) {
-            lblk[P.col_slot[q]] = (int32_t)gsl.size();
-            gsl.push_back(P.col_slot[q]);
-            bq.push_back(q);
-            bk.push_back(k);
-          }
-    const int nblk = (int)gsl.size();
-    int n_int = 0;
-    for (int b = 0; b < nblk; b++) n_int += P.col_row[bq[b]] < c0;
-    // LDS: W (49) + y (7) doubles per column, flags (nblk + 2 ncol + 4 ints), then blocks
-    const int64_t fixed = 8 * (int64_t)ncol * 56 + 4 * ((int64_t)nblk + 2 * ncol + 4);
-    const int64_t room = lds_cap_bytes - fixed;
-    const int n_lds = (int)std::max<int64_t>(0, std::min<int64_t>(with_border ? nblk : n_int, room / (8 * 49)));
-    out.lds_bytes = std::max(out.lds_bytes, fixed + 8 * 49 * (int64_t)n_lds);
-    // per-block column and the global OFF task it is
-    std::vector<int32_t> tcol(nblk), tptr(1, 0), tlist, dptr(1, 0), dlist, itA, itB;
-    for (int b = 0; b < nblk; b++) {
-      const int q = bq[b], k = bk[b];
-      tcol[b] = lcol[k];
-      const int t = P.ctask0[k] + (q - P.col_ptr[k]);
-      for (int e = P.task_tr_ptr[t]; e < P.task_tr_ptr[t + 1]; e++) {
-        tlist.push_back(lblk[P.tr_a[e]]);
-        tlist.push_back(lblk[P.tr_b[e]]);
-      }
-      tptr.push_back((int32_t)tlist.size() / 2);
-    }
-    for (int c = 0; c < ncol; c++) {
-      const int k = cols[c];
-      for (int e = P.dtr_ptr[k]; e < P.dtr_ptr[k + 1]; e++) {
-        dlist.push_back(lblk[P.dtr_slot[e]]);
-        dlist.push_back(lcol[P.dtr_p[e]]);
-      }
-      dptr.push_back((int32_t)dlist.size() / 2);
-    }
-    // back-substitution (subtree_backsub_kernel): per column its internal and
-    // border block ranges (rows ascending within each), the row of each block
-    // (internal: local column; border: global column), the level order
-    std::vector<int32_t> ci(ncol + 1, 0), cb(ncol + 1, 0), brow(nblk), corder;
-    for (int b = 0; b < nblk; b++) {
-      const int row = P.col_row[bq[b]];
-      brow[b] = b < n_int ? lcol[row] : row;
-      (b < n_int ? ci : cb)[tcol[b] + 1]++;
-    }
-    for (int c = 0; c < ncol; c++) ci[c + 1] += ci[c], cb[c + 1] += cb[c];
-    for (int c = 0; c <= ncol; c++) cb[c] += n_int;
-    int maxlev = 0;
-    for (int k : cols) maxlev = std::max(maxlev, level[k]);
-    for (int l = 0; l <= maxlev; l++)
-      for (int c = 0; c < ncol; c++)
-        if (level[cols[c]] == l) corder.push_back(c);
-    for (int l = 0; l <= maxlev; l++) {
-      for (int c = 0; c < ncol; c++)
-        if (level[cols[c]] == l) {
-          itA.push_back(-1 - c);
-          for (int b = 0; b < n_int; b++)
-            if (tcol[b] == c) itA.push_back(b);
-        }
-      if (with_border)
-        for (int b = n_int; b < nblk; b++)
-          if (level[cols[tcol[b]]] == l) itB.push_back(b);
-    }
-    // waves on list A: enough for its width, the rest start on the border list
-    const int nwA = itB.empty() ? 16 : std::max(8, std::min(14, 16 * (int)itA.size() / (int)(itA.size() + itB.size()) + 2));
-    const int rec = (int)D.size();
-    D[1 + s] = rec;
-    D.resize(D.size() + kSubRec, 0);
-    auto put = [&](const std::vector<int32_t> &v) {
-      const int o = (int)D.size();
-      D.insert(D.end(), v.begin(), v.end());
-      return o;
-    };
-    // back-substitution LDS: W, x (49 + 7 per column), flags, border terms (7
-    // per border block), then as many internal blocks as fit
-    const int64_t bs_fixed = 8 * (int64_t)ncol * 56 + 8 * 7 * (int64_t)(nblk - n_int) + 4 * ((int64_t)ncol + 2);
-    const int n_li = (int)std::max<int64_t>(0, std::min<int64_t>(n_int, (lds_cap_bytes - bs_fixed) / (8 * 49)));
-    out.bs_lds_bytes = std::max(out.bs_lds_bytes, bs_fixed + 8 * 49 * (int64_t)n_li);
-    int32_t h[kSubRec] = {ncol, nblk, n_lds, (int32_t)itA.size(), (int32_t)itB.size(), 0, 0, 0, 0, 0, 0, 0, 0, 0, nwA,
-                          0, 0, 0, 0, n_int, n_li};
-    std::vector<int32_t> gcols(cols.begin(), cols.end());
-    h[5] = put(gcols);
-    h[6] = put(gsl);
-    h[7] = put(itA);
-    h[8] = put(itB);
-    h[9] = put(dptr);
-    h[10] = put(dlist);
-    h[11] = put(tcol);
-    h[12] = put(tptr);
-    h[13] = put(tlist);
-    h[15] = put(ci);
-    h[16] = put(cb);
-    h[17] = put(brow);
-    h[18] = put(corder);
-    for (int q = 0; q < kSubRec; q++) D[rec + q] = h[q];
-    for (int32_t sl : gsl) lblk[sl] = -1;
-    for (int k : cols) lcol[k] = -1;
-  }
-  D[1 + ns] = (int32_t)out.lds_bytes;
-}
-
 void flatten_plan(const SparsePlan &P, PlanImage &img) {
   img.data.clear();
   auto put = [&](const std::vector<int32_t> &v) {

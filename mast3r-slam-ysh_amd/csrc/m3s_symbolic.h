@@ -79,39 +79,6 @@ void build_sparse_plan(int N, const std::vector<int32_t> &ri, const std::vector<
                        bool schedule = true);
 void schedule_plan_items(SparsePlan &P);
 
-// Subtrees below the dense tail (chip-wide path, round 4). Every row of
-// struct(k) is an etree ancestor of k, so the columns below the dense tail
-// split into subtrees whose DIAG / OFF update lists stay inside the subtree:
-// each is factored by one workgroup with its blocks in LDS
-// (subtree_factor_kernel). Image (int32, offsets relative to its start):
-//   [0] ns, [1 .. ns] record offsets, [ns + 1] max dynamic LDS bytes
-//   record: ncol, nblk, n_lds, nA, nB, o_cols, o_gsl, o_itemsA, o_itemsB,
-//           o_dptr, o_dlist, o_tcol, o_tptr, o_tlist, nwA,
-//           o_ci, o_cb, o_brow, o_corder, n_int, n_li (back-substitution: per
-//           column its internal blocks [ci[c], ci[c+1]) and border blocks
-//           [cb[c], cb[c+1]), rows ascending; brow[b] = the row's local
-//           column (internal) or global column (border); level order;
-//           internal blocks b < n_li are staged in LDS)
-// Local blocks b < nblk are the off-diagonal blocks of the subtree's columns
-// (internal rows first, then border rows >= c0, column order); gsl[b] = the
-// global slot; blocks b < n_lds live in LDS. DIAG(c) list: (block of L_kp,
-// local p) pairs; OFF task b (one per block): column tcol[b], list
-// [tptr[b], tptr[b + 1]) of (block of L_ip, block of L_kp) pairs. Both in the
-// global plan's order (ascending p). itemsA: DIAG(-1 - c) and internal OFF
-// blocks, level by level; itemsB: border OFF blocks, level by level (waves
-// [0, nwA) start on list A; a list once exhausted sends its waves to the other).
-constexpr int kSubRec = 21;  // record header ints
-struct SubtreeImage {
-  std::vector<int32_t> data;
-  int ns = 0;
-  int64_t lds_bytes = 0;     // largest subtree's dynamic LDS (factor)
-  int64_t bs_lds_bytes = 0;  // (back-substitution)
-};
-// with_border = false: the border blocks (rows in the dense tail) are not
-// the subtree workgroup's items (list B empty, only internal blocks in LDS):
-// df_factor_kernel computes them over the chip (subtree path, round 4)
-void build_subtree_image(const SparsePlan &P, int64_t lds_cap_bytes, SubtreeImage &out, bool with_border = false);
-
 // Flattened int32 image of the plan (offsets of each array into it).
 struct PlanImage {
   std::vector<int32_t> data;

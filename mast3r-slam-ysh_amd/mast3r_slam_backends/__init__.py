@@ -122,7 +122,7 @@ EXPORTS = (
     "m3s_gn_workspace_size", "m3s_gauss_newton_points", "m3s_gauss_newton_rays",
     "m3s_gauss_newton_calib", "m3s_gn_prepare", "m3s_gn_linearize", "m3s_gn_solve", "m3s_gn_release",
     "m3s_track_workspace_size", "m3s_track_rays_sim3", "m3s_track_calib_sim3", "m3s_version",
-    "m3s_sparse_plan_debug", "m3s_subtree_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
+    "m3s_sparse_plan_debug", "m3s_gn_layout_debug", "m3s_iter_proj", "m3s_refine_matches",
     "m3s_fuse_pointmap", "m3s_prep_rays", "m3s_debug_stamps", "m3s_debug_sim3",
     "m3s_debug_copy", "m3s_set_knob", "m3s_debug_call_timing", "m3s_debug_call_times",
 )
@@ -156,8 +156,6 @@ def _load(path=LIB_PATH):
         getattr(lib, f).argtypes = [P(TrackArgs), _VP]
     lib.m3s_version.restype = ctypes.c_char_p
     lib.m3s_version.argtypes = []
-    lib.m3s_subtree_plan_debug.restype = ctypes.c_int64
-    lib.m3s_subtree_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, _VP, ctypes.c_int64, _VP]
     lib.m3s_sparse_plan_debug.restype = ctypes.c_int64
     lib.m3s_sparse_plan_debug.argtypes = [ctypes.c_int32, ctypes.c_int64, _VP, _VP, ctypes.c_int32, ctypes.c_int32, _VP,
                                           ctypes.c_int64, _VP]
@@ -293,40 +291,6 @@ def workspace_layout(N, HW, E):
     offs = (ctypes.c_size_t * len(LAYOUT_SECTIONS))()
     _lib.m3s_gn_layout_debug(int(N), int(HW), int(E), offs)
     return dict(zip(LAYOUT_SECTIONS, list(offs)))
-
-
-SUBTREE_REC = ("ncol", "nblk", "n_lds", "nA", "nB", "cols", "gsl", "itemsA", "itemsB", "dptr", "dlist", "tcol",
-               "tptr", "tlist", "nwA", "ci", "cb", "brow", "corder", "n_int", "n_li")
-
-
-def subtree_plan(N, ri, rj):
-    """The chip-wide path's subtree image (diagnostics/tests; CPU only): a list
-    of per-subtree dicts with the record's arrays, plus the image meta."""
-    import numpy as np
-
-    ri = np.ascontiguousarray(ri, np.int32)
-    rj = np.ascontiguousarray(rj, np.int32)
-    meta = np.zeros(4, np.int64)
-    P = ctypes.c_void_p
-    args = (int(N), len(ri), P(ri.ctypes.data), P(rj.ctypes.data))
-    n = _lib.m3s_subtree_plan_debug(*args, None, 0, P(meta.ctypes.data))
-    img = np.zeros(n, np.int32)
-    _lib.m3s_subtree_plan_debug(*args, P(img.ctypes.data), n, P(meta.ctypes.data))
-    ns = int(img[0])
-    subs = []
-    for s_ in range(ns):
-        h = img[int(img[1 + s_]):int(img[1 + s_]) + len(SUBTREE_REC)]
-        d = {k: int(v) for k, v in zip(SUBTREE_REC, h)}
-        ncol, nblk, nt = d["ncol"], d["nblk"], d["nblk"]
-        lens = {"cols": ncol, "gsl": nblk, "itemsA": d["nA"], "itemsB": d["nB"], "dptr": ncol + 1, "tcol": nblk,
-                "tptr": nt + 1, "ci": ncol + 1, "cb": ncol + 1, "brow": nblk, "corder": ncol}
-        for k, ln in lens.items():
-            d[k] = img[d[k]:d[k] + ln].copy()
-        d["dlist"] = img[d["dlist"]:d["dlist"] + 2 * int(d["dptr"][-1])].reshape(-1, 2).copy()
-        d["tlist"] = img[d["tlist"]:d["tlist"] + 2 * int(d["tptr"][-1])].reshape(-1, 2).copy()
-        subs.append(d)
-    return subs, {"ns": ns, "lds_bytes": int(meta[1]), "bs_lds_bytes": int(meta[2]), "nc": int(meta[3]),
-                  "max_lds_bytes": int(img[1 + ns])}
 
 
 def sparse_plan(N, ri, rj, split=0, max_parts=0):

@@ -563,28 +563,6 @@ def test_block_dataflow_matches_column_tasks_bitwise(test_lib, be, N, knobs):
     np.testing.assert_array_equal(T_a, T_b)
 
 
-@pytest.mark.parametrize("N", [90, 140, 256, 400])
-def test_subtree_factor_matches_block_dataflow_bitwise(test_lib, be, N, knobs):
-    """Large graphs (round 4): the sparse columns below the dense tail factored
-    as subtrees, one LDS workgroup each (subtree_factor_kernel, test knob
-    subtree=1; the A/B path, measured slower), against df_factor_kernel's
-    chip-wide dataflow over the same columns (the product path). Both run
-    every block's update list in the global plan's order with the same
-    per-block arithmetic: poses and dx agree bitwise."""
-    from mast3r_slam_amd import synthetic
-
-    g = synthetic.make_graph(N, 12, 16, seed=750 + N)
-    knobs("gcomb", "0")  # the same back-substitution on both sides (col_backsub_kernel's sums)
-    knobs("subtree", "1")
-    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
-    knobs("subtree", "0")
-    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
-    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
-    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
-    np.testing.assert_array_equal(dx_a, dx_b)
-    np.testing.assert_array_equal(T_a, T_b)
-
-
 @pytest.mark.parametrize("N", [128, 140, 256, 400])
 def test_tail_pairs_match_tail_columns_bitwise(test_lib, be, N, knobs):
     """The dense tail with two tile columns per workgroup (tail_pair_kernel,
@@ -702,34 +680,6 @@ def test_tail_warmup_leaves_factor_bitwise(test_lib, be, N, knobs):
     np.testing.assert_array_equal(T_a, T_b)
 
 
-@pytest.mark.parametrize("N", [128, 140, 256, 400])
-def test_tail_zinv_matches_substitution(test_lib, be, N, knobs):
-    """Round 5: the dense tail's back-substitution through Z = L^-1, one
-    column per wave as the factor's column flags land (tail_zinv_col, test
-    knob tail_zinv=1; measured slower, kept as a checked A/B path), against
-    the substitution over the tile columns after the last one
-    (tail_backsub_wg, the default): the same factor, a different fp64
-    summation order, so dx agrees to fp64 round-off seen through the fp32
-    output (as the one-workgroup tail above); bitwise run to run; odd and
-    even tile counts."""
-    from mast3r_slam_amd import synthetic
-
-    g = synthetic.make_graph(N, 12, 16, seed=870 + N)
-    knobs("gcomb", "0")  # col_backsub_kernel on both sides (the workers need tail_backsub_wg's x_t flag)
-    knobs("tail_zinv", "1")
-    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
-    knobs("tail_zinv", "0")
-    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
-    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
-    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
-    np.testing.assert_allclose(dx_a, dx_b, rtol=0, atol=1e-6 * np.abs(dx_b).max() + 1e-9)
-    np.testing.assert_allclose(T_a, T_b, rtol=0, atol=1e-6)
-    knobs("tail_zinv", "1")
-    T_a2, dx_a2, _ = run_gpu(be, "rays", g, 3, 0.0)
-    np.testing.assert_array_equal(dx_a, dx_a2)
-    np.testing.assert_array_equal(T_a, T_a2)
-
-
 @pytest.mark.parametrize("N", [90, 128, 140, 256, 400])
 def test_sparse_backsub_workers_match_column_tasks(test_lib, be, N, knobs):
     """Round 5: the sparse columns' back-substitution as x_k = a_k + B_k x_t
@@ -775,23 +725,3 @@ def test_broken_plan_through_workers_is_solve_failure(test_lib, be, knobs):
     T_ok, _, info = run_gpu(be, "rays", g, 1, 0.0)
     assert info[be.INFO_SOLVE_FAIL] == 0 and info[be.INFO_ITERS] == 1
     assert not np.array_equal(T_ok, g.T_init.data.numpy())
-
-
-@pytest.mark.parametrize("N", [140, 256])
-def test_tail_beside_factor_matches_sequential(test_lib, be, N, knobs):
-    """Round 5, test build: the dense tail launched on a second stream beside
-    df_factor_kernel (knob tail_conc: every tile-column pair waits for its own
-    border blocks' flags, the workers for df's slot flags) against the
-    sequential launches: the same operations on the same data, so the same
-    result bitwise; no failures."""
-    from mast3r_slam_amd import synthetic
-
-    g = synthetic.make_graph(N, 12, 16, seed=890 + N)
-    knobs("gcomb_min_nc", "0")  # the workers on too
-    T_a, dx_a, info_a = run_gpu(be, "rays", g, 3, 0.0)
-    knobs("tail_conc", "1")
-    T_b, dx_b, info_b = run_gpu(be, "rays", g, 3, 0.0)
-    assert info_a[be.INFO_SOLVE_FAIL] == info_b[be.INFO_SOLVE_FAIL] == 0
-    assert info_a[be.INFO_ITERS] == info_b[be.INFO_ITERS] == 3
-    np.testing.assert_array_equal(dx_a, dx_b)
-    np.testing.assert_array_equal(T_a, T_b)

@@ -237,139 +237,3 @@ def test_plan_fill_is_sparse_on_loop_graph(be):
     dense_slots = 31 * 32 // 2
     assert p["S"] < 0.4 * dense_slots
     assert p["levels"] < 31
-
-
-def run_subtree_plan(p, subs, Hjj, gj):
-    """The chip-wide path with subtrees (round 4) in numpy: every subtree's
-    items in the order one workgroup may run them (list A, then list B; each
-    level-ordered), checking every input is final when read; the dense tail
-    from the border updates; the back-substitution over the subtree image's
-    per-column block ranges. Returns x in the original variable order."""
-    m, S = p["m"], p["S"]
-    nc = p["nc"]
-    c0 = m - nc
-    L = np.zeros((S, 7, 7))
-    for s_ in range(S):
-        for t in range(p["asm_ptr"][s_], p["asm_ptr"][s_ + 1]):
-            L[s_] += Hjj[p["asm_edge"][t]] * (1 if s_ < m else -1)
-    y = np.zeros((m, 7))
-    for v in range(m):
-        for t in range(p["g_ptr"][v], p["g_ptr"][v + 1]):
-            ent = p["g_edge"][t]
-            y[v] += gj[ent >> 1] * (1 if ent & 1 else -1)
-    W = np.zeros((m, 7, 7))
-    fdone = np.zeros(S, bool)  # final factor blocks (global slots); diagonal k = W_k and y_k
-    seen = set()
-    for d in subs:
-        cols, gsl = d["cols"], d["gsl"]
-        seen.update(cols.tolist())
-        for code in list(d["itemsA"]) + list(d["itemsB"]):
-            if code < 0:
-                c = -1 - code
-                k = cols[c]
-                D, b = L[k].copy(), y[k].copy()
-                for blk, pc in d["dlist"][d["dptr"][c]:d["dptr"][c + 1]]:
-                    assert fdone[gsl[blk]] and fdone[cols[pc]]
-                    A = L[gsl[blk]]
-                    D -= A @ A.T
-                    b -= A @ y[cols[pc]]
-                Lk = np.linalg.cholesky(D)
-                W[k] = np.linalg.inv(Lk)
-                y[k] = W[k] @ b
-                fdone[k] = True
-            else:
-                blk = code
-                k = cols[d["tcol"][blk]]
-                A = L[gsl[blk]].copy()
-                for ba, bb in d["tlist"][d["tptr"][blk]:d["tptr"][blk + 1]]:
-                    assert fdone[gsl[ba]] and fdone[gsl[bb]]
-                    A -= L[gsl[ba]] @ L[gsl[bb]].T
-                assert fdone[k]
-                L[gsl[blk]] = A @ W[k].T
-                fdone[gsl[blk]] = True
-        assert d["nB"] == 0  # border rows are df_factor_kernel's (level order over the chip)
-        for blk in range(d["n_int"], d["nblk"]):  # column order: a topological order of the border blocks
-            k = cols[d["tcol"][blk]]
-            A = L[gsl[blk]].copy()
-            for ba, bb in d["tlist"][d["tptr"][blk]:d["tptr"][blk + 1]]:
-                assert fdone[gsl[ba]] and fdone[gsl[bb]]
-                A -= L[gsl[ba]] @ L[gsl[bb]].T
-            L[gsl[blk]] = A @ W[k].T
-            fdone[gsl[blk]] = True
-        assert all(fdone[g_] for g_ in gsl) and all(fdone[k] for k in cols)
-    assert seen == set(range(c0))  # every sparse column in exactly one subtree
-    assert sum(len(d["cols"]) for d in subs) == c0
-    x = np.zeros((m, 7))
-    if nc:  # dense tail: border updates from every sparse column, then a dense solve
-        T = np.zeros((7 * nc, 7 * nc))
-        rt = np.zeros(7 * nc)
-        blocks = {}
-        for k in range(m):
-            for q in range(p["col_ptr"][k], p["col_ptr"][k + 1]):
-                blocks[(p["col_row"][q], k)] = p["col_slot"][q]
-        for ci in range(nc):
-            for ri_ in range(ci, nc):
-                i, j = c0 + ri_, c0 + ci
-                A = L[i].copy() if i == j else L[blocks[(i, j)]].copy()
-                for pp in range(c0):
-                    if (i, pp) in blocks and (j, pp) in blocks:
-                        A -= L[blocks[(i, pp)]] @ L[blocks[(j, pp)]].T
-                T[7 * ri_:7 * ri_ + 7, 7 * ci:7 * ci + 7] = A
-                T[7 * ci:7 * ci + 7, 7 * ri_:7 * ri_ + 7] = A.T
-            b = y[c0 + ci].copy()
-            for pp in range(c0):
-                if (c0 + ci, pp) in blocks:
-                    b -= L[blocks[(c0 + ci, pp)]] @ y[pp]
-            rt[7 * ci:7 * ci + 7] = b
-        x[c0:] = np.linalg.solve(T, rt).reshape(nc, 7)
-    done = np.zeros(m, bool)
-    done[c0:] = True
-    for d in subs:  # back-substitution, root first, rows ascending (internal, then border)
-        cols, gsl = d["cols"], d["gsl"]
-        for c in d["corder"][::-1]:
-            k = cols[c]
-            r = y[k].copy()
-            for b in range(d["ci"][c], d["ci"][c + 1]):
-                pc = d["brow"][b]
-                assert done[cols[pc]]
-                r -= L[gsl[b]].T @ x[cols[pc]]
-            for b in range(d["cb"][c], d["cb"][c + 1]):
-                r -= L[gsl[b]].T @ x[d["brow"][b]]
-            x[k] = W[k].T @ r
-            done[k] = True
-    assert done.all()
-    out = np.zeros((m, 7))
-    for vn in range(m):
-        out[p["perm"][vn]] = x[vn]
-    return out.reshape(-1)
-
-
-@pytest.mark.parametrize("N,seed", [(90, 11), (128, 1003), (140, 12), (256, 1003)])
-def test_subtree_plan_executes_to_dense_solution(be, N, seed):
-    """The subtree image (chip-wide path, round 4): disjoint subtrees that
-    cover every sparse column, update lists that stay inside a subtree, a
-    workgroup order whose inputs are final when read, and a back-substitution
-    whose block ranges solve the system: x equals a dense fp64 solve."""
-    from mast3r_slam_amd import synthetic
-
-    g = synthetic.make_graph(N, 2, 2, seed=seed, edge_range=(0, 0))
-    ii, jj = g.ii.numpy(), g.jj.numpy()
-    u = np.unique(np.concatenate([ii, jj]))
-    ri, rj = np.searchsorted(u, ii), np.searchsorted(u, jj)
-    rng = np.random.default_rng(seed)
-    E = len(ii)
-    Hjj = np.zeros((E, 7, 7))
-    for e in range(E):
-        A = rng.standard_normal((7, 7))
-        Hjj[e] = A @ A.T + 7 * np.eye(7)
-    gj = rng.standard_normal((E, 7))
-    p = be.sparse_plan(N, ri, rj)
-    subs, meta = be.subtree_plan(N, ri, rj)
-    assert meta["ns"] == len(subs) >= 1 and meta["nc"] == p["nc"]
-    assert meta["lds_bytes"] <= 140 * 1024 and meta["bs_lds_bytes"] <= 140 * 1024
-    for d in subs:  # every block's rows: internal (local column) before border (tail column)
-        assert (d["brow"][:d["n_int"]] < d["ncol"]).all()
-        assert (d["brow"][d["n_int"]:] >= p["m"] - p["nc"]).all()
-    H, gv = dense_system(N, ri, rj, Hjj, gj)
-    x = run_subtree_plan(p, subs, Hjj, gj)
-    np.testing.assert_allclose(x, np.linalg.solve(H, gv), rtol=1e-9, atol=1e-9)

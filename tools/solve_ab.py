@@ -5,7 +5,7 @@ settings in SOLVE_AB ("name=v;name=v|name=v" groups), prints the median call
 time per setting and whether poses agree bitwise with the first setting.
 Under rocprofv3 --kernel-trace --stats the per-kernel times come out too.
 
-usage: python tools/solve_ab.py   (env: SOLVE_N="128,256" SOLVE_AB="subtree=1|subtree=0"
+usage: python tools/solve_ab.py   (env: SOLVE_N="128,256" SOLVE_AB="tail_pair=1|tail_pair=0"
                                     SOLVE_MODE=calib SOLVE_ITERS=3 SOLVE_ROUNDS=7
                                     LIB=variants/lib_X_test.so: another test build)
 """
@@ -28,7 +28,7 @@ def main():
     mode = os.environ.get("SOLVE_MODE", "calib")
     iters = int(os.environ.get("SOLVE_ITERS", "3"))
     rounds = int(os.environ.get("SOLVE_ROUNDS", "7"))
-    groups = [dict(kv.split("=") for kv in g.split(";") if kv) for g in os.environ.get("SOLVE_AB", "subtree=0;tail_pair=1|subtree=0;tail_pair=0|subtree=1;tail_pair=1").split("|")]
+    groups = [dict(kv.split("=") for kv in g.split(";") if kv) for g in os.environ.get("SOLVE_AB", "tail_pair=1|tail_pair=0").split("|")]
     H, W = 12, 16
     for N in [int(x) for x in os.environ.get("SOLVE_N", "128,256").split(",")]:
         g = synthetic.make_graph(N, H, W, seed=1003, device=dev)

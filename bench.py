@@ -206,17 +206,18 @@ def run(args):
                        ops=ops, **sig)
     info = torch.zeros(8, dtype=torch.int32, device=dev)
 
-    def step(delta=0.0):
+    def step(delta=0.0, iters=None):
+        iters = args.iters if iters is None else iters
         Twc.copy_(T_init)
         if world == 1 and not dry:  # the drop-in entry point itself
             if calib_mode:
                 be.gauss_newton_calib(Twc, Xs, Cs, g.K, ii, jj, idx, valid, Q, H, W, -10, 1e-6, 1.0,
-                                      10.0, 0.0, 1.5, args.iters, delta, info=info)
+                                      10.0, 0.0, 1.5, iters, delta, info=info)
             else:
                 be.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5,
-                                     args.iters, delta, info=info)
+                                     iters, delta, info=info)
         else:
-            solver.solve(args.iters, delta)
+            solver.solve(iters, delta)
 
     def sync():
         if not dry:
@@ -321,7 +322,7 @@ def run(args):
                        "not a scaling measurement" % world)
     else:
         out["roofline"] = roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
-                                       world, dev, step if world == 1 else None)
+                                       world, dev, step if world == 1 else None, elapsed / args.steps)
 
     if rank == 0 and world == 1 and not dry:
         out["hbm_copy"] = copy_leg(be, dev)
@@ -340,15 +341,24 @@ def run(args):
         dist.destroy_process_group()
 
 
-def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s, world, dev, call=None):
+def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s, world, dev, call=None,
+                 step_s=None):
     """The dominant kernel: GN iterations 2..10 of a call run
     linearize_packed_kernel (the first runs the gathering kernel that also
-    stores the target-side planes). Timed in the benched call's own launch
-    pattern: at N = 1 the drop-in call itself records HIP timing events on its
-    stream around each iteration's linearize launch and solve launches
-    (m3s_debug_call_timing; nothing else is launched between them); a sharded
-    rank times its stepwise solve's linearize launches (their per-edge reduce
-    included). The same kernel launched back to back is timed too."""
+    stores the target-side planes).
+
+    At N = 1 (round 6, reconciled with the timed steps): the packed kernel's
+    time per launch in the benched calls themselves is
+        (T_10 - T_1) / 9 - solve,
+    T_10 / T_1 the per-call times of un-instrumented drop-in calls with 10 and
+    1 GN iterations (HIP events around batches of calls, interleaved), solve
+    the LLT dispatch's own span. The instrumented calls (m3s_debug_call_timing:
+    each linearize and the one-launch solve through hipExtLaunchKernel with
+    the dispatch's begin / end events) give the gathering launch, the solve
+    and the packed kernel's dispatch span as a cross-check; spans x launches
+    is reported beside ms_per_step. A sharded rank times its stepwise solve's
+    linearize launches (their per-edge reduce included). The same kernel
+    launched back to back is timed too."""
     n_loc = len(ids)
     sel = torch.tensor(ids, dtype=torch.int64, device=ii.device)
     kf_touched = torch.unique(torch.cat([ii[sel], jj[sel]])).numel() if n_loc else 0
@@ -367,11 +377,27 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
         first = [ms for k, ms in spans if k == 0]
         lin = [ms for k, ms in spans if k == 1]
         slv = [ms for k, ms in spans if k == 2]
-        timing = ("each packed launch's own dispatch span inside the drop-in call (m3s_debug_call_timing: "
-                  "begin / end events of the dispatch itself via hipExtLaunchKernel; the call's own launch "
-                  "pattern, 5 calls x %d packed launches; profiles/r04/prof_bench/prof_split.txt puts it "
-                  "within 1%% of the kernel trace of the same calls); back_to_back_ms = the same kernel "
-                  "launched back to back (HIP events around the run)" % (args.iters - 1))
+        # un-instrumented calls of 10 and 1 GN iterations, interleaved batches
+        t_n, t_1 = [], []
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for _ in range(4):
+            for iters, acc in ((args.iters, t_n), (1, t_1)):
+                call(iters=iters)
+                ev[0].record()
+                for _ in range(10):
+                    call(iters=iters)
+                ev[1].record()
+                torch.cuda.synchronize()
+                acc.append(ev[0].elapsed_time(ev[1]) / 10)
+        call_n, call_1 = statistics.median(t_n), statistics.median(t_1)
+        slv_ms = sum(slv) / len(slv)
+        lin_step = (call_n - call_1) / (args.iters - 1) - slv_ms
+        timing = ("packed launch time in the benched calls: (T_%d - T_1) / %d - solve, T_k = per-call time of "
+                  "un-instrumented drop-in calls of k GN iterations (HIP events around 4 x 10 calls each, "
+                  "interleaved; medians), solve = the LLT dispatch's own span (hipExtLaunchKernel); "
+                  "dispatch_span_ms = the packed dispatch's own span in 5 instrumented calls; back_to_back_ms = "
+                  "the same kernel launched back to back (HIP events around the run)"
+                  % (args.iters, args.iters - 1))
     else:
         for rep in range(4):
             Twc.copy_(T_init)
@@ -382,7 +408,8 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
                 slv += t_slv
         timing = ("HIP events around each linearize launch (+ its per-edge reduce) of this rank's "
                   "stepwise solves; back_to_back_ms = the same kernel launched back to back")
-    lin_ms = sum(lin) / len(lin)
+    span_ms = sum(lin) / len(lin)
+    lin_ms = lin_step if call is not None else span_ms
     Twc.copy_(T_init)
     be.gn_prepare(solver.args, solver.keep)
     solver.linearize_only()  # first launch: gathering kernel + planes
@@ -421,6 +448,7 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
         "algorithmic_bytes_per_launch": bytes_alg,
         "avg_launch_ms": round(lin_ms, 5),
         "timing": timing,
+        "dispatch_span_ms": round(span_ms, 5),
         "in_call_ms_min_max": [round(min(lin), 5), round(max(lin), 5)],
         "back_to_back_ms": round(b2b_ms, 5),
         "gather_kernel": {
@@ -432,10 +460,19 @@ def roofline_leg(args, solver, be, Twc, T_init, ii, jj, ids, HW, gn_iters_per_s,
         },
         "solve": {
             "kernels": "fp64 block-sparse LLT + retraction: every solve launch of one GN iteration "
-                       "(in-call events at N = 1; the stepwise path's finalize + assemble included at N > 1)",
+                       "(at N = 1 the one sparse_llt_kernel dispatch's own span; the stepwise path's finalize + "
+                       "assemble included at N > 1)",
             "avg_ms": round(sum(slv) / len(slv), 5),
             "bound": "latency (elimination-tree critical path, DESIGN.md §4)",
         },
+        "reconcile": None if call is None else {
+            "ms_per_step": round(step_s * 1e3, 5) if step_s else None,
+            "call_ms": {str(args.iters): round(call_n, 5), "1": round(call_1, 5)},
+            "spans_x_launches_ms": round(first_ms + (args.iters - 1) * lin_ms + args.iters * slv_ms, 5),
+            "ratio_to_ms_per_step": round((first_ms + (args.iters - 1) * lin_ms + args.iters * slv_ms)
+                                          / (step_s * 1e3), 4) if step_s else None,
+            "note": "gathering span + %d x packed + %d x solve; the rest of a call is its prologue kernel and "
+                    "the inter-call gap" % (args.iters - 1, args.iters)},
         "iteration_level": {
             "achieved": round(bytes_alg * gn_iters_per_s / 1e9, 1) if world == 1 else None,
             "note": "SURVEY.md §8(d) B_iter x GN iterations/s (whole iteration: linearize, "

@@ -226,9 +226,11 @@ int m3s_debug_copy(const void *src, void *dst, int64_t nbytes, int blocks, void 
  * record is cleared after reading. Linearize spans are the dispatch's own
  * begin / end timestamps: the call launches each linearize through
  * hipExtLaunchKernel with a start / stop event pair (round 4: events recorded
- * around the launch read 6-12% above the kernel trace). A linearize that does
- * not go through that launch (the non-vectorised first iteration) and every
- * solve span use the events recorded around the launches. */
+ * around the launch read 6-12% above the kernel trace). A small graph's solve
+ * (one sparse_llt_kernel launch) is timed the same way (round 6: the events
+ * around it read ~19% above the trace). A linearize that does not go through
+ * that launch (the non-vectorised first iteration) and a large graph's
+ * multi-launch solve use the events recorded around the launches. */
 int m3s_debug_call_timing(int enable);
 int m3s_debug_call_times(float *ms, int32_t *kinds, int cap);
 

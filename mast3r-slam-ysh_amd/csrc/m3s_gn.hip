@@ -951,6 +951,15 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
 // flight), the pose-only math, the rest, the plane stores. Same arithmetic per
 // pixel as linearize_kernel<MODE, false, true, true> (gather_pixel +
 // make_pixin + pixel_contrib): bitwise the same planes, partials and sums.
+// Floor builds (A/B measurement only, wrong sums):
+// M3S_GATHER_FLOOR = 1 no math, 2 no gathers (the slot's values stand in),
+// 3 no plane stores, 4 streams only (no gathers, math or stores).
+#ifndef M3S_GATHER_FLOOR
+#define M3S_GATHER_FLOOR 0
+#endif
+constexpr bool kGFloorNoMath = M3S_GATHER_FLOOR == 1 || M3S_GATHER_FLOOR == 4;
+constexpr bool kGFloorNoGather = M3S_GATHER_FLOOR == 2 || M3S_GATHER_FLOOR == 4;
+constexpr bool kGFloorNoStore = M3S_GATHER_FLOOR == 3 || M3S_GATHER_FLOOR == 4;
 // per-wave slot (bytes): valid u8x4 | Q | idx (int64: two 1-KB rows; int32: one) | Xj (3 rows) | Cj
 constexpr int kGsValid = 0, kGsQ = 256, kGsIdx = 1280, kGsXj = 3328, kGsCj = 6400, kGsBytes = 7424;
 __device__ __forceinline__ void buf_lds4_nt(__amdgpu_buffer_rsrc_t R, __attribute__((address_space(3))) void *lds,
@@ -1047,13 +1056,14 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
 
   AccumFlat acc;
   acc.zero();
+  float gsink = 0.0f;  // the floor builds only
   int pw = (int)p_begin + kPixPerThread * 64 * wv;
   if (pw < pend) issue(pw, false);
   for (int trip = 0; pw < pend; pw += kBlockPix, trip++) {
     // the slot's DMA is done once only the previous trip's NPL plane stores
     // may still be in flight behind it (stores count in vmcnt, in issue
     // order); the first trip has no stores behind its loads
-    if (trip == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (trip == 0 || kGFloorNoStore) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (NPL == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     const int p0 = pw + kPixPerThread * ln;
@@ -1082,6 +1092,10 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
       // 12 id on the full-rate 24-bit multiply (v_mul_lo_u32 is quarter rate;
       // the host takes this kernel only for HW <= 2^24)
       const int o12 = (int)__umul24((unsigned)id[s4], 12u);
+      if constexpr (kGFloorNoGather) {  // floor build: the slot's own values stand in for the gathers
+        gx[s4][0] = g.x0.x, gx[s4][1] = g.x0.y, gx[s4][2] = g.x0.z + (float)o12, gc[s4] = g.c.x;
+        continue;
+      }
       if (MODE == M3S_MODE_CALIB) {
         gx[s4][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(RXi, o12 + 8, 0, 0));
       } else {
@@ -1099,8 +1113,16 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
     const float qs[4] = {g.q.x, g.q.y, g.q.z, g.q.w};
     const float cjs[4] = {g.c.x, g.c.y, g.c.z, g.c.w};
     PixIn<MODE> in[4];
+    if constexpr (kGFloorNoMath) {  // floor build: the loaded values go straight to the planes
 #pragma unroll
-    for (int s4 = 0; s4 < 4; s4++) {
+      for (int s4 = 0; s4 < 4; s4++) {
+#pragma unroll
+        for (int k = 0; k < NPL; k++) in[s4].v[k] = gx[s4][k % 3] + (k == 1 ? gc[s4] + qs[s4] + cjs[s4] + Xj[s4][0] : 0.0f);
+      }
+      gsink += in[0].v[0] + in[3].v[NPL - 1];
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4 && !kGFloorNoMath; s4++) {
       const bool ok = vm[s4] && (qs[s4] > P.Q_thresh) && (gc[s4] > P.C_thresh) && (cjs[s4] > P.C_thresh);
       int u_t = 0, v_t = 0;
       if (MODE == M3S_MODE_CALIB) {  // gather_pixel's ind_Xi % width, ind_Xi / width
@@ -1117,10 +1139,14 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
       in[s4] = make_pixin<MODE>(P, gx[s4], ok, qs[s4], u_t, v_t);
     }
 #pragma unroll
-    for (int s4 = 0; s4 < 4; s4++) {
+    for (int s4 = 0; s4 < 4 && !kGFloorNoMath; s4++) {
       float Y[3];
       act(Tm, Xj[s4], Y);
       pixel_contrib<MODE>(acc, P, in[s4], Y);
+    }
+    if constexpr (kGFloorNoStore) {
+      gsink += in[0].v[0] + in[1].v[NPL - 1] + in[2].v[0] + in[3].v[NPL - 1];
+      continue;
     }
     // NPL plane stores after the refill: the loop top's counted vmcnt(NPL)
     // relies on at least NPL vector-memory operations following the refill's
@@ -1136,6 +1162,7 @@ __global__ void __launch_bounds__(kThreads) linearize_gather_kernel(LinArgs A) {
 #pragma unroll
   for (int k = 0; k < kNP; k++) sums[k] = 0.0f;
   acc.fold(sums);
+  sums[0] += gsink;  // 0 but in the floor builds
   store_partial(sums, A.partials + (size_t)b * kNP);
   if (A.edge_cnt) edge_tail(A, e_loc, e);
 }
@@ -3239,13 +3266,81 @@ __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], doub
   for (int r = 0; r < 4; r++) Wk[lk + 4 * r][lr] = M[r];
   return bad;
 }
-// Not inlined: each tail workgroup factors its diagonal tile(s) once, so the
-// ~600 instructions run from a cold instruction cache (measured ~2.5 us per
-// tile, ~4x the MFMA / LDS latencies it is made of). One copy of the code, run
-// once on a dummy tile while the workgroup waits for its updates
-// (tail_diag_warm), is then hot when the real tile arrives.
-__device__ __noinline__ bool tail_diag_full(f64x4 a, double (*Wk)[17], double *yv_k, int lane) {
-  return tail_diag_mfma_t<true>(a, Wk, yv_k, 16, -1, lane);
+// Lane I's value to every lane of its 16-lane row (DPP row_newbcast, gfx90a+:
+// one v_mov_b64_dpp); I must fold to a constant (unrolled loops)
+template <int I>
+__device__ __forceinline__ double row_bcast_c(double v) {
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + I, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double row_bcast(double v, int i) {
+  switch (i) {
+    case 0: return row_bcast_c<0>(v);
+    case 1: return row_bcast_c<1>(v);
+    case 2: return row_bcast_c<2>(v);
+    case 3: return row_bcast_c<3>(v);
+    case 4: return row_bcast_c<4>(v);
+    case 5: return row_bcast_c<5>(v);
+    case 6: return row_bcast_c<6>(v);
+    case 7: return row_bcast_c<7>(v);
+    case 8: return row_bcast_c<8>(v);
+    case 9: return row_bcast_c<9>(v);
+    case 10: return row_bcast_c<10>(v);
+    case 11: return row_bcast_c<11>(v);
+    case 12: return row_bcast_c<12>(v);
+    case 13: return row_bcast_c<13>(v);
+    case 14: return row_bcast_c<14>(v);
+    default: return row_bcast_c<15>(v);
+  }
+}
+
+// Full diagonal tile (jv == 16, round 6): a right-looking 16-column Cholesky
+// and W = L^-1 on the VALU with no LDS or MFMA on the chain. After one LDS
+// transpose every 16-lane row of the wave holds the tile by columns (lane c:
+// column c, which is row c of the symmetric tile; the four rows compute the
+// same, so any lane has what it needs). Step k: the pivot A(k,k) from lane k
+// by a DPP row broadcast, r = 1 / sqrt (rsqrt_nr), L(c,k) = A(k,c) r and
+// W(k,c) = R(k,c) r on every lane c, then for every row i > k the broadcast
+// L(i,k) updates A(i,c) -= L(i,k) L(c,k) and R(i,c) -= L(i,k) W(k,c) (R starts
+// as I: the forward substitution of L W = I, right-looking). One
+// v_mov_b64_dpp and two v_fma_f64 per (k, i): ~600 instructions with the
+// chain per column a broadcast, the rsqrt, a product and one update, where
+// the blocked MFMA form (tail_diag_mfma_t, kept for the partial last tile)
+// spent ~2.4 us per tile on four LDS round trips and dependent MFMAs. The
+// same arithmetic as the by-columns definition of L and W; another fp64
+// rounding order than the MFMA form (dx within fp64 round-off). Not inlined:
+// one copy of the code, warmed on a dummy tile while the workgroup waits for
+// its updates (tail_diag_warm).
+__device__ __noinline__ bool tail_diag_full(f64x4 a4, double (*Wk)[17], double *yv_k, int lane) {
+  (void)yv_k;
+  __shared__ double xt[16][17];
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; r++) xt[lr][lk + 4 * r] = a4[r];  // entry (row lk + 4 r, column lr)
+  wave_lds_fence();
+  double a[16], R[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    a[i] = xt[lr][i];  // A(i, lr) = A(lr, i)
+    R[i] = i == lr ? 1.0 : 0.0;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const double d0 = row_bcast(a[k], k);
+    bad |= !(d0 > 0.0);
+    const double r = rsqrt_nr(d0 > 0.0 ? d0 : 1.0);
+    const double l = a[k] * r;  // lane c: L(c, k) for c >= k
+    const double w = R[k] * r;  // lane c: W(k, c)
+    if (lk == 0) Wk[k][lr] = w;
+#pragma unroll
+    for (int i = k + 1; i < 16; i++) {
+      const double li = row_bcast(l, i);  // L(i, k)
+      a[i] = __builtin_fma(-li, l, a[i]);
+      R[i] = __builtin_fma(-li, w, R[i]);
+    }
+  }
+  wave_lds_fence();  // Wk (LDS) written before the caller's reads
+  return bad;
 }
 __device__ __noinline__ bool tail_diag_part(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row, int lane) {
   return tail_diag_mfma_t<false>(a, Wk, yv_k, jv, rhs_row, lane);
@@ -4797,6 +4892,9 @@ bool gather_lds_path();  // (knobs, below)
 // linearize went through another launch (the pack == 0 path) and fall back to
 // the events recorded around it.
 thread_local hipEvent_t *g_lin_ext_ev = nullptr;
+// the same for the one-workgroup solve's launch (sparse_llt_kernel, small
+// graphs: the whole solve of an iteration is that one dispatch)
+thread_local hipEvent_t *g_slv_ext_ev = nullptr;
 template <typename K>
 void launch_lin(K kernel, dim3 g, dim3 b, hipStream_t st, const LinArgs &L) {
   if (g_lin_ext_ev) {
@@ -5390,7 +5488,13 @@ int gn_solve_impl(const m3s_gn_args *a, const double *edge_sums, const float *pa
         col_backsub_kernel<<<g4, 64, 0, st>>>(C);
       }
     } else if (meta.store == 1)
-      sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
+      if (g_slv_ext_ev) {
+        hipExtLaunchKernelGGL(sparse_llt_kernel<1>, dim3(1), dim3(1024), meta.lds_bytes, st, g_slv_ext_ev[0],
+                              g_slv_ext_ev[1], 0, D);
+        g_slv_ext_ev = nullptr;
+      } else {
+        sparse_llt_kernel<1><<<1, 1024, meta.lds_bytes, st>>>(D);
+      }
     else if (meta.store == 2)
       sparse_llt_kernel<2><<<1, 1024, meta.lds_bytes, st>>>(D);
     else if (meta.nc > 0 && border_split()) {
@@ -6007,7 +6111,22 @@ int gn_full(const m3s_gn_args *a, int mode, void *stream) {
     g_lin_ext_ev = nullptr;
     if (rc) return rc;
     if (timing && !call_mark(st, 2)) return M3S_ELAUNCH;
-    if ((rc = gn_solve_impl(a, nullptr, partials, chunks, st, sparse))) return rc;
+    if (timing) {  // the solve dispatch's own begin / end when it is one launch (sparse_llt_kernel<1>)
+      while (CT.kev.size() < CT.kused + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return M3S_ELAUNCH;
+        CT.kev.push_back(e);
+      }
+      if (CT.kev_ok.size() < CT.kev.size() / 2) CT.kev_ok.resize(CT.kev.size() / 2);
+      g_slv_ext_ev = &CT.kev[CT.kused];
+    }
+    rc = gn_solve_impl(a, nullptr, partials, chunks, st, sparse);
+    if (timing) {
+      CT.kev_ok[CT.kused / 2] = g_slv_ext_ev == nullptr;
+      CT.kused += 2;
+    }
+    g_slv_ext_ev = nullptr;
+    if (rc) return rc;
     if (timing && !call_mark(st, -1)) return M3S_ELAUNCH;
   }
   return M3S_OK;
@@ -6756,21 +6875,22 @@ int m3s_debug_call_times(float *ms, int32_t *kinds, int cap) {
   std::lock_guard<std::mutex> g(T.mu);
   if (T.used == 0) return 0;
   if (hipEventSynchronize(T.ev[T.used - 1]) != hipSuccess) return M3S_ELAUNCH;
-  // linearize spans (kinds 0, 1): the dispatch's own begin / end events
-  // (hipExtLaunchKernel); solve spans (kind 2): the events around its launches
+  // every span (kinds 0, 1 linearize, 2 solve) has an event pair in kev: the
+  // dispatch's own begin / end (hipExtLaunchKernel) when its work was one
+  // launch that took the pair, else the events recorded around its launches
   int n = 0;
   size_t li = 0;
   for (size_t q = 0; q + 1 < T.used; q++) {
     if (T.kind[q] < 0) continue;
     if (n < cap) {
       float t = 0.0f;
-      const bool lin = T.kind[q] <= 1 && li + 1 < T.kused && T.kev_ok[li / 2];
-      if (hipEventElapsedTime(&t, lin ? T.kev[li] : T.ev[q], lin ? T.kev[li + 1] : T.ev[q + 1]) != hipSuccess)
+      const bool own = li + 1 < T.kused && T.kev_ok[li / 2];
+      if (hipEventElapsedTime(&t, own ? T.kev[li] : T.ev[q], own ? T.kev[li + 1] : T.ev[q + 1]) != hipSuccess)
         return M3S_ELAUNCH;
       ms[n] = t;
       kinds[n] = T.kind[q];
     }
-    if (T.kind[q] <= 1) li += 2;
+    li += 2;
     n++;
   }
   T.used = 0;

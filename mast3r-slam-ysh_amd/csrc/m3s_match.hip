@@ -136,21 +136,32 @@ __global__ void __launch_bounds__(kMatchThreads) iter_proj_kernel(m3s_iter_proj_
 #pragma clang fp contract(on)
 
 // ------------------------------------------------------- refine_matches --
-// Scores accumulate in the descriptor type, one fused multiply-add per
-// feature in feature order (the reference's `score += D21[k] * D11[k]` on
-// __half, matching_kernels.cu:65-67). The running maximum starts at the
-// type's smallest positive normal (numeric_limits<T>::min(), :47): a window
-// whose scores are all below it keeps its centre. Ties keep the first
-// candidate in scan order (dilation descending, u offset outer, v inner).
+// Scores accumulate as the reference's `score += D21[k] * D11[k]`
+// (matching_kernels.cu:58-60) in feature order. fp16 descriptors (scalar_t =
+// c10::Half, the reference's only caller, matching.py:80): a rounded product
+// and a rounded sum per feature (c10::Half computes in float and converts back,
+// score2_f16 below), the running maximum starting at 0 (libcu++'s
+// numeric_limits has no c10::Half specialization: T() = 0, :47). fp32
+// descriptors: nvcc contracts the float expression to one fused multiply-add
+// per feature, the maximum starts at FLT_MIN. A window whose scores never
+// exceed the start keeps its centre. Ties keep the first candidate in scan
+// order (dilation descending, u offset outer, v inner).
 template <typename T>
-__device__ __forceinline__ T min_normal();
+__device__ __forceinline__ T score_start();
 template <>
-__device__ __forceinline__ _Float16 min_normal<_Float16>() {
-  return (_Float16)6.103515625e-05f;
+__device__ __forceinline__ _Float16 score_start<_Float16>() {
+  return (_Float16)0.0f;
 }
 template <>
-__device__ __forceinline__ float min_normal<float>() {
+__device__ __forceinline__ float score_start<float>() {
   return 1.17549435082228750797e-38f;
+}
+// score + a * b in the reference's arithmetic for T
+__device__ __forceinline__ float score_step(float a, float b, float s) { return __builtin_fmaf(a, b, s); }
+__device__ __forceinline__ _Float16 score_step(_Float16 a, _Float16 b, _Float16 s) {
+#pragma clang fp contract(off)
+  const _Float16 p = a * b;
+  return s + p;
 }
 
 // Round 4 measured four restructurings of this kernel on one 512 x 512 pair
@@ -176,7 +187,7 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
     for (int k = 0; k < FMAX; k++) q[k] = d21[k];
   }
   int64_t u0 = A.p1[2 * gid], v0 = A.p1[2 * gid + 1];
-  T max_score = min_normal<T>();
+  T max_score = score_start<T>();
   int64_t u_new = u0, v_new = v0;
   for (int d = A.dilation_max; d > 0; d--) {
     const int rd = A.radius * d;
@@ -190,9 +201,9 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
           T score = (T)0.0f;
           if (FMAX > 0) {
 #pragma unroll
-            for (int k = 0; k < FMAX; k++) score = __builtin_elementwise_fma(q[k], x[k], score);
+            for (int k = 0; k < FMAX; k++) score = score_step(q[k], x[k], score);
           } else {
-            for (int64_t k = 0; k < F; k++) score = __builtin_elementwise_fma(d21[k], x[k], score);
+            for (int64_t k = 0; k < F; k++) score = score_step(d21[k], x[k], score);
           }
           if (score > max_score) {
             max_score = score;
@@ -210,9 +221,9 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
 }
 
 // ---- round 5: refine_f16_kernel (fp16 descriptors, F in {16, 24, 32}) ----
-// The same scan, the same sequential fp16 FMA chain per candidate and the
-// same first-maximum rule as refine_kernel (bitwise equal outputs), re-cut
-// for the memory path:
+// The same scan, the same per-candidate fp16 chain (score2_f16, the
+// reference's c10::Half arithmetic) and the same first-maximum rule as
+// refine_kernel (bitwise equal outputs), re-cut for the memory path:
 // * XCD bands: hardware block b runs on XCD b % 8; logical block
 //   (b % 8) * per + b / 8 gives each XCD one contiguous band of queries
 //   (image rows), so the D11 rows its windows read (+-radius*dilation_max
@@ -220,8 +231,8 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
 //   whole descriptor image;
 // * buffer loads whose offset is past the descriptor image when the
 //   candidate lies outside it (the hardware returns zeros without an access):
-//   no branch per candidate, and a zero score never beats max_score (>= the
-//   smallest positive normal), as a skipped candidate never does;
+//   no branch per candidate, and a zero score never beats max_score (>= 0,
+//   strict >), as a skipped candidate never does;
 // * the next candidate's 16-B loads are issued before the current one's FMA
 //   chain (one candidate in flight per lane besides the one computing);
 // * the odd features are read from the high halves by op_sel (no shifts).
@@ -236,27 +247,36 @@ __global__ void __launch_bounds__(kMatchThreads) refine_kernel(m3s_refine_args A
 typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
 constexpr int kRefFar = 0x7fff0000;  // past any descriptor image (the kernel takes images < 2^30 B): loads return zeros, and o + 16 l stays below 2^31
 
-// Two candidates' scores, each the sequential fp16 FMA chain of the
-// reference in feature order (the low halves of v_pk_fma_f16: one rounding
-// per step, as v_fma_f16; the high halves compute a throw-away chain). The
-// odd feature is read from the high halves by op_sel (the .yy swizzle), so
-// no shifts; the two chains interleave, which also fills the one wait state
-// gfx950 needs between a VALU write and a dependent op_sel read.
+// Two candidates' scores in the reference's c10::Half arithmetic. The
+// reference dispatches refine_matches_kernel on scalar_t = c10::Half
+// (AT_DISPATCH_FLOATING_TYPES_AND_HALF, matching_kernels.cu:103; matching.py:80
+// passes .half() descriptors), and c10::Half's operators compute in float and
+// convert back (c10/util/Half-inl.h): `score += a * b` (:58-60) is
+// p = Half(float(a) * float(b)), score = Half(float(score) + float(p)) -- a
+// rounded product and a rounded sum per feature, in feature order, with no
+// contraction across the conversions. On gfx950: v_pk_mul_f16 forms two
+// features' products at once (a product of two halves is exact in fp32, so
+// its one rounding equals the reference's multiply-then-convert), and
+// v_add_f16 adds them in order (fp32 carries >= 2 * 11 + 2 bits, so the
+// float add then convert equals the correctly rounded half add).
+// Parity unpinned against reference outputs (no fixtures):
+// this follows the source semantics.
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 template <int NL>
 __device__ __forceinline__ void score2_f16(const h2v (&q)[4 * NL], const u32x4m (&xa)[NL], const u32x4m (&xb)[NL],
                                            _Float16 &sa, _Float16 &sb) {
-  h2v a = {0, 0}, b = {0, 0};
+#pragma clang fp contract(off)
+  _Float16 a = 0, b = 0;
 #pragma unroll
   for (int w = 0; w < 4 * NL; w++) {
-    const h2v pa = __builtin_bit_cast(h2v, (unsigned)xa[w >> 2][w & 3]);
-    const h2v pb = __builtin_bit_cast(h2v, (unsigned)xb[w >> 2][w & 3]);
-    a = __builtin_elementwise_fma(q[w], pa, a);
-    b = __builtin_elementwise_fma(q[w], pb, b);
-    a = __builtin_elementwise_fma(q[w].yy, pa.yy, a);
-    b = __builtin_elementwise_fma(q[w].yy, pb.yy, b);
+    const h2v pa = q[w] * __builtin_bit_cast(h2v, (unsigned)xa[w >> 2][w & 3]);
+    const h2v pb = q[w] * __builtin_bit_cast(h2v, (unsigned)xb[w >> 2][w & 3]);
+    a = a + pa.x;
+    b = b + pb.x;
+    a = a + pa.y;
+    b = b + pb.y;
   }
-  sa = a.x, sb = b.x;
+  sa = a, sb = b;
 }
 
 template <int FMAX, int NR>
@@ -290,7 +310,9 @@ __global__ void __launch_bounds__(kMatchThreads) refine_f16_kernel(m3s_refine_ar
   // (radius * dilation_max < 2^20): the reference returns it unchanged
   const bool far = pu < -(1 << 30) || pu > (1 << 30) || pv < -(1 << 30) || pv > (1 << 30);
   int u0 = far ? -(1 << 30) : (int)pu, v0 = far ? -(1 << 30) : (int)pv;
-  _Float16 max_score = min_normal<_Float16>();
+  // ::cuda::std::numeric_limits<c10::Half>::min() (:47): libcu++ has no
+  // specialization for c10::Half, so the primary template's T() = 0
+  _Float16 max_score = (_Float16)0.0f;
   bool moved = false;
   for (int d = A.dilation_max; d > 0; d--) {
     const int rd = NR * d;

@@ -11,18 +11,26 @@ imports it.
                       :271, `*= 10.0` :276), no fused multiply-add.
 * ``refine_matches``  follows matching_kernels.cu:25-78 (refine_matches_kernel):
                       dilation d = dilation_max..1, window offsets u outer / v
-                      inner, strict `score > max_score` with max_score starting
-                      at numeric_limits<T>::min() (:47), centre moved to the best
+                      inner, strict `score > max_score`, centre moved to the best
                       match after every dilation level (:75-76). Scores
-                      accumulate in the descriptor dtype, one correctly rounded
-                      fused multiply-add per feature in feature order.
+                      accumulate in feature order in the arithmetic of the
+                      dispatched scalar_t (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
+                      :103):
+                      - c10::Half (the reference's caller passes .half()
+                        descriptors, matching.py:80): c10::Half's operators
+                        compute in float and convert back (c10/util/Half-inl.h),
+                        so `score += a * b` (:58-60) rounds the product to half
+                        and then the sum to half; max_score starts at
+                        ::cuda::std::numeric_limits<c10::Half>::min() (:47),
+                        which libcu++ does not specialise for c10::Half: the
+                        primary template's T() = 0;
+                      - float: nvcc contracts `score += a * b` to one fused
+                        multiply-add; max_score starts at FLT_MIN.
 
 Parity unpinned: the reference's own tests hold no fixtures for these kernels
  and the CUDA module cannot be built or run here, so this
-restatement is checked against the kernel source, not against reference
-outputs. Where the CUDA source leaves the arithmetic open — whether nvcc fuses
-`score += a * b` on __half, and which `min()` libcu++ returns for __half — the
-choices above are the ones the HIP kernel implements.
+restatement (and the HIP kernel, which implements the same arithmetic) follows
+the kernel source and the c10 / libcu++ semantics above, not reference outputs.
 """
 from __future__ import annotations
 
@@ -114,9 +122,14 @@ def iter_proj(rays_img, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh)
     return np.stack([u, v], -1).reshape(B, N, 2), conv.reshape(B, N)
 
 
-def _fma_to(a, b, c, dt):
-    """Correctly rounded fused multiply-add in dtype dt (via exact fp64)."""
-    return (a.astype(F64) * b.astype(F64) + c.astype(F64)).astype(dt)
+def _score_step(a, b, s, dt):
+    """score + a * b in the reference's arithmetic for dt: fp16 (c10::Half) a
+    product rounded to half, then the sum rounded to half (both exact in fp64
+    before their one rounding); fp32 one correctly rounded fused multiply-add."""
+    if dt == np.float16:
+        p = (a.astype(F64) * b.astype(F64)).astype(np.float16)
+        return (s.astype(F64) + p.astype(F64)).astype(np.float16)
+    return (a.astype(F64) * b.astype(F64) + s.astype(F64)).astype(dt)
 
 
 def refine_matches(D11, D21, p1, radius, dilation_max):
@@ -130,8 +143,9 @@ def refine_matches(D11, D21, p1, radius, dilation_max):
     b = np.repeat(np.arange(B), N)
     u0 = np.ascontiguousarray(p1, np.int64).reshape(-1, 2)[:, 0].copy()
     v0 = np.ascontiguousarray(p1, np.int64).reshape(-1, 2)[:, 1].copy()
-    min_pos = np.finfo(dt).tiny  # numeric_limits<T>::min(): smallest positive normal
-    best = np.full(u0.shape, min_pos, dt)
+    # numeric_limits<T>::min() (:47): c10::Half -> T() = 0; float -> FLT_MIN
+    start = 0.0 if dt == np.float16 else np.finfo(dt).tiny
+    best = np.full(u0.shape, start, dt)
     u_new, v_new = u0.copy(), v0.copy()
     for d in range(int(dilation_max), 0, -1):
         rd = radius * d
@@ -144,7 +158,7 @@ def refine_matches(D11, D21, p1, radius, dilation_max):
                 x = D11[b, np.clip(v, 0, H - 1), np.clip(u, 0, W - 1)]
                 s = np.zeros(u.shape, dt)
                 for k in range(Fd):
-                    s = _fma_to(D21[:, k], x[:, k], s, dt)
+                    s = _score_step(D21[:, k], x[:, k], s, dt)
                 upd = inside & (s > best)
                 best = np.where(upd, s, best)
                 u_new = np.where(upd, u, u_new)

@@ -101,7 +101,7 @@ def test_matching_rejects_bad_inputs():
 @pytest.mark.parametrize("F", [16, 24, 32])
 def test_refine_matches_f16_kernel_batches_and_far_centres(F):
     """refine_f16_kernel (round 5: XCD bands, zero-returning out-of-image
-    loads, pk-FMA chains): batched (a wave straddles the two batches: 37 x 53
+    loads; round 6: the reference's c10::Half chains): batched (a wave straddles the two batches: 37 x 53
     pixels is not a multiple of 64), centres near and past the borders and far
     outside (|p| up to 2^40: no candidate is inside, p is returned as is),
     F = 16 / 24 / 32; integer output equal to the oracle."""
@@ -121,3 +121,21 @@ def test_refine_matches_f16_kernel_batches_and_far_centres(F):
     out = out.cpu().numpy()
     assert np.array_equal(out, ref), (out != ref).any(-1).sum()
     assert np.array_equal(out[far], p[far])
+
+
+@pytest.mark.parametrize("F,radius", [(16, 3), (8, 1)])
+def test_refine_matches_subnormal_score_moves_centre(F, radius):
+    """Both refine kernels (refine_f16_kernel: F = 16, radius 3; refine_kernel:
+    F = 8, radius 1) start the running maximum at c10::Half's numeric_limits
+    min() as libcu++ leaves it, 0 (matching_kernels.cu:47): a candidate whose
+    c10::Half score is the smallest positive subnormal wins; every other
+    candidate scores 0 and the first-maximum rule keeps the planted one."""
+    H, W = 9, 11
+    D11 = torch.zeros(1, H, W, F, dtype=torch.float16)
+    D11[0, 6, 2, 0] = 2.0 ** -12
+    D21 = torch.zeros(1, 1, F, dtype=torch.float16)
+    D21[0, 0, 0] = 2.0 ** -12
+    p = np.array([[[3, 5]]], np.int64)
+    ref = mo.refine_matches(D11.numpy(), D21.numpy(), p, radius, 1)
+    (out,) = be.refine_matches(D11.to(DEV), D21.to(DEV), torch.from_numpy(p).to(DEV), radius, 1)
+    assert np.array_equal(ref, np.array([[[2, 6]]])) and np.array_equal(out.cpu().numpy(), ref)

@@ -63,3 +63,39 @@ def test_refine_keeps_centre_when_no_positive_score():
     D21 = np.ones((1, 2, 8), np.float16)
     p1 = np.array([[[1, 2], [3, 0]]], np.int64)
     assert np.array_equal(mo.refine_matches(D11, D21, p1, 1, 2), p1)
+
+
+def test_refine_score_chain_is_c10_half_arithmetic():
+    """The oracle's fp16 score step (a rounded product, then a rounded sum per
+    feature) is c10::Half's `score += a * b`, the reference kernel's arithmetic
+    for its .half() descriptors (matching_kernels.cu:58-60, :103): checked
+    bitwise against torch's own CPU Half tensors, whose operators are c10's
+    (compute in float, convert back). A fused multiply-add chain differs from
+    it on these inputs, so the test tells the two apart."""
+    g = torch.Generator().manual_seed(71)
+    n, fd = 4096, 24
+    a = F.normalize(torch.randn(n, fd, generator=g), dim=-1).half()
+    b = F.normalize(torch.randn(n, fd, generator=g), dim=-1).half()
+    s_t = torch.zeros(n, dtype=torch.float16)
+    s_o = np.zeros(n, np.float16)
+    s_f = np.zeros(n, np.float16)
+    for k in range(fd):
+        s_t = s_t + a[:, k] * b[:, k]
+        s_o = mo._score_step(a[:, k].numpy(), b[:, k].numpy(), s_o, np.float16)
+        s_f = (a[:, k].numpy().astype(np.float64) * b[:, k].numpy().astype(np.float64)
+               + s_f.astype(np.float64)).astype(np.float16)
+    assert np.array_equal(s_o.view(np.uint16), s_t.numpy().view(np.uint16))
+    assert not np.array_equal(s_f.view(np.uint16), s_t.numpy().view(np.uint16))
+
+
+def test_refine_tiny_positive_score_moves_the_centre():
+    """max_score starts at c10::Half's numeric_limits min() as libcu++ defines
+    it for an unspecialised type, T() = 0 (matching_kernels.cu:47): a
+    candidate whose score is a positive subnormal (below the smallest normal
+    half, 6.1e-5) still wins over the centre."""
+    D11 = np.zeros((1, 3, 3, 2), np.float16)
+    D11[0, 1, 2] = [np.float16(2.0 ** -12), 0]  # score 2^-12 * 2^-12 = 2^-24, the smallest subnormal
+    D21 = np.zeros((1, 1, 2), np.float16)
+    D21[0, 0] = [np.float16(2.0 ** -12), 0]
+    p1 = np.array([[[1, 1]]], np.int64)
+    assert np.array_equal(mo.refine_matches(D11, D21, p1, 1, 1), np.array([[[2, 1]]]))

@@ -56,3 +56,37 @@ if len(sys.argv) > 2:
     print(f"bench line: in-call avg_launch_ms {r['avg_launch_ms'] * 1e3:.2f} us, back_to_back_ms "
           f"{r['back_to_back_ms'] * 1e3:.2f} us; trace, the same calls: {ic:.2f} us "
           f"({(r['avg_launch_ms'] * 1e3 / ic - 1) * 100:+.1f}% bench vs trace)")
+
+# per drop-in call (round 6, verdict item 5): a call starts at its
+# gn_prologue_kernel; its kernels' summed durations against its wall span
+# (first kernel start -> last kernel end) and the idle gap before the next
+# call, for the C3 calls (10 solves each)
+calls, cur = [], None
+for s, e, n in seq:
+    if "gn_prologue_kernel" in n:
+        if cur:
+            calls.append(cur)
+        cur = []
+    if cur is not None:
+        cur.append((s, e, n))
+if cur:
+    calls.append(cur)
+c3 = [c for c in calls if sum("sparse_llt" in n for _, _, n in c) == 10]
+if c3:
+    busy = [sum(e - s for s, e, _ in c) / 1e3 for c in c3]
+    span = [(c[-1][1] - c[0][0]) / 1e3 for c in c3]
+    nxt = [(calls[calls.index(c) + 1][0][0] - c[-1][1]) / 1e3 for c in c3 if calls.index(c) + 1 < len(calls)]
+    print(f"C3 calls {len(c3)}: kernel time per call avg {statistics.mean(busy):8.1f} us (median "
+          f"{statistics.median(busy):.1f}), wall span {statistics.mean(span):8.1f} us, idle to next call median "
+          f"{statistics.median(nxt) if nxt else 0:.1f} us")
+    per = {}
+    for c in c3:
+        for s, e, n in c:
+            k = n.split("<")[0]
+            per.setdefault(k, []).append((e - s) / 1e3)
+    for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        print(f"  {k:28s} per call {sum(v) / len(c3):8.1f} us  ({len(v) / len(c3):.0f} launches, avg "
+              f"{statistics.mean(v):.2f} us)")
+    if len(sys.argv) > 2:
+        print(f"bench ms_per_step {b['ms_per_step'] * 1e3:.1f} us; roofline line spans x launches: "
+              f"{(r['gather_kernel']['avg_launch_ms'] + (b['config']['gn_iters_per_step'] - 1) * r['avg_launch_ms'] + b['config']['gn_iters_per_step'] * r['solve']['avg_ms']) * 1e3:.1f} us")

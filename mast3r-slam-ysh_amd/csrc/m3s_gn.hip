@@ -3266,81 +3266,18 @@ __device__ __forceinline__ bool tail_diag_mfma_t(f64x4 a, double (*Wk)[17], doub
   for (int r = 0; r < 4; r++) Wk[lk + 4 * r][lr] = M[r];
   return bad;
 }
-// Lane I's value to every lane of its 16-lane row (DPP row_newbcast, gfx90a+:
-// one v_mov_b64_dpp); I must fold to a constant (unrolled loops)
-template <int I>
-__device__ __forceinline__ double row_bcast_c(double v) {
-  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + I, 0xf, 0xf, false);
-}
-__device__ __forceinline__ double row_bcast(double v, int i) {
-  switch (i) {
-    case 0: return row_bcast_c<0>(v);
-    case 1: return row_bcast_c<1>(v);
-    case 2: return row_bcast_c<2>(v);
-    case 3: return row_bcast_c<3>(v);
-    case 4: return row_bcast_c<4>(v);
-    case 5: return row_bcast_c<5>(v);
-    case 6: return row_bcast_c<6>(v);
-    case 7: return row_bcast_c<7>(v);
-    case 8: return row_bcast_c<8>(v);
-    case 9: return row_bcast_c<9>(v);
-    case 10: return row_bcast_c<10>(v);
-    case 11: return row_bcast_c<11>(v);
-    case 12: return row_bcast_c<12>(v);
-    case 13: return row_bcast_c<13>(v);
-    case 14: return row_bcast_c<14>(v);
-    default: return row_bcast_c<15>(v);
-  }
-}
-
-// Full diagonal tile (jv == 16, round 6): a right-looking 16-column Cholesky
-// and W = L^-1 on the VALU with no LDS or MFMA on the chain. After one LDS
-// transpose every 16-lane row of the wave holds the tile by columns (lane c:
-// column c, which is row c of the symmetric tile; the four rows compute the
-// same, so any lane has what it needs). Step k: the pivot A(k,k) from lane k
-// by a DPP row broadcast, r = 1 / sqrt (rsqrt_nr), L(c,k) = A(k,c) r and
-// W(k,c) = R(k,c) r on every lane c, then for every row i > k the broadcast
-// L(i,k) updates A(i,c) -= L(i,k) L(c,k) and R(i,c) -= L(i,k) W(k,c) (R starts
-// as I: the forward substitution of L W = I, right-looking). One
-// v_mov_b64_dpp and two v_fma_f64 per (k, i): ~600 instructions with the
-// chain per column a broadcast, the rsqrt, a product and one update, where
-// the blocked MFMA form (tail_diag_mfma_t, kept for the partial last tile)
-// spent ~2.4 us per tile on four LDS round trips and dependent MFMAs. The
-// same arithmetic as the by-columns definition of L and W; another fp64
-// rounding order than the MFMA form (dx within fp64 round-off). Not inlined:
-// one copy of the code, warmed on a dummy tile while the workgroup waits for
-// its updates (tail_diag_warm).
-__device__ __noinline__ bool tail_diag_full(f64x4 a4, double (*Wk)[17], double *yv_k, int lane) {
-  (void)yv_k;
-  __shared__ double xt[16][17];
-  const int lr = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int r = 0; r < 4; r++) xt[lr][lk + 4 * r] = a4[r];  // entry (row lk + 4 r, column lr)
-  wave_lds_fence();
-  double a[16], R[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    a[i] = xt[lr][i];  // A(i, lr) = A(lr, i)
-    R[i] = i == lr ? 1.0 : 0.0;
-  }
-  bool bad = false;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const double d0 = row_bcast(a[k], k);
-    bad |= !(d0 > 0.0);
-    const double r = rsqrt_nr(d0 > 0.0 ? d0 : 1.0);
-    const double l = a[k] * r;  // lane c: L(c, k) for c >= k
-    const double w = R[k] * r;  // lane c: W(k, c)
-    if (lk == 0) Wk[k][lr] = w;
-#pragma unroll
-    for (int i = k + 1; i < 16; i++) {
-      const double li = row_bcast(l, i);  // L(i, k)
-      a[i] = __builtin_fma(-li, l, a[i]);
-      R[i] = __builtin_fma(-li, w, R[i]);
-    }
-  }
-  wave_lds_fence();  // Wk (LDS) written before the caller's reads
-  return bad;
+// Not inlined: each tail workgroup factors its diagonal tile(s) once, so the
+// ~600 instructions run from a cold instruction cache (measured ~2.5 us per
+// tile, ~4x the MFMA / LDS latencies it is made of). One copy of the code, run
+// once on a dummy tile while the workgroup waits for its updates
+// (tail_diag_warm), is then hot when the real tile arrives.
+// Round 6 measured a right-looking by-columns form on DPP row broadcasts
+// (v_mov_b64_dpp row_newbcast, no LDS or MFMA on the chain):
+// 8.7k cycles per hot call against 5.4k for this one
+// (profiles/r06/r6h_ubench_diag16.txt, tools/ubench_diag16.hip): a 64-bit
+// DPP broadcast feeding an FMA costs ~30 cycles, 120 of them per tile.
+__device__ __noinline__ bool tail_diag_full(f64x4 a, double (*Wk)[17], double *yv_k, int lane) {
+  return tail_diag_mfma_t<true>(a, Wk, yv_k, 16, -1, lane);
 }
 __device__ __noinline__ bool tail_diag_part(f64x4 a, double (*Wk)[17], double *yv_k, int jv, int rhs_row, int lane) {
   return tail_diag_mfma_t<false>(a, Wk, yv_k, jv, rhs_row, lane);

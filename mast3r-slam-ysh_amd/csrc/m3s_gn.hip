@@ -223,6 +223,7 @@ struct LinArgs {
   float *planes;           // per-edge target-side planes (PixIn), [E_loc][kPlanes][HW]
   float *partials;         // [task][36]
   uint32_t *edge_cnt;      // non-null: the last chunk of an edge to finish also finalizes it into fin
+  double *esum;            // non-null (stepwise API): that chunk writes the edge's fp64 sums here instead
   double *fin;             // [E][kFin] per-edge blocks M L M^T, M g (fused finalize)
   TrackState *track;       // tracker: the last chunk of an iteration runs the 7x7 solve (else null)
   int32_t *info;           // tracker outputs / convergence rule
@@ -585,6 +586,8 @@ __device__ __forceinline__ void store_partial(const float *acc, float *out) {
 // iterations and is zeroed per call) sums the edge's chunk partials in fp64
 // in chunk order with sc1 loads (the same sums as edge_reduce_kernel /
 // finalize_edges_kernel) and writes fin[e] - the finalize launch disappears.
+// Stepwise API (a sharded rank's range): the same chunk writes the 36 sums
+// to esum[e_loc] - the edge_reduce launch disappears (bitwise the same sums).
 __device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64_t e) {
   __shared__ double esl[kNP], Ms[7][7];
   __shared__ int last_s;
@@ -613,11 +616,15 @@ __device__ __forceinline__ void edge_tail(const LinArgs &A, int64_t e_loc, int64
     }
     for (; c < A.chunks; c++)
       acc += (double)__uint_as_float(__hip_atomic_load(p + (size_t)c * kNP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    esl[t] = acc;
-  } else if (t >= 64 && t < 64 + 49) {  // the second wave forms M under the first's loads
+    if (A.esum)
+      A.esum[(size_t)e_loc * kNP + t] = acc;
+    else
+      esl[t] = acc;
+  } else if (!A.esum && t >= 64 && t < 64 + 49) {  // the second wave forms M under the first's loads
     const int q = t - 64;
     Ms[q / 7][q % 7] = adjT_inv_entry(A.Twc + 8 * (size_t)A.rank_i[e], q / 7, q % 7);
   }
+  if (A.esum) return;
   __syncthreads();
   finalize_edge(esl, A.Twc + 8 * (size_t)A.rank_i[e], A.fin + (size_t)e * kFin, Ms);
 }
@@ -5023,6 +5030,11 @@ struct PlanMeta {
   int64_t range_b = -1, range_e = -1;  // the edge range last linearized
   bool order_ok = false;               // its edge order is in the workspace (Layout::eorder)
   bool planes_ok = false;
+  // stepwise linearize with fused edge sums: edge_cnt arrivals counted since
+  // the counters were last zeroed (valid for every edge of the range); false:
+  // the counters hold arrivals of another range or of a drop-in call
+  uint32_t cnt_arr = 0;
+  bool cnt_ok = true;
   std::vector<int32_t> eorder;         // host copy of the full range's order (host prepare)
   // the symbolic plan of this call is built by its first solve (cache miss at
   // prepare): the host analysis then overlaps the first linearize kernel
@@ -5158,8 +5170,11 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   L.planes = at<float>(ws, Ly.planes);
   L.eorder = nullptr;
   L.cnt_base = 0;
-  // fused finalize only over the whole edge set (single-GPU solve)
-  L.edge_cnt = (fuse_fin && eb == 0 && ee == a->E) ? at<uint32_t>(ws, Ly.edge_cnt) : nullptr;
+  // fused finalize only over the whole edge set (single-GPU solve); fused
+  // edge sums for the stepwise API (any range)
+  const bool fin_tail = fuse_fin && eb == 0 && ee == a->E;
+  L.edge_cnt = (fin_tail || edge_sums) ? at<uint32_t>(ws, Ly.edge_cnt) : nullptr;
+  L.esum = fin_tail ? nullptr : edge_sums;
   L.fin = at<double>(ws, Ly.fin);
   L.HW = a->HW;
   L.edge_begin = eb;
@@ -5186,6 +5201,7 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
     PlanMeta &M = it->second;
     if (M.range_b != eb || M.range_e != ee) {  // a sharded rank's own edge range
       M.range_b = eb, M.range_e = ee, M.planes_ok = false, M.order_ok = false;
+      if (M.cnt_arr) M.cnt_ok = false;
       if ((int64_t)M.rj.size() >= ee) {
         std::vector<int32_t> order;
         build_eorder(M.rj, eb, E_loc, order);
@@ -5211,13 +5227,23 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
       pack = M.planes_ok ? 2 : 1;
       M.planes_ok = true;
     }
+    // chunking: the gathering kernel's own (smaller chunks); the packed kernel
+    // counts its arrivals after the first iteration's (edge_tail)
+    const int64_t c_gather = chunks_for(a->HW, E_loc, kGatherBlocks);
+    L.chunks = pack == 2 ? chunks_for(a->HW, E_loc) : c_gather;
+    L.cnt_base = pack == 2 ? (uint32_t)c_gather : 0u;
+    if (fin_tail) {
+      M.cnt_ok = false;  // the drop-in call counts from its own prepare
+    } else if (L.esum) {
+      if (!M.cnt_ok) {  // stale arrivals: zero every counter (a few KB)
+        if (hipMemsetAsync(L.edge_cnt, 0, edge_cnt_bytes(a->E), st) != hipSuccess) return M3S_ELAUNCH;
+        M.cnt_arr = 0, M.cnt_ok = true;
+      }
+      L.cnt_base = M.cnt_arr;
+      M.cnt_arr += (uint32_t)L.chunks;
+    }
   }
-  // chunking: the gathering kernel's own (smaller chunks); the packed kernel
-  // counts its arrivals after the first iteration's (edge_tail)
-  const int64_t c_gather = chunks_for(a->HW, E_loc, kGatherBlocks);
-  L.chunks = pack == 2 ? chunks_for(a->HW, E_loc) : c_gather;
   L.chunk_pix = chunk_pixels(a->HW, L.chunks);
-  L.cnt_base = pack == 2 ? (uint32_t)c_gather : 0u;
   const int64_t T = E_loc * L.chunks;
   L.per = (T + 7) / 8;
   int64_t blocks = T;
@@ -5227,9 +5253,12 @@ int gn_linearize_impl(const m3s_gn_args *a, const ResidualParams &P, int64_t eb,
   }
   if (chunks_used) *chunks_used = L.chunks;
   int rc = dispatch_linearize<false>(a->mode, L, blocks, vec, pack, st);
-  if (rc || !edge_sums) return rc;  // NULL edge_sums: partials only (kernel timing)
-  edge_reduce_kernel<<<dim3((unsigned)E_loc), dim3(64), 0, st>>>(L.partials, L.chunks, edge_sums, L.stop);
-  return launch_ok();
+  if (rc && L.esum) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(ws);
+    if (it != g_reg.end()) it->second.cnt_ok = false;  // arrivals unknown
+  }
+  return rc;  // NULL edge_sums: partials only (kernel timing)
 }
 
 constexpr size_t kMaxLdsBytes = 150 * 1024;

@@ -69,15 +69,6 @@ constexpr int kTargetBlocks = M3S_TARGET_BLOCKS;  // linearize grid target (edge
 // random Xi reads then stay closer together in time per XCD (C3: 249 -> 232
 // us, 128 KFs rays: 1092 -> 1004 us; profiles/r03/tb_sweep_r3f.txt)
 constexpr int kGatherBlocks = M3S_GATHER_BLOCKS;
-// M3S_PK_RES_MB: the packed kernel loads the planes of a launch's first
-// edges, up to this many MB, with the default cache policy (they stay in the
-// 256-MB Infinity Cache across GN iterations, next to the ~100 MB of
-// pointmaps at C3), the rest non-temporal (round 6,
-// profiles/r06/r6r_pk_res*.txt: C3 calls 0.5-1.6 % shorter with 20-40 % of
-// the edges, i.e. 60-120 MB; 0: all non-temporal)
-#ifndef M3S_PK_RES_MB
-#define M3S_PK_RES_MB 96
-#endif
 #ifndef M3S_MAX_BLOCKS
 #define M3S_MAX_BLOCKS 8192
 #endif
@@ -865,8 +856,6 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Xs_j), 0, (int)(12 * HW), 0x00020000);
   const int vo_p = 16 * ln, vo_x = 48 * ln;
   const int pend = (int)p_end;
-  // the planes of the first M3S_PK_RES_MB of the launch: default cache policy
-  const bool res = (e_loc + 1) * NPL * HW * 4 <= ((int64_t)M3S_PK_RES_MB << 20);
   // pw: the wave's first pixel of a trip (wave-uniform); lane pixels pw + 4 ln
   auto issue = [&](int pw, int sl_) {
 #if defined(M3S_PK_FLOOR) && M3S_PK_FLOOR == 2  // compute floor (A/B only): no loads
@@ -892,15 +881,9 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? M3S_PK_WAVES_RAYS : M3S_
         buf_lds16_sc0(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vx, 12 * pw + 16 * k);
       return;
     }
-    if (M3S_PK_RES_MB > 0 && res) {
 #pragma unroll
-      for (int k = 0; k < NPL; k++)
-        buf_lds16(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vo_p, 4 * pw);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NPL; k++)
-        buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vo_p, 4 * pw);
-    }
+    for (int k = 0; k < NPL; k++)
+      buf_lds16_nt(Rp[k], (__attribute__((address_space(3))) void *)(&stage[sl_][wv][k][0]), vo_p, 4 * pw);
 #pragma unroll
     for (int k = 0; k < 3; k++)
       buf_lds16(Rx, (__attribute__((address_space(3))) void *)(&stage[sl_][wv][NPL + k][0]), vo_x, 12 * pw + 16 * k);
